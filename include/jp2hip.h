@@ -1,0 +1,146 @@
+/*
+ * jp2hip.h -- C ABI of libjp2hip, the MI355X (gfx950) JPEG 2000 encoder that
+ * replaces `kdu_compress` behind Bucketeer's converter plug-in API.
+ *
+ * Reference interfaces this ABI stands in for (paths relative to
+ * src/main/java/edu/ucla/library/bucketeer/ in UCLALibrary/jp2-bucketeer):
+ *
+ *   converters/Converter.java:22
+ *       File convert(String aID, File aTIFF, Conversion aConversion)
+ *           -> jp2hip_encode_file(): TIFF path in, JPX path out, blocking,
+ *              every failure reported as rc < 0 + jp2hip_last_error()
+ *              (the Java side turns that into IOException, like
+ *              AbstractConverter.java:33-35 does for a non-zero exit).
+ *   converters/Conversion.java:8-10          enum {LOSSY, LOSSLESS}
+ *           -> JP2HIP_LOSSY = 0, JP2HIP_LOSSLESS = 1 (same ordinals).
+ *   converters/KakaduConverter.java:38-44    BASE_OPTIONS + LOSSLESS_OPTIONS /
+ *                                            LOSSY_OPTION (the kdu recipe)
+ *           -> jp2hip_recipe / jp2hip_recipe_init().
+ *   converters/KakaduConverter.java:61-71    fork/exec of kdu_compress
+ *           -> in-process call; no child process.
+ *   converters/ConverterFactory.java:86-103  checkSystemKakadu() probe
+ *           -> jp2hip_probe() (a device with gfx950 is visible).
+ *
+ * All pointers are plain host pointers unless the name says d_ (device).
+ * Paths are UTF-8 bytes.  Calls on one context are serialised internally;
+ * different contexts (one per GPU) run concurrently.
+ */
+#ifndef JP2HIP_H
+#define JP2HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JP2HIP_LOSSY 0    /* Conversion.LOSSY    (Conversion.java:9)  */
+#define JP2HIP_LOSSLESS 1 /* Conversion.LOSSLESS (Conversion.java:9)  */
+
+#define JP2HIP_FORMAT_J2K 0 /* raw codestream                          */
+#define JP2HIP_FORMAT_JP2 1
+#define JP2HIP_FORMAT_JPX 2 /* what a ".jpx" output name asks Kakadu for */
+
+typedef struct jp2hip_ctx jp2hip_ctx;
+
+typedef struct jp2hip_config {
+    int32_t device;       /* HIP device ordinal                                */
+    int32_t host_threads; /* tier-2 worker threads (<=0: min(16, hw threads))  */
+    int32_t profile;      /* 1: record per-stage HIP event times in stats      */
+    int32_t reserved;
+} jp2hip_config;
+
+/* The kdu_compress recipe (KakaduConverter.java:38-44), field by field. */
+typedef struct jp2hip_recipe {
+    int32_t levels;          /* Clevels=6                                      */
+    int32_t layers;          /* Clayers=6                                      */
+    int32_t tile_w, tile_h;  /* Stiles={512,512}                               */
+    int32_t cblk_w_log2;     /* Cblk={64,64}                                   */
+    int32_t cblk_h_log2;
+    int32_t nprecincts;      /* Cprecincts={256,256},{256,256},{128,128}:     */
+    int32_t prec_w_log2[16]; /*   highest resolution first, last one repeats   */
+    int32_t prec_h_log2[16];
+    int32_t progression;     /* Corder=RPCL (2); the only order implemented    */
+    int32_t sop, eph;        /* Cuse_sop=yes Cuse_eph=yes                      */
+    int32_t plt;             /* ORGgen_plt=yes                                 */
+    int32_t tparts_r;        /* ORGtparts=R                                    */
+    int32_t guard_bits;      /* 1                                              */
+    int32_t reversible;      /* Creversible=yes -> 5/3 + RCT, else 9/7 + ICT   */
+    int32_t mct;             /* colour transform on components 0..2            */
+    double qstep;            /* irreversible base step (Kakadu Qstep=1/256)    */
+    double rate_bpp;         /* "-rate 3"; <= 0 means "-rate -" (all passes)   */
+    int32_t format;          /* JP2HIP_FORMAT_*                                */
+    int32_t comment;         /* emit a COM marker                              */
+} jp2hip_recipe;
+
+/* Where the samples live inside a source buffer (a baseline TIFF's strips). */
+typedef struct jp2hip_layout {
+    int32_t width, height, components, bits; /* bits 8 or 16, unsigned      */
+    int32_t planar;                          /* 1 chunky, 2 planar          */
+    int32_t big_endian;                      /* 16-bit sample byte order    */
+    int32_t rows_per_strip;
+    int32_t nstrips;                         /* entries in strip_offsets    */
+    const uint64_t *strip_offsets;           /* byte offset of each strip   */
+} jp2hip_layout;
+
+typedef struct jp2hip_stats {
+    double total_ms;      /* host wall time of the call                       */
+    double h2d_ms;        /* source upload (encode_file / encode_tiff only)   */
+    double ingest_ms;     /* strip gather + level shift + RCT/ICT kernel      */
+    double dwt_ms;        /* all DWT kernels                                  */
+    double quant_ms;      /* quantisation + bit-plane kernel                  */
+    double t1_ms;         /* EBCOT tier-1 kernel                              */
+    double pcrd_ms;       /* hull + threshold selection kernels               */
+    double d2h_ms;        /* metadata + compressed bytes download             */
+    double t2_ms;         /* host tier-2 / codestream assembly                */
+    int64_t codeblocks;
+    int64_t coded_passes;
+    int64_t t1_bytes;     /* MQ bytes produced by tier-1 (before truncation)  */
+    int64_t out_bytes;
+    int32_t rate_iterations;
+    int32_t reserved;
+} jp2hip_stats;
+
+const char *jp2hip_version(void);
+
+/* Thread-local message for the last failing call on this thread. */
+const char *jp2hip_last_error(void);
+
+/* 1 if a gfx950 device is usable (ConverterFactory.checkSystemKakadu analogue). */
+int jp2hip_probe(void);
+
+/* Fill the Bucketeer recipe for JP2HIP_LOSSY / JP2HIP_LOSSLESS. */
+void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion);
+
+int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg);
+void jp2hip_destroy(jp2hip_ctx *ctx);
+
+/* Converter.convert(): TIFF file -> JPEG 2000 file, written atomically
+ * (temp file + rename; nothing is left behind on failure).
+ * recipe == NULL -> jp2hip_recipe_init(conversion).  Returns 0 or < 0. */
+int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path_utf8, const char *out_path_utf8,
+                       int conversion, const jp2hip_recipe *recipe, jp2hip_stats *stats);
+
+/* TIFF bytes in host memory -> encoded bytes (*out malloc'd; jp2hip_free). */
+int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int conversion,
+                       const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
+                       jp2hip_stats *stats);
+
+/* Parse a baseline TIFF's header into a layout (offsets into the file). */
+int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout,
+                       uint64_t *offsets, int32_t max_offsets);
+
+/* Device-resident source: d_src holds the TIFF file (or any buffer the
+ * layout describes) in HBM.  This is the entry the benchmark times. */
+int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len,
+                         const jp2hip_layout *layout, int conversion,
+                         const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
+                         jp2hip_stats *stats);
+
+void jp2hip_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,400 @@
+// api.cpp -- the C ABI of libjp2hip (include/jp2hip.h).
+//
+// jp2hip_encode_file() is the in-process replacement for the kdu_compress
+// child process that KakaduConverter.convert() spawns
+// (KakaduConverter.java:55-77 -> AbstractConverter.run, AbstractConverter.java:29-39):
+// same inputs (TIFF path, output path, Conversion), same recipe, blocking,
+// and every failure surfaces as a negative return code plus a message,
+// never as a partially written output file.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <unistd.h>
+
+#include "gpu_encoder.h"
+#include "jp2hip.h"
+#include "jp2hip_internal.h"
+
+struct jp2hip_ctx {
+    std::mutex mu;
+    jp2hip::GpuEncoder gpu;
+    jp2hip_config cfg;
+    int threads = 1;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string &msg) {
+    g_err = msg;
+    return -1;
+}
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// ---- baseline TIFF header parsing (tags 256-339, classic TIFF only) ----
+struct TiffReader {
+    const uint8_t *b;
+    size_t n;
+    bool le;
+    uint32_t u16(size_t o) const {
+        if (o + 2 > n) return 0;
+        return le ? (uint32_t)(b[o] | (b[o + 1] << 8)) : (uint32_t)((b[o] << 8) | b[o + 1]);
+    }
+    uint32_t u32(size_t o) const {
+        if (o + 4 > n) return 0;
+        return le ? ((uint32_t)b[o] | ((uint32_t)b[o + 1] << 8) | ((uint32_t)b[o + 2] << 16) |
+                     ((uint32_t)b[o + 3] << 24))
+                  : (((uint32_t)b[o] << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) |
+                     (uint32_t)b[o + 3]);
+    }
+    uint32_t val(size_t e, uint32_t i) const {
+        uint32_t type = u16(e + 2), cnt = u32(e + 4);
+        uint32_t sz = type == 3 ? 2 : (type == 4 ? 4 : 1);
+        size_t base = (uint64_t)sz * cnt <= 4 ? e + 8 : u32(e + 8);
+        if (i >= cnt) return 0;
+        return sz == 2 ? u16(base + 2 * i) : (sz == 4 ? u32(base + 4 * i) : (base + i < n ? b[base + i] : 0));
+    }
+};
+
+int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<uint64_t> &offs) {
+    if (!buf || len < 8) return fail("tiff: input too short");
+    TiffReader t{buf, len, true};
+    if (buf[0] == 'I' && buf[1] == 'I') t.le = true;
+    else if (buf[0] == 'M' && buf[1] == 'M') t.le = false;
+    else return fail("tiff: bad byte-order mark");
+    if (t.u16(2) == 43) return fail("tiff: BigTIFF is not supported yet");
+    if (t.u16(2) != 42) return fail("tiff: not a TIFF file");
+    size_t ifd = t.u32(4);
+    if (ifd + 2 > len) return fail("tiff: IFD offset out of range");
+    uint32_t ne = t.u16(ifd);
+    uint32_t w = 0, h = 0, spp = 1, bps = 8, comp = 1, planar = 1, rps = 0xFFFFFFFFu, fmt = 1;
+    size_t e_off = 0, e_cnt = 0;
+    uint32_t n_off = 0;
+    for (uint32_t i = 0; i < ne; i++) {
+        size_t e = ifd + 2 + 12 * (size_t)i;
+        if (e + 12 > len) return fail("tiff: truncated IFD");
+        switch (t.u16(e)) {
+        case 256: w = t.val(e, 0); break;
+        case 257: h = t.val(e, 0); break;
+        case 258: bps = t.val(e, 0); break;
+        case 259: comp = t.val(e, 0); break;
+        case 273: e_off = e; n_off = t.u32(e + 4); break;
+        case 277: spp = t.val(e, 0); break;
+        case 278: rps = t.val(e, 0); break;
+        case 279: e_cnt = e; break;
+        case 284: planar = t.val(e, 0); break;
+        case 339: fmt = t.val(e, 0); break;
+        default: break;
+        }
+    }
+    if (!w || !h || !e_off) return fail("tiff: missing ImageWidth/ImageLength/StripOffsets");
+    if (comp != 1) return fail("tiff: compression " + std::to_string(comp) + " is not supported (uncompressed only)");
+    if (bps != 8 && bps != 16) return fail("tiff: " + std::to_string(bps) + " bits/sample is not supported");
+    if (fmt != 1) return fail("tiff: only unsigned integer samples are supported");
+    if (spp < 1 || spp > 4) return fail("tiff: " + std::to_string(spp) + " samples/pixel is not supported");
+    if (planar != 1 && planar != 2) return fail("tiff: bad PlanarConfiguration");
+    if (rps > h) rps = h;
+    uint32_t per_plane = (h + rps - 1) / rps;
+    uint32_t need = per_plane * (planar == 2 ? spp : 1);
+    if (n_off < need) return fail("tiff: too few strips");
+    offs.resize(need);
+    size_t row = (size_t)w * (planar == 2 ? 1 : spp) * (bps / 8);
+    for (uint32_t s = 0; s < need; s++) {
+        offs[s] = t.val(e_off, s);
+        uint32_t y0 = (s % per_plane) * rps;
+        uint32_t rows = std::min(rps, h - y0);
+        if (offs[s] + row * rows > len) return fail("tiff: strip " + std::to_string(s) + " out of range");
+        if (e_cnt && t.val(e_cnt, s) < row * rows) return fail("tiff: strip byte count too small");
+    }
+    lay->width = (int32_t)w;
+    lay->height = (int32_t)h;
+    lay->components = (int32_t)spp;
+    lay->bits = (int32_t)bps;
+    lay->planar = (int32_t)planar;
+    lay->big_endian = t.le ? 0 : 1;
+    lay->rows_per_strip = (int32_t)rps;
+    lay->nstrips = (int32_t)need;
+    lay->strip_offsets = offs.data();
+    return 0;
+}
+
+void default_recipe(jp2hip_recipe *r, int conversion) {
+    std::memset(r, 0, sizeof *r);
+    r->levels = 6;
+    r->layers = 6;
+    r->tile_w = r->tile_h = 512;
+    r->cblk_w_log2 = r->cblk_h_log2 = 6;
+    r->nprecincts = 3;
+    r->prec_w_log2[0] = r->prec_h_log2[0] = 8;
+    r->prec_w_log2[1] = r->prec_h_log2[1] = 8;
+    r->prec_w_log2[2] = r->prec_h_log2[2] = 7;
+    r->progression = 2;
+    r->sop = r->eph = r->plt = r->tparts_r = 1;
+    r->guard_bits = 1;
+    bool lossless = conversion == JP2HIP_LOSSLESS;
+    r->reversible = lossless ? 1 : 0;
+    r->mct = 1;
+    r->qstep = 1.0 / 256.0;
+    r->rate_bpp = lossless ? 0.0 : 3.0;
+    r->format = JP2HIP_FORMAT_JPX;
+    r->comment = 1;
+}
+
+// The whole encode with the source already in device memory.
+int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *lay,
+                int conversion, const jp2hip_recipe *recipe, std::vector<uint8_t> &file,
+                jp2hip_stats *stats, double t_start, double h2d_ms) {
+    using namespace jp2hip;
+    if (conversion != JP2HIP_LOSSY && conversion != JP2HIP_LOSSLESS)
+        return fail("conversion must be JP2HIP_LOSSY (0) or JP2HIP_LOSSLESS (1)");
+    jp2hip_recipe rc;
+    if (recipe) rc = *recipe;
+    else default_recipe(&rc, conversion);
+    if (!lay || !d_src) return fail("null source or layout");
+    (void)src_len;
+    Plan plan;
+    std::string err;
+    if (!build_plan(plan, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
+    const bool prof = ctx->cfg.profile != 0;
+    StageTimes st;
+    if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err)) return fail(err);
+    const int nb = (int)plan.blocks.size();
+    const int L = rc.layers;
+    const std::vector<int32_t> &len = ctx->gpu.block_lengths();
+    std::vector<uint8_t> h_nl;
+    std::vector<int32_t> h_lrate;
+    std::vector<int64_t> budgets((size_t)L, 0);
+    T2Input in;
+    in.plan = &plan;
+    in.P = ctx->gpu.block_planes().data();
+    in.data = nullptr;
+    in.data_off = nullptr;
+    in.threads = ctx->threads;
+    double t2ms = 0;
+    int iters = 0;
+    if (rc.rate_bpp <= 0.0) {
+        int64_t total = 0;
+        for (int b = 0; b < nb; b++) total += len[b];
+        for (int l = 0; l < L; l++) budgets[l] = total >> (L - 1 - l);
+        if (!ctx->gpu.select(plan, budgets, h_nl, h_lrate, prof, st, err)) return fail(err);
+        iters = 1;
+    } else {
+        const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
+        int64_t budget = target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
+        for (int it = 0; it < 8; it++) {
+            if (budget < 0) budget = 0;
+            for (int l = 0; l < L; l++) budgets[l] = budget >> (L - 1 - l);
+            if (!ctx->gpu.select(plan, budgets, h_nl, h_lrate, prof, st, err)) return fail(err);
+            iters++;
+            in.nl = h_nl.data();
+            in.lrate = h_lrate.data();
+            double t0 = now_ms();
+            int64_t size = t2_write(in, nullptr);
+            t2ms += now_ms() - t0;
+            if (size <= target) break;
+            budget -= (size - target) << it;  // exponential back-off, as the oracle
+        }
+    }
+    in.nl = h_nl.data();
+    in.lrate = h_lrate.data();
+    std::vector<int32_t> final_len((size_t)nb);
+    std::vector<uint64_t> offs((size_t)nb);
+    uint64_t total = 0;
+    for (int b = 0; b < nb; b++) {
+        final_len[b] = h_lrate[(size_t)b * L + (L - 1)];
+        offs[b] = total;
+        total += (uint64_t)final_len[b];
+    }
+    const uint8_t *data = nullptr;
+    double tg = now_ms();
+    if (!ctx->gpu.gather(plan, final_len, offs, total, &data, prof, st, err)) return fail(err);
+    double gather_ms = now_ms() - tg;
+    in.data = data;
+    in.data_off = offs.data();
+    double t0 = now_ms();
+    std::vector<uint8_t> cs;
+    t2_write(in, &cs);
+    wrap_file(plan, cs, file);
+    t2ms += now_ms() - t0;
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        stats->total_ms = now_ms() - t_start;
+        stats->h2d_ms = h2d_ms;
+        stats->ingest_ms = st.ingest;
+        stats->dwt_ms = st.dwt;
+        stats->quant_ms = st.quant;
+        stats->t1_ms = st.t1;
+        stats->pcrd_ms = st.pcrd;
+        stats->d2h_ms = prof ? st.d2h : gather_ms;
+        stats->t2_ms = t2ms;
+        stats->codeblocks = nb;
+        int64_t tb = 0, tp = 0;
+        ctx->gpu.t1_total_bytes(tb, tp);
+        stats->t1_bytes = tb;
+        stats->coded_passes = tp;
+        stats->out_bytes = (int64_t)file.size();
+        stats->rate_iterations = iters;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *jp2hip_version(void) { return "jp2hip 0.1.0 (gfx950)"; }
+
+const char *jp2hip_last_error(void) { return g_err.c_str(); }
+
+int jp2hip_probe(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
+    for (int i = 0; i < n; i++) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0)
+            return 1;
+    }
+    return 0;
+}
+
+void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
+    if (recipe) default_recipe(recipe, conversion);
+}
+
+int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg) {
+    if (!out) return fail("null output pointer");
+    *out = nullptr;
+    jp2hip_ctx *c = new (std::nothrow) jp2hip_ctx();
+    if (!c) return fail("out of memory");
+    std::memset(&c->cfg, 0, sizeof c->cfg);
+    if (cfg) c->cfg = *cfg;
+    int hw = (int)std::thread::hardware_concurrency();
+    c->threads = c->cfg.host_threads > 0 ? c->cfg.host_threads : std::max(1, std::min(16, hw));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        delete c;
+        return fail("no HIP device visible (libjp2hip needs an MI355X / gfx950)");
+    }
+    if (c->cfg.device < 0 || c->cfg.device >= ndev) {
+        delete c;
+        return fail("device ordinal out of range");
+    }
+    std::string err;
+    if (!c->gpu.init(c->cfg.device, err)) {
+        delete c;
+        return fail(err);
+    }
+    *out = c;
+    return 0;
+}
+
+void jp2hip_destroy(jp2hip_ctx *ctx) { delete ctx; }
+
+int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout, uint64_t *offsets,
+                       int32_t max_offsets) {
+    if (!layout) return fail("null layout");
+    std::vector<uint64_t> offs;
+    if (parse_tiff(tiff, len, layout, offs)) return -1;
+    if ((int32_t)offs.size() > max_offsets || !offsets) {
+        layout->strip_offsets = nullptr;
+        return fail("offsets array too small: need " + std::to_string(offs.size()));
+    }
+    std::memcpy(offsets, offs.data(), offs.size() * sizeof(uint64_t));
+    layout->strip_offsets = offsets;
+    return 0;
+}
+
+int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *layout,
+                         int conversion, const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
+                         jp2hip_stats *stats) {
+    if (!ctx || !out || !out_len) return fail("null argument");
+    *out = nullptr;
+    *out_len = 0;
+    double t0 = now_ms();
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<uint8_t> file;
+    if (encode_core(ctx, d_src, src_len, layout, conversion, recipe, file, stats, t0, 0.0)) return -1;
+    *out = (uint8_t *)std::malloc(file.size() ? file.size() : 1);
+    if (!*out) return fail("out of memory");
+    std::memcpy(*out, file.data(), file.size());
+    *out_len = file.size();
+    return 0;
+}
+
+int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int conversion,
+                       const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len, jp2hip_stats *stats) {
+    if (!ctx || !out || !out_len) return fail("null argument");
+    *out = nullptr;
+    *out_len = 0;
+    double t0 = now_ms();
+    jp2hip_layout lay;
+    std::vector<uint64_t> offs;
+    if (parse_tiff(tiff, len, &lay, offs)) return -1;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::string err;
+    double th = now_ms();
+    if (!ctx->gpu.upload_source(tiff, len, err)) return fail(err);
+    double h2d = now_ms() - th;
+    std::vector<uint8_t> file;
+    if (encode_core(ctx, ctx->gpu.source(), len, &lay, conversion, recipe, file, stats, t0, h2d)) return -1;
+    *out = (uint8_t *)std::malloc(file.size() ? file.size() : 1);
+    if (!*out) return fail("out of memory");
+    std::memcpy(*out, file.data(), file.size());
+    *out_len = file.size();
+    return 0;
+}
+
+int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path, const char *out_path, int conversion,
+                       const jp2hip_recipe *recipe, jp2hip_stats *stats) {
+    if (!ctx || !tiff_path || !out_path) return fail("null argument");
+    FILE *f = std::fopen(tiff_path, "rb");
+    if (!f) return fail(std::string("cannot open TIFF: ") + tiff_path);
+    std::vector<uint8_t> buf;
+    if (std::fseek(f, 0, SEEK_END) == 0) {
+        long n = std::ftell(f);
+        if (n > 0) {
+            buf.resize((size_t)n);
+            std::fseek(f, 0, SEEK_SET);
+            if (std::fread(buf.data(), 1, buf.size(), f) != buf.size()) buf.clear();
+        }
+    }
+    std::fclose(f);
+    if (buf.empty()) return fail(std::string("cannot read TIFF: ") + tiff_path);
+    uint8_t *out = nullptr;
+    size_t olen = 0;
+    if (jp2hip_encode_tiff(ctx, buf.data(), buf.size(), conversion, recipe, &out, &olen, stats)) return -1;
+    std::string tmp = std::string(out_path) + ".part-" + std::to_string((long)getpid()) + "-" +
+                      std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000);
+    FILE *o = std::fopen(tmp.c_str(), "wb");
+    if (!o) {
+        std::free(out);
+        return fail(std::string("cannot write output: ") + out_path);
+    }
+    bool ok = std::fwrite(out, 1, olen, o) == olen;
+    ok = (std::fclose(o) == 0) && ok;
+    std::free(out);
+    if (!ok || std::rename(tmp.c_str(), out_path) != 0) {
+        std::remove(tmp.c_str());
+        return fail(std::string("cannot write output: ") + out_path);
+    }
+    return 0;
+}
+
+void jp2hip_free(void *p) { std::free(p); }
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// gpu_encoder.h -- device side of one encode (buffers, stream, stage kernels).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "jp2hip_internal.h"
+
+namespace jp2hip {
+
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct StageTimes {
+    double ingest = 0, dwt = 0, quant = 0, t1 = 0, pcrd = 0, d2h = 0;
+};
+
+// Owns all device memory of a context; buffers only grow, so repeated
+// encodes of the same geometry never allocate.
+class GpuEncoder {
+  public:
+    ~GpuEncoder();
+    bool init(int device, std::string &err);
+
+    // host -> device copy of a source buffer into the internal `src` buffer
+    bool upload_source(const void *host, size_t len, std::string &err);
+    const void *source() const { return src.ptr; }
+
+    // ingest, DWT, quantiser, tier-1, hulls; downloads per-block totals
+    bool run_front(const void *d_src, const jp2hip_layout &lay, const Plan &plan, bool profile,
+                   StageTimes &st, std::string &err);
+    // layer thresholds for the given data budgets -> per-block layer tables
+    bool select(const Plan &plan, const std::vector<int64_t> &budgets, std::vector<uint8_t> &h_nl,
+                std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err);
+    // compact the included bytes of every block and download them
+    bool gather(const Plan &plan, const std::vector<int32_t> &final_len,
+                const std::vector<uint64_t> &offsets, uint64_t total, const uint8_t **host_data,
+                bool profile, StageTimes &st, std::string &err);
+
+    bool t1_total_bytes(int64_t &bytes, int64_t &passes) const;
+    const std::vector<int32_t> &block_lengths() const { return h_lengths; }
+    const std::vector<uint8_t> &block_passes() const { return h_npasses; }
+    const std::vector<uint8_t> &block_planes() const { return h_P; }
+    hipStream_t get_stream() const { return stream; }
+
+  private:
+    // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
+    bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
+    static constexpr int kNumEvents = 10;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[kNumEvents] = {};
+    DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
+        nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src;
+    uint8_t *h_packed = nullptr;
+    size_t h_packed_cap = 0;
+    std::vector<int32_t> h_lengths;
+    std::vector<uint8_t> h_npasses, h_P;
+};
+
+}  // namespace jp2hip

@@ -1,0 +1,102 @@
+// jp2hip_internal.h -- host-side model of one encode (geometry, quantiser,
+// code-block table) shared by the HIP launch code (kernels.hip), tier-2
+// (t2.cpp) and the C ABI (api.cpp).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "jp2hip.h"
+
+namespace jp2hip {
+
+constexpr int kMaxPasses = 96;    // 3*32-2 rounded up; per-block pass table stride
+constexpr int kMaxLayers = 32;
+constexpr int kMaxLevels = 12;
+
+// Per-band quantiser (Annex E).  For the reversible path eps follows the
+// 5/3 BIBO-gain rule that reproduces test.jpx's QCD.
+struct BandQuant {
+    int eps = 0, mu = 0, Mb = 0;
+    float inv_delta = 1.0f;
+    double wnorm = 1.0;  // Delta^2 * synthesis energy gain
+};
+
+BandQuant band_quant(const jp2hip_recipe &rc, int bits, int level, int band);
+
+// One code-block, as the kernels see it (uploaded as-is).
+struct BlockDesc {
+    int32_t tc;         // tile-component plane index
+    int16_t x0, y0;     // top-left inside the tile-component plane (Mallat layout)
+    int16_t w, h;       // <= 64
+    int8_t band;        // 0 LL, 1 HL, 2 LH, 3 HH
+    int8_t Mb;          // magnitude bit-planes of the band
+    int8_t pad0, pad1;
+    float inv_delta;    // irreversible quantiser reciprocal
+    uint32_t pad2;
+    uint64_t bp_off;    // bit-plane storage offset, in uint64 words
+    uint64_t sm_off;    // sign-magnitude storage offset, in int32 words
+    uint64_t out_off;   // tier-1 output offset, bytes
+    uint32_t out_cap;   // tier-1 output capacity, bytes
+    uint32_t pad3;
+};
+static_assert(sizeof(BlockDesc) == 56, "BlockDesc layout");
+
+struct PrecBand {
+    int ncw = 0, nch = 0;
+    int first = 0;  // index of the first block (raster order, contiguous)
+};
+struct Precinct {
+    PrecBand pb[3];
+    int nb = 0;
+};
+struct Resolution {
+    int npx = 0, npy = 0;
+    std::vector<Precinct> prec;
+};
+struct TileComp {
+    Resolution res[kMaxLevels + 1];
+};
+struct Tile {
+    int tx0, ty0, tx1, ty1;
+    std::vector<TileComp> tc;
+};
+
+struct Plan {
+    jp2hip_recipe rc;
+    int w = 0, h = 0, nc = 0, bits = 0;
+    int ntx = 0, nty = 0, ntc = 0;
+    int plane_w = 0, plane_h = 0;           // tile-component plane stride / rows
+    std::vector<Tile> tiles;
+    std::vector<BlockDesc> blocks;
+    std::vector<double> weight;             // PCRD weight per block
+    std::vector<int32_t> t1_order;          // lane -> block mapping for tier-1
+    std::vector<int32_t> tc_w, tc_h;        // tile-component sizes
+    uint64_t bp_words = 0, sm_words = 0, out_bytes = 0;
+    int64_t npackets = 0, ntileparts = 0;
+    double compw[4] = {1, 1, 1, 1};
+};
+
+bool build_plan(Plan &plan, const jp2hip_recipe &rc, int w, int h, int nc, int bits,
+                std::string &err);
+
+int prec_log2(const jp2hip_recipe &rc, int r, bool vertical);
+
+// Tier-2: writes the whole codestream (main header .. EOC).  `data` holds the
+// included bytes of every block back to back at `data_off[b]`.
+struct T2Input {
+    const Plan *plan;
+    const uint8_t *P;           // coded bit-planes per block
+    const uint8_t *nl;          // [block][layers] cumulative passes per layer
+    const int32_t *lrate;       // [block][layers] cumulative bytes per layer
+    const uint8_t *data;        // may be null for a size-only pass
+    const uint64_t *data_off;
+    int threads;
+};
+// returns total codestream size; fills out when out != nullptr
+int64_t t2_write(const T2Input &in, std::vector<uint8_t> *out);
+
+void wrap_file(const Plan &plan, const std::vector<uint8_t> &cs, std::vector<uint8_t> &file);
+
+}  // namespace jp2hip

@@ -1,0 +1,193 @@
+"""ctypes binding of libjp2hip (include/jp2hip.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C jp2-bucketeer_amd/csrc``) next to this file.  There is no fallback:
+if the library or a gfx950 device is missing, calls raise ``Jp2hipError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, byref, c_char_p, c_double, c_int, c_int32,
+                    c_int64, c_size_t, c_uint8, c_uint64, c_void_p)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libjp2hip.so")
+
+LOSSY = 0      # Conversion.LOSSY    (Conversion.java:9)
+LOSSLESS = 1   # Conversion.LOSSLESS (Conversion.java:9)
+FORMAT_J2K, FORMAT_JP2, FORMAT_JPX = 0, 1, 2
+
+
+class Jp2hipError(OSError):
+    """Raised for every libjp2hip failure (maps to IOException on the Java side)."""
+
+
+class Config(Structure):
+    _fields_ = [("device", c_int32), ("host_threads", c_int32), ("profile", c_int32),
+                ("reserved", c_int32)]
+
+
+class Recipe(Structure):
+    _fields_ = [("levels", c_int32), ("layers", c_int32), ("tile_w", c_int32), ("tile_h", c_int32),
+                ("cblk_w_log2", c_int32), ("cblk_h_log2", c_int32), ("nprecincts", c_int32),
+                ("prec_w_log2", c_int32 * 16), ("prec_h_log2", c_int32 * 16),
+                ("progression", c_int32), ("sop", c_int32), ("eph", c_int32), ("plt", c_int32),
+                ("tparts_r", c_int32), ("guard_bits", c_int32), ("reversible", c_int32),
+                ("mct", c_int32), ("qstep", c_double), ("rate_bpp", c_double),
+                ("format", c_int32), ("comment", c_int32)]
+
+
+class Layout(Structure):
+    _fields_ = [("width", c_int32), ("height", c_int32), ("components", c_int32),
+                ("bits", c_int32), ("planar", c_int32), ("big_endian", c_int32),
+                ("rows_per_strip", c_int32), ("nstrips", c_int32),
+                ("strip_offsets", POINTER(c_uint64))]
+
+
+class Stats(Structure):
+    _fields_ = [("total_ms", c_double), ("h2d_ms", c_double), ("ingest_ms", c_double),
+                ("dwt_ms", c_double), ("quant_ms", c_double), ("t1_ms", c_double),
+                ("pcrd_ms", c_double), ("d2h_ms", c_double), ("t2_ms", c_double),
+                ("codeblocks", c_int64), ("coded_passes", c_int64), ("t1_bytes", c_int64),
+                ("out_bytes", c_int64), ("rate_iterations", c_int32), ("reserved", c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+# every symbol include/jp2hip.h declares
+EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_recipe_init",
+           "jp2hip_create", "jp2hip_destroy", "jp2hip_encode_file", "jp2hip_encode_tiff",
+           "jp2hip_tiff_layout", "jp2hip_encode_device", "jp2hip_free")
+
+_lib = None
+
+
+def lib():
+    """Load libjp2hip.so once; raise if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise Jp2hipError(f"libjp2hip is not built ({LIB_PATH} missing); run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    L.jp2hip_version.restype = c_char_p
+    L.jp2hip_last_error.restype = c_char_p
+    L.jp2hip_probe.restype = c_int
+    L.jp2hip_recipe_init.argtypes = [POINTER(Recipe), c_int]
+    L.jp2hip_create.argtypes = [POINTER(c_void_p), POINTER(Config)]
+    L.jp2hip_destroy.argtypes = [c_void_p]
+    L.jp2hip_encode_file.argtypes = [c_void_p, c_char_p, c_char_p, c_int, POINTER(Recipe),
+                                     POINTER(Stats)]
+    L.jp2hip_encode_tiff.argtypes = [c_void_p, c_void_p, c_size_t, c_int, POINTER(Recipe),
+                                     POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(Stats)]
+    L.jp2hip_tiff_layout.argtypes = [c_void_p, c_size_t, POINTER(Layout), POINTER(c_uint64),
+                                     c_int32]
+    L.jp2hip_encode_device.argtypes = [c_void_p, c_void_p, c_size_t, POINTER(Layout), c_int,
+                                       POINTER(Recipe), POINTER(POINTER(c_uint8)),
+                                       POINTER(c_size_t), POINTER(Stats)]
+    L.jp2hip_free.argtypes = [c_void_p]
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return lib().jp2hip_last_error().decode("utf-8", "replace")
+
+
+def version() -> str:
+    return lib().jp2hip_version().decode()
+
+
+def probe() -> bool:
+    return bool(lib().jp2hip_probe())
+
+
+def recipe(conversion: int, **overrides) -> Recipe:
+    r = Recipe()
+    lib().jp2hip_recipe_init(byref(r), conversion)
+    for k, v in overrides.items():
+        if k in ("prec_w_log2", "prec_h_log2"):
+            arr = getattr(r, k)
+            for i, x in enumerate(v):
+                arr[i] = x
+        else:
+            setattr(r, k, v)
+    return r
+
+
+def tiff_layout(data: bytes):
+    """Parse a baseline TIFF header; returns (Layout, offsets array)."""
+    lay = Layout()
+    cap = 1 << 20
+    offs = (c_uint64 * cap)()
+    buf = ctypes.create_string_buffer(data, len(data))
+    if lib().jp2hip_tiff_layout(buf, len(data), byref(lay), offs, cap) != 0:
+        raise Jp2hipError(last_error())
+    n = lay.nstrips
+    keep = (c_uint64 * n)(*offs[:n])
+    lay.strip_offsets = ctypes.cast(keep, POINTER(c_uint64))
+    return lay, keep
+
+
+class Encoder:
+    """One libjp2hip context bound to one GPU (thread-safe, calls serialise)."""
+
+    def __init__(self, device: int = 0, host_threads: int = 0, profile: bool = False):
+        cfg = Config(device, host_threads, 1 if profile else 0, 0)
+        h = c_void_p()
+        if lib().jp2hip_create(byref(h), byref(cfg)) != 0:
+            raise Jp2hipError(last_error())
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().jp2hip_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _take(self, out, n):
+        try:
+            return ctypes.string_at(out, n.value)
+        finally:
+            lib().jp2hip_free(out)
+
+    def encode_tiff(self, data: bytes, conversion: int, rcp: Recipe | None = None):
+        out = POINTER(c_uint8)()
+        n = c_size_t()
+        st = Stats()
+        buf = ctypes.create_string_buffer(data, len(data))
+        rc = lib().jp2hip_encode_tiff(self._h, buf, len(data), conversion,
+                                      byref(rcp) if rcp is not None else None,
+                                      byref(out), byref(n), byref(st))
+        if rc != 0:
+            raise Jp2hipError(last_error())
+        return self._take(out, n), st
+
+    def encode_device(self, d_ptr: int, nbytes: int, layout: Layout, conversion: int,
+                      rcp: Recipe | None = None):
+        out = POINTER(c_uint8)()
+        n = c_size_t()
+        st = Stats()
+        rc = lib().jp2hip_encode_device(self._h, c_void_p(d_ptr), nbytes, byref(layout), conversion,
+                                        byref(rcp) if rcp is not None else None,
+                                        byref(out), byref(n), byref(st))
+        if rc != 0:
+            raise Jp2hipError(last_error())
+        return self._take(out, n), st
+
+    def encode_file(self, tiff_path: str, out_path: str, conversion: int,
+                    rcp: Recipe | None = None):
+        st = Stats()
+        rc = lib().jp2hip_encode_file(self._h, os.fsencode(tiff_path), os.fsencode(out_path),
+                                      conversion, byref(rcp) if rcp is not None else None,
+                                      byref(st))
+        if rc != 0:
+            raise Jp2hipError(last_error())
+        return st

@@ -1,0 +1,214 @@
+"""Host-side mirror of Bucketeer's converter plug-in API.
+
+Reference (src/main/java/edu/ucla/library/bucketeer/converters/):
+  Conversion.java:8-10        enum Conversion {LOSSY, LOSSLESS}
+  Converter.java:10-24        File convert(String aID, File aTIFF, Conversion)
+  KakaduConverter.java:26-128 kdu_compress wrapper (recipe :38-44, output name :57,
+                              KAKADU_HOME :111-128)
+  OpenJPEGConverter.java:9-27 stub, convert() returns null
+  ConverterFactory.java:20-103 getConverter(), getConverter(Class), checkSystemKakadu()
+
+``GpuConverter`` is the new plug-in: same contract as KakaduConverter.convert
+(blocking, output ``<tmp>/<workdir>/<urlencoded id>.jpx`` owned by the caller,
+every failure an ``IOError`` carrying the BUCKETEER-001 text), but the encode
+runs in-process on MI355X through libjp2hip instead of a kdu_compress child.
+"""
+from __future__ import annotations
+
+import enum
+import os
+import shutil
+import subprocess
+import tempfile
+import threading
+import urllib.parse
+from pathlib import Path
+
+from . import _lib
+
+# bucketeer_messages.xml:12  BUCKETEER-001 "Failed to convert TIFF to JP2: {}"
+BUCKETEER_001 = "Failed to convert TIFF to JP2: {}"
+# BUCKETEER-002 (KakaduConverter.getPath, :97-103)
+BUCKETEER_002 = "Output directory is not writable: {}"
+# BUCKETEER-032 (ConverterFactory.getConverter(Class), :70)
+BUCKETEER_032 = "No known converter"
+
+
+class Conversion(enum.IntEnum):
+    """Conversion.java:8-10 (ordinals kept: LOSSY=0, LOSSLESS=1)."""
+    LOSSY = _lib.LOSSY
+    LOSSLESS = _lib.LOSSLESS
+
+
+class KakaduNotFoundError(RuntimeError):
+    """KakaduNotFoundException (an unchecked I18nRuntimeException in the reference)."""
+
+
+class Converter:
+    """Converter.java:10-24."""
+
+    def convert(self, image_id: str, tiff: os.PathLike | str, conversion: Conversion) -> Path:
+        raise NotImplementedError
+
+
+def _jpx_name(image_id: str) -> str:
+    # URLEncoder.encode(aID, UTF-8) + ".jpx"   (KakaduConverter.java:57)
+    return urllib.parse.quote_plus(image_id, safe="*-._") + ".jpx"
+
+
+class KakaduConverter(Converter):
+    """Mirror of KakaduConverter.java: shells out to kdu_compress with the recipe."""
+
+    WORKING_DIR_NAME = "kakadu"
+    KAKADU_HOME = "KAKADU_HOME"
+    BASE_OPTIONS = ["Clevels=6", "Clayers=6", "Cprecincts={256,256},{256,256},{128,128}",
+                    "Stiles={512,512}", "Corder=RPCL", "ORGgen_plt=yes", "ORGtparts=R",
+                    "Cblk={64,64}", "Cuse_sop=yes", "Cuse_eph=yes", "-flush_period", "1024"]
+    LOSSLESS_OPTIONS = ["Creversible=yes", "-rate", "-"]
+    LOSSY_OPTION = ["-rate", "3"]
+
+    def __init__(self):
+        self.tmp_dir = Path(tempfile.gettempdir()) / self.WORKING_DIR_NAME
+        self.tmp_dir.mkdir(parents=True, exist_ok=True)
+
+    @classmethod
+    def get_executable(cls) -> str:
+        home = os.environ.get(cls.KAKADU_HOME)
+        return str(Path(home) / "kdu_compress") if home else "kdu_compress"
+
+    def convert(self, image_id, tiff, conversion):
+        jpx = self.tmp_dir / _jpx_name(image_id)
+        cmd = [self.get_executable(), "-i", str(Path(tiff).absolute()), "-o", str(jpx)]
+        cmd += self.BASE_OPTIONS
+        cmd += self.LOSSLESS_OPTIONS if conversion == Conversion.LOSSLESS else self.LOSSY_OPTION
+        if not ConverterFactory.has_system_kakadu():
+            raise KakaduNotFoundError("Kakadu not found")
+        proc = subprocess.run(cmd, capture_output=True)
+        if proc.returncode != 0:
+            raise IOError(BUCKETEER_001.format(image_id))
+        return jpx
+
+
+class OpenJPEGConverter(Converter):
+    """OpenJPEGConverter.java:9-27 -- the reference's stub; convert() returns None."""
+
+    def convert(self, image_id, tiff, conversion):
+        return None
+
+
+class GpuConverter(Converter):
+    """MI355X converter: libjp2hip in-process, one context per visible GPU.
+
+    Safe for concurrent callers (the reference runs one ImageWorkerVerticle
+    thread, MainVerticle.java:229-231; raising that count gives each call its
+    own GPU context from the pool).
+    """
+
+    WORKING_DIR_NAME = "jp2hip"
+
+    def __init__(self, devices: list[int] | None = None, host_threads: int = 0):
+        self.tmp_dir = Path(tempfile.gettempdir()) / self.WORKING_DIR_NAME
+        try:
+            self.tmp_dir.mkdir(parents=True, exist_ok=True)
+        except OSError as e:  # KakaduConverter.java:48-52 throws BUCKETEER_163 here
+            raise IOError(BUCKETEER_002.format(self.tmp_dir)) from e
+        if devices is None:
+            devices = [0]
+        self._pool = [_lib.Encoder(d, host_threads) for d in devices]
+        self._free = list(self._pool)
+        self._cv = threading.Condition()
+
+    def _acquire(self):
+        with self._cv:
+            while not self._free:
+                self._cv.wait()
+            return self._free.pop()
+
+    def _release(self, enc):
+        with self._cv:
+            self._free.append(enc)
+            self._cv.notify()
+
+    def convert(self, image_id, tiff, conversion):
+        tiff = Path(tiff)
+        jpx = self.tmp_dir / _jpx_name(image_id)
+        if not os.access(jpx.parent, os.W_OK):
+            raise IOError(BUCKETEER_002.format(jpx))
+        enc = self._acquire()
+        try:
+            enc.encode_file(str(tiff.absolute()), str(jpx), int(Conversion(conversion)))
+        except (_lib.Jp2hipError, ValueError) as e:
+            raise IOError(BUCKETEER_001.format(image_id) + f": {e}") from e
+        finally:
+            self._release(enc)
+        return jpx
+
+    def close(self):
+        for e in self._pool:
+            e.close()
+
+
+class ConverterFactory:
+    """ConverterFactory.java:20-103, plus the GPU branch."""
+
+    _converter: Converter | None = None
+    _has_kakadu = False
+    _lock = threading.Lock()
+
+    @classmethod
+    def get_converter(cls, klass: type | None = None) -> Converter:
+        with cls._lock:
+            if klass is None:
+                if cls._converter is None:
+                    if cls.check_system_gpu():
+                        cls._converter = GpuConverter()
+                    elif cls.check_system_kakadu():
+                        cls._converter = KakaduConverter()
+                    else:
+                        cls._converter = OpenJPEGConverter()
+                return cls._converter
+            if klass is KakaduConverter:
+                if not cls.check_system_kakadu():
+                    raise KakaduNotFoundError("Kakadu not found")
+                cls._converter = KakaduConverter()
+            elif klass is OpenJPEGConverter:
+                cls._converter = OpenJPEGConverter()
+            elif klass is GpuConverter:
+                if not cls.check_system_gpu():
+                    raise IOError(BUCKETEER_001.format("(no gfx950 device)"))
+                if not isinstance(cls._converter, GpuConverter):
+                    cls._converter = GpuConverter()
+            else:
+                raise ValueError(BUCKETEER_032)
+            return cls._converter
+
+    @classmethod
+    def has_system_kakadu(cls) -> bool:
+        return cls._has_kakadu
+
+    @classmethod
+    def check_system_kakadu(cls) -> bool:
+        """`kdu_compress -v` exit status (ConverterFactory.java:86-103)."""
+        exe = KakaduConverter.get_executable()
+        ok = False
+        if shutil.which(exe) or os.path.exists(exe):
+            try:
+                ok = subprocess.run([exe, "-v"], capture_output=True).returncode == 0
+            except OSError:
+                ok = False
+        cls._has_kakadu = ok
+        return ok
+
+    @classmethod
+    def check_system_gpu(cls) -> bool:
+        try:
+            return _lib.probe()
+        except _lib.Jp2hipError:
+            return False
+
+    @classmethod
+    def reset(cls):
+        with cls._lock:
+            if isinstance(cls._converter, GpuConverter):
+                cls._converter.close()
+            cls._converter = None

@@ -1198,7 +1198,7 @@ static void write_main_header(encoder *E, bytes *o) {
         else bput16(o, (q.eps << 11) | q.mu);
     }
     if (rc->comment) {
-        static const char msg[] = "jp2hip oracle";
+        static const char msg[] = "jp2hip";
         bput16(o, 0xFF64);
         bput16(o, 4 + (int)strlen(msg));
         bput16(o, 1);
@@ -1449,7 +1449,7 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
             cs.n = 0;
             write_codestream(&E, &cs);
             if ((int64_t)cs.n <= target) break;
-            budget -= (int64_t)cs.n - target;
+            budget -= ((int64_t)cs.n - target) << it; /* exponential back-off */
         }
     }
     free(S);

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/golden.json (run in the build container).
+
+Sources of truth, none of them part of the product:
+  * tests/golden/test.jpx -- byte copy of the reference's only image fixture,
+    src/test/resources/images/test.jpx (Kakadu 7.10.6 output of the lossless
+    recipe, KakaduConverter.java:38-44).  We record its
+    main-header segments, packet/tile-part structure and the SHA-256 of its
+    decoded pixels (opj_decompress 2.4.0 and Pillow/OpenJPEG 2.5.4 agree).
+  * opj_compress 2.4.0 (/opt/conda/bin) -- the CPU reference encoder that
+    north_star names when Kakadu is unlicensed -- run with the Appendix A
+    mapping of the recipe, to pin the lossy yardstick: PSNR at a given bpp.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import imaging as im  # noqa: E402
+
+PREC = "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]"
+
+
+def opj_encode(img: np.ndarray, ratios: str, lossy: bool, levels=6, tile=512) -> bytes:
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.tif"), os.path.join(d, "out.j2k")
+        with open(src, "wb") as f:
+            f.write(im.tiff_bytes(img))
+        prec = ",".join(["[256,256]", "[256,256]"] + ["[128,128]"] * (levels - 1))
+        cmd = [im.opj("opj_compress"), "-i", src, "-o", dst, "-n", str(levels + 1), "-t", f"{tile},{tile}",
+               "-b", "64,64", "-p", "RPCL", "-SOP", "-EPH", "-PLT", "-TP", "R", "-c", prec, "-r", ratios]
+        if lossy:
+            cmd.insert(1, "-I")
+        subprocess.run(cmd, check=True, capture_output=True)
+        return open(dst, "rb").read()
+
+
+def opj_psnr_at(img, bits, target_bytes, levels=6):
+    """opj lossy PSNR with the final layer sized to `target_bytes` (same bpp)."""
+    raw_bits = img.size * bits
+    r = raw_bits / (8.0 * target_bytes)
+    ratios = ",".join(f"{r * 2 ** k:.4f}" for k in range(5, -1, -1))
+    cs = opj_encode(img, ratios, True, levels)
+    dec = im.decode_opj(cs, ".j2k")
+    return len(cs), im.psnr(img, dec, bits)
+
+
+def main():
+    g = {}
+    tj = open(os.path.join(HERE, "test.jpx"), "rb").read()
+    pix = im.decode_opj(tj, ".j2k")
+    pil = im.decode_pillow(tj)
+    assert np.array_equal(pix, pil)
+    seg = im.main_header_segments(tj)
+    g["testjpx"] = {
+        "size": len(tj),
+        "shape": list(pix.shape),
+        "sha256": im.sha256(pix),
+        "siz": seg["ff51"].hex(), "cod": seg["ff52"].hex(), "qcd": seg["ff5c"].hex(),
+        "sop": im.count_marker(tj, b"\xff\x91"),
+        "tileparts": len(im.tile_parts(tj)),
+        "tp_order": [[t[0], t[2]] for t in im.tile_parts(tj)][:16],
+        "min_size_assert": 30000,   # KakaduConverterTest.java:107
+    }
+    # lossy yardsticks: opj at exactly the oracle's output size
+    sys.path.insert(0, os.path.dirname(HERE))
+    import oracle_lib as ol
+    cases = []
+    for name, img, bits, lv in [
+        ("synth_rgb8_1024x1536", im.synth_rgb8(1024, 1536, seed=1234), 8, 6),
+        ("testjpx_rgb_crop_1024", pix[:1024, :1024, :3].copy(), 8, 6),
+        ("synth_gray16_1024", im.synth_u16(1024, 1024, comps=1, seed=5), 16, 7),
+    ]:
+        rc = ol.recipe(False, levels=lv, format=0)
+        cs = ol.encode(img, rc)
+        dec = im.decode_opj(cs, ".j2k")
+        ps = im.psnr(img, dec, bits)
+        n_opj, ps_opj = opj_psnr_at(img, bits, len(cs), lv)
+        cases.append({"name": name, "bits": bits, "levels": lv, "oracle_bytes": len(cs),
+                      "oracle_psnr": round(ps, 4), "opj_bytes": n_opj, "opj_psnr": round(ps_opj, 4),
+                      "bpp": round(8.0 * len(cs) / (img.shape[0] * img.shape[1]), 5)})
+        print(cases[-1])
+    g["lossy"] = cases
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(g, f, indent=1)
+    print(json.dumps(g["testjpx"], indent=1))
+
+
+if __name__ == "__main__":
+    main()

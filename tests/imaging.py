@@ -1,0 +1,241 @@
+"""Test helpers: synthetic images, a baseline TIFF writer, decoders, PSNR.
+
+Decoding uses OpenJPEG (opj_decompress from /opt/conda/bin, or Pillow's bundled
+OpenJPEG) -- the "reference decoder" north_star names for parity; nothing here
+is part of the product.
+"""
+from __future__ import annotations
+
+import hashlib
+import io
+import os
+import shutil
+import struct
+import subprocess
+import tempfile
+
+import numpy as np
+
+OPJ_DIR = "/opt/conda/bin"
+
+
+def opj(tool: str) -> str | None:
+    p = os.path.join(OPJ_DIR, tool)
+    if os.path.exists(p):
+        return p
+    return shutil.which(tool)
+
+
+def synth_rgb8(h, w, seed=1234, noise=6.0):
+    """C2-style content: sinusoids + checker patch + gaussian noise."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.zeros((h, w, 3))
+    for c in range(3):
+        img[..., c] = 128 + 40 * np.sin(x / 37.0 + c) + 30 * np.cos(y / 23.0 - c) + 20 * np.sin((x + y) / 11.0)
+    ys, xs = slice(h // 5, 2 * h // 5), slice(w // 5, 7 * w // 15)
+    chk = 50 * ((np.floor(x[ys, xs] / 16) + np.floor(y[ys, xs] / 16)) % 2 - 0.5)
+    img[ys, xs, :] += chk[..., None]
+    img += rng.normal(0, noise, img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def synth_u16(h, w, comps=3, seed=2):
+    """C3/C5-style 16-bit content scaled to [0, 65535] plus N(0, 400)."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    out = np.zeros((h, w, comps))
+    for c in range(comps):
+        out[..., c] = 32768 + 12000 * np.sin(x / 53.0 + c) + 9000 * np.cos(y / 31.0 - 2 * c) + \
+            6000 * np.sin((x - y) / 17.0)
+    out += rng.normal(0, 400, out.shape)
+    out = np.clip(out, 0, 65535).astype(np.uint16)
+    return out if comps > 1 else out[..., 0]
+
+
+def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=False,
+               alpha=None) -> bytes:
+    """Uncompressed baseline TIFF (strips), 8/16-bit, 1-4 samples."""
+    if img.ndim == 2:
+        img = img[..., None]
+    h, w, nc = img.shape
+    bits = img.dtype.itemsize * 8
+    e = ">" if big_endian else "<"
+    rps = min(rows_per_strip, h)
+    nstrip = (h + rps - 1) // rps
+    planes = [img[..., c] for c in range(nc)] if planar else [img]
+    strips = []
+    for pl in planes:
+        for s in range(nstrip):
+            blk = np.ascontiguousarray(pl[s * rps:(s + 1) * rps])
+            strips.append(blk.astype(blk.dtype.newbyteorder(e)).tobytes())
+    ntags = 11 + (1 if nc in (2, 4) else 0)
+    ifd_off = 8
+    ifd_size = 2 + 12 * ntags + 4
+    extra = bytearray()
+    extra_base = ifd_off + ifd_size
+
+    def arr(vals, typ):
+        nonlocal extra
+        off = extra_base + len(extra)
+        fmt = "H" if typ == 3 else "I"
+        extra += struct.pack(e + fmt * len(vals), *vals)
+        if len(extra) % 2:
+            extra += b"\0"
+        return off
+
+    data_base_placeholder = []
+    nst = len(strips)
+    bps_off = arr([bits] * nc, 3) if nc > 2 else None
+    so_off = arr([0] * nst, 4) if nst > 1 else None
+    sbc_off = arr([len(s) for s in strips], 4) if nst > 1 else None
+    data_base = extra_base + len(extra)
+    offs = []
+    pos = data_base
+    for s in strips:
+        offs.append(pos)
+        pos += len(s)
+    if nst > 1:
+        extra[so_off - extra_base:so_off - extra_base + 4 * nst] = struct.pack(e + "I" * nst, *offs)
+    tags = []
+
+    def tag(t, typ, cnt, val_or_off, inline=True):
+        if inline and typ == 3 and cnt == 1:
+            v = struct.pack(e + "HH", val_or_off, 0)
+        elif inline and typ == 3 and cnt == 2:
+            v = struct.pack(e + "HH", *val_or_off)
+        else:
+            v = struct.pack(e + "I", val_or_off)
+        tags.append((t, struct.pack(e + "HHI", t, typ, cnt) + v))
+
+    tag(256, 4, 1, w)
+    tag(257, 4, 1, h)
+    if nc == 1:
+        tag(258, 3, 1, bits)
+    elif nc == 2:
+        tag(258, 3, 2, (bits, bits))
+    else:
+        tag(258, 3, nc, bps_off, inline=False)
+    tag(259, 3, 1, 1)
+    tag(262, 3, 1, 2 if nc >= 3 else 1)
+    tag(273, 4, nst, offs[0] if nst == 1 else so_off, inline=(nst == 1))
+    tag(277, 3, 1, nc)
+    tag(278, 4, 1, rps)
+    tag(279, 4, nst, len(strips[0]) if nst == 1 else sbc_off, inline=(nst == 1))
+    tag(284, 3, 1, 2 if planar else 1)
+    if nc in (2, 4):
+        tag(338, 3, 1, 2 if alpha is None else alpha)
+    tag(339, 3, 1, 1)
+    tags.sort(key=lambda t: t[0])
+    assert len(tags) == ntags
+    hdr = (b"MM\0*" if big_endian else b"II*\0") + struct.pack(e + "I", ifd_off)
+    ifd = struct.pack(e + "H", ntags) + b"".join(t[1] for t in tags) + struct.pack(e + "I", 0)
+    del data_base_placeholder
+    return hdr + ifd + bytes(extra) + b"".join(strips)
+
+
+def decode_opj(data: bytes, ext=".jpx") -> np.ndarray:
+    """Decode with opj_decompress (exact for 16-bit RGB, unlike Pillow)."""
+    tool = opj("opj_decompress")
+    if tool is None:
+        raise RuntimeError("opj_decompress not available")
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "in" + (".jp2" if ext in (".jpx", ".jp2") else ".j2k"))
+        dst = os.path.join(d, "out.tif")
+        with open(src, "wb") as f:
+            f.write(data)
+        r = subprocess.run([tool, "-i", src, "-o", dst], capture_output=True)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr.decode() + r.stdout.decode())
+        return read_tiff(open(dst, "rb").read())
+
+
+def read_tiff(data: bytes) -> np.ndarray:
+    """Minimal TIFF reader for opj_decompress output (uncompressed strips)."""
+    le = data[:2] == b"II"
+    e = "<" if le else ">"
+    ifd = struct.unpack(e + "I", data[4:8])[0]
+    n = struct.unpack(e + "H", data[ifd:ifd + 2])[0]
+    tags = {}
+    for i in range(n):
+        t, typ, cnt, val = struct.unpack(e + "HHI4s", data[ifd + 2 + 12 * i: ifd + 14 + 12 * i])
+        sz = {3: 2, 4: 4, 1: 1}.get(typ, 1)
+        fmt = {3: "H", 4: "I", 1: "B"}.get(typ, "B")
+        if sz * cnt <= 4:
+            vals = struct.unpack(e + fmt * cnt, val[:sz * cnt])
+        else:
+            off = struct.unpack(e + "I", val)[0]
+            vals = struct.unpack(e + fmt * cnt, data[off:off + sz * cnt])
+        tags[t] = vals
+    w, h = tags[256][0], tags[257][0]
+    bits = tags[258][0]
+    spp = tags.get(277, (1,))[0]
+    planar = tags.get(284, (1,))[0]
+    assert tags.get(259, (1,))[0] == 1
+    dt = np.dtype(np.uint8 if bits == 8 else np.uint16).newbyteorder(e)
+    raw = b"".join(data[o:o + c] for o, c in zip(tags[273], tags[279]))
+    a = np.frombuffer(raw, dtype=dt).astype(dt.newbyteorder("="))
+    if planar == 2:
+        a = a.reshape(spp, h, w).transpose(1, 2, 0)
+    else:
+        a = a.reshape(h, w, spp)
+    return a if spp > 1 else a[..., 0]
+
+
+def decode_pillow(data: bytes) -> np.ndarray:
+    from PIL import Image
+    return np.array(Image.open(io.BytesIO(data)))
+
+
+def psnr(a: np.ndarray, b: np.ndarray, bits=8) -> float:
+    mse = np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)
+    peak = (1 << bits) - 1
+    return float("inf") if mse == 0 else 10 * np.log10(peak * peak / mse)
+
+
+def sha256(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def markers(cs: bytes):
+    """(offset, marker) list of the main header + the count of SOP/SOT/PLT markers."""
+    i = cs.find(b"\xff\x4f")
+    return i
+
+
+def main_header_segments(cs: bytes) -> dict:
+    """SIZ/COD/QCD segment bytes of a J2K codestream (possibly inside a JP2/JPX)."""
+    i = cs.find(b"\xff\x4f\xff\x51")
+    assert i >= 0, "no SOC+SIZ"
+    out = {}
+    p = i + 2
+    while True:
+        m = cs[p:p + 2]
+        if m == b"\xff\x90":
+            break
+        L = struct.unpack(">H", cs[p + 2:p + 4])[0]
+        out.setdefault(m.hex(), cs[p:p + 2 + L])
+        p += 2 + L
+    return out
+
+
+def codestream(data: bytes) -> bytes:
+    i = data.find(b"\xff\x4f\xff\x51")
+    return data[i:]
+
+
+def count_marker(cs: bytes, marker: bytes) -> int:
+    return cs.count(marker)
+
+
+def tile_parts(cs: bytes):
+    """Walk SOT markers: list of (Isot, Psot, TPsot, TNsot)."""
+    out = []
+    p = cs.find(b"\xff\x90")
+    while p >= 0 and cs[p:p + 2] == b"\xff\x90":
+        isot, psot, tp, tn = struct.unpack(">HIBB", cs[p + 4:p + 12])
+        out.append((isot, psot, tp, tn))
+        if psot == 0:
+            break
+        p += psot
+    return out

@@ -1,0 +1,145 @@
+"""The C-ABI boundary (include/jp2hip.h) and the converter API mirror, on CPU.
+
+No compute calls here: only that libjp2hip loads, exports every declared
+symbol, parses TIFF headers, exposes the Kakadu recipe, and that the Python
+mirror of converters/* behaves like the reference when no GPU / Kakadu exists.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import imaging as im
+import jp2hip
+from jp2hip import _lib
+from jp2hip.converters import (Conversion, ConverterFactory, GpuConverter, KakaduConverter,
+                               KakaduNotFoundError, OpenJPEGConverter, _jpx_name)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "jp2hip.h")).read()
+    return sorted(set(re.findall(r"\b(jp2hip_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_declares_what_the_binding_expects():
+    assert _declared_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for sym in _declared_symbols():
+        assert hasattr(L, sym), sym
+
+
+def test_version_and_probe():
+    assert "gfx950" in jp2hip.version()
+    assert jp2hip.probe() in (True, False)
+
+
+def test_recipe_is_the_kakadu_recipe():
+    # KakaduConverter.java:38-44
+    for conv, lossless in ((jp2hip.LOSSLESS, True), (jp2hip.LOSSY, False)):
+        r = jp2hip.recipe(conv)
+        assert (r.levels, r.layers, r.tile_w, r.tile_h) == (6, 6, 512, 512)
+        assert (r.cblk_w_log2, r.cblk_h_log2) == (6, 6)
+        assert r.nprecincts == 3 and list(r.prec_w_log2[:3]) == [8, 8, 7]
+        assert (r.progression, r.sop, r.eph, r.plt, r.tparts_r) == (2, 1, 1, 1, 1)
+        assert r.reversible == (1 if lossless else 0)
+        assert r.rate_bpp == (0.0 if lossless else 3.0)
+        assert r.format == jp2hip.FORMAT_JPX
+
+
+def test_recipe_identical_to_oracle_recipe():
+    import oracle_lib as ol
+    for conv in (jp2hip.LOSSLESS, jp2hip.LOSSY):
+        a = jp2hip.recipe(conv)
+        b = ol.recipe(conv == jp2hip.LOSSLESS)
+        for name, _ in _lib.Recipe._fields_:
+            va, vb = getattr(a, name), getattr(b, name)
+            if name.startswith("prec_"):
+                assert list(va) == list(vb)
+            else:
+                assert va == vb, name
+
+
+@pytest.mark.parametrize("kw", [{}, {"planar": True}, {"big_endian": True}, {"rows_per_strip": 3}])
+def test_tiff_layout(kw):
+    img = im.synth_rgb8(37, 53, seed=1)
+    data = im.tiff_bytes(img, **kw)
+    lay, offs = jp2hip.tiff_layout(data)
+    assert (lay.width, lay.height, lay.components, lay.bits) == (53, 37, 3, 8)
+    assert lay.planar == (2 if kw.get("planar") else 1)
+    assert lay.big_endian == (1 if kw.get("big_endian") else 0)
+    rps = kw.get("rows_per_strip", 64)
+    assert lay.rows_per_strip == min(rps, 37)
+    # strip 0 holds row 0
+    o = offs[0]
+    if not kw.get("planar"):
+        assert data[o:o + 3] == img[0, 0].tobytes()
+
+
+def test_tiff_layout_16bit():
+    img = im.synth_u16(20, 30, comps=1)
+    lay, offs = jp2hip.tiff_layout(im.tiff_bytes(img, big_endian=True))
+    assert (lay.bits, lay.components, lay.big_endian) == (16, 1, 1)
+
+
+@pytest.mark.parametrize("bad,msg", [(b"XX*\0" + b"\0" * 16, "byte-order"),
+                                     (b"II+\0" + b"\0" * 16, "BigTIFF"),
+                                     (b"II*\0", "short")])
+def test_tiff_layout_rejects(bad, msg):
+    with pytest.raises(jp2hip.Jp2hipError, match=msg):
+        jp2hip.tiff_layout(bad)
+
+
+def test_tiff_layout_rejects_compressed():
+    data = bytearray(im.tiff_bytes(im.synth_rgb8(8, 8)))
+    # Compression tag (259) value -> 5 (LZW)
+    i = data.find(bytes([0x03, 0x01, 0x03, 0x00, 0x01, 0x00, 0x00, 0x00, 0x01, 0x00]))
+    assert i > 0
+    data[i + 8] = 5
+    with pytest.raises(jp2hip.Jp2hipError, match="compression 5"):
+        jp2hip.tiff_layout(bytes(data))
+
+
+def test_conversion_ordinals_match_reference():
+    assert int(Conversion.LOSSY) == 0 and int(Conversion.LOSSLESS) == 1
+
+
+def test_jpx_name_is_url_encoded():
+    # KakaduConverter.java:57 URLEncoder.encode(id, UTF-8) + ".jpx"
+    assert _jpx_name("ark:/21198/zz0019pp86") == "ark%3A%2F21198%2Fzz0019pp86.jpx"
+    assert _jpx_name("a b") == "a+b.jpx"
+    assert _jpx_name("熵") == "%E7%86%B5.jpx"
+
+
+def test_kakadu_executable_honours_kakadu_home(monkeypatch):
+    # KakaduConverterTest.testGetExecutable (KakaduConverterTest.java:77-87)
+    monkeypatch.setenv("KAKADU_HOME", "/opt/kakadu")
+    assert KakaduConverter.get_executable() == "/opt/kakadu/kdu_compress"
+    monkeypatch.delenv("KAKADU_HOME")
+    assert KakaduConverter.get_executable() == "kdu_compress"
+
+
+@pytest.mark.skipif(jp2hip.probe(), reason="factory fallback is only observable without a GPU")
+def test_factory_without_gpu_or_kakadu(monkeypatch):
+    monkeypatch.delenv("KAKADU_HOME", raising=False)
+    ConverterFactory.reset()
+    assert isinstance(ConverterFactory.get_converter(), OpenJPEGConverter)
+    assert ConverterFactory.get_converter(OpenJPEGConverter).convert("x", "y.tif", Conversion.LOSSLESS) is None
+    with pytest.raises(KakaduNotFoundError):
+        ConverterFactory.get_converter(KakaduConverter)
+    with pytest.raises(IOError):
+        ConverterFactory.get_converter(GpuConverter)
+    with pytest.raises(ValueError):
+        ConverterFactory.get_converter(str)
+    ConverterFactory.reset()
+
+
+@pytest.mark.skipif(jp2hip.probe(), reason="needs a machine without a GPU")
+def test_encoder_fails_loudly_without_gpu():
+    with pytest.raises(jp2hip.Jp2hipError, match="no HIP device"):
+        jp2hip.Encoder(0)
