@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark: encoded megapixels/s of the MI355X JPEG 2000 path (libjp2hip).
+
+Workload (BASELINE.json configs[1], "C2"): a 6000x4000 8-bit RGB TIFF,
+lossy 9/7 at 3 bpp with the Bucketeer/Kakadu recipe (6 levels, 6 layers, 512^2
+tiles, 64^2 blocks, RPCL, SOP/EPH/PLT, tile-parts per resolution), JPX out.
+One step = one full encode of one image per GPU: TIFF strips already resident
+in HBM -> JPX bytes in host memory (ingest, DWT, quantiser, tier-1, PCRD,
+tier-2).  Images are independent, so N GPUs run N replicas (weak scaling,
+no collective on the data path); the barrier/max are only for timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "jp2-bucketeer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "encoded megapixels/sec (node), lossless 5/3 + lossy 9/7, at 1/2/4/8 MI355X"
+HBM_PEAK = 8.0e12  # MI355X_MICROARCH.md chip table (spec)
+
+
+def dwt_bytes_per_px(C, s, L):
+    """B_dwt = C*[s + 4 + (8/3)(1 - 4^-(L-1))]."""
+    return C * (s + 4 + (8.0 / 3.0) * (1 - 4.0 ** (-(L - 1))))
+
+
+def make_image(kind: str, seed: int):
+    import imaging as im
+    if kind == "c2":
+        return im.synth_rgb8(4000, 6000, seed=seed)
+    if kind == "c3":
+        return im.synth_u16(8000, 10000, comps=3, seed=seed)
+    raise ValueError(kind)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("JP2HIP_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend=backend)
+    return world, rank, local
+
+
+def barrier_max(world, value, device):
+    """Barrier + max over ranks (RCCL all-reduce of one float)."""
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def cpu_baseline_oracle(img, budget_s=20.0):
+    """The oracle (plain C, 1 thread) on a bounded crop of the same workload."""
+    import oracle_lib as ol
+    crop = np.ascontiguousarray(img[:1024, :2048])
+    rc = ol.recipe(False)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        ol.encode(crop, rc)
+        n += 1
+        if time.perf_counter() - t0 > min(budget_s, 3.0) or n >= 4:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * crop.shape[0] * crop.shape[1] / 1e6 / dt, 4), "unit": "MP/s",
+            "cores": 1, "kind": "port",
+            "sample": f"{n}x encode of a 1024x2048 crop of the C2 image, lossy 9/7 3 bpp, oracle/jp2_oracle.c single thread"}
+
+
+def cpu_converter_opj(img, nproc):
+    """north_star's CPU reference converter: opj_compress (Kakadu is absent),
+    `nproc` concurrent single-image processes with the Appendix A recipe."""
+    import imaging as im
+    tool = im.opj("opj_compress")
+    if tool is None:
+        return None
+    crop = np.ascontiguousarray(img[:2048, :2048])
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "in.tif")
+        open(src, "wb").write(im.tiff_bytes(crop))
+        cmd = [tool, "-i", src, "-I", "-n", "7", "-t", "512,512", "-b", "64,64", "-p", "RPCL", "-SOP",
+               "-EPH", "-PLT", "-TP", "R", "-c",
+               "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]",
+               "-r", "256,128,64,32,16,8"]
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen(cmd + ["-o", os.path.join(d, f"o{i}.j2k")], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL) for i in range(nproc)]
+        ok = all(p.wait() == 0 for p in ps)
+        dt = time.perf_counter() - t0
+    if not ok:
+        return None
+    mp = nproc * crop.shape[0] * crop.shape[1] / 1e6
+    return {"tool": "opj_compress 2.4.0", "value": round(mp / dt, 3), "unit": "MP/s", "processes": nproc,
+            "sample": "2048x2048 crop of the C2 image per process, lossy 3 bpp, Appendix A recipe"}
+
+
+def run(args):
+    import torch  # device memory + distributed plumbing only
+
+    import jp2hip
+    import imaging as im
+
+    world, rank, local = dist_setup(args.gpus)
+    device = f"cuda:{local}"
+    torch.cuda.set_device(local)
+    img = make_image("c2", seed=1234 + rank)
+    tif = im.tiff_bytes(img, rows_per_strip=64)
+    lay, offs = jp2hip.tiff_layout(tif)
+    d_src = torch.frombuffer(bytearray(tif), dtype=torch.uint8).to(device)
+    torch.cuda.synchronize()
+    enc = jp2hip.Encoder(local, profile=True)
+    rc = jp2hip.recipe(jp2hip.LOSSY)
+    out = None
+    for _ in range(args.warmup):
+        out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
+    barrier(world)
+    torch.cuda.synchronize()
+    stages = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
+        stages.append(st.as_dict())
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt_max = barrier_max(world, dt, device)
+    mp = img.shape[0] * img.shape[1] / 1e6
+    value = world * mp * args.steps / dt_max
+    res = None
+    if rank == 0:
+        avg = {k: float(np.mean([s[k] for s in stages])) for k in stages[0]}
+        kern = {"k_t1": avg["t1_ms"], "k_dwt": avg["dwt_ms"], "k_quant": avg["quant_ms"],
+                "k_ingest": avg["ingest_ms"], "k_pcrd": avg["pcrd_ms"]}
+        dom = max(kern, key=kern.get)
+        C, L = 3, 6
+        npx = img.shape[0] * img.shape[1]
+        # algorithmic bytes per launch (DESIGN.md "Roofline"):
+        #   tier-1 reads one int32 coefficient per sample and writes the MQ bytes
+        #   DWT per SURVEY.md 8(d) B_dwt
+        t1_alg = 4 * C * npx + avg["t1_bytes"]
+        dwt_alg = dwt_bytes_per_px(C, 1, L) * npx
+        alg = {"k_t1": t1_alg, "k_dwt": dwt_alg, "k_quant": 4 * C * npx * 2,
+               "k_ingest": (C + 4 * C) * npx, "k_pcrd": 0}
+        ach = alg[dom] / (kern[dom] * 1e-3) / 1e9
+        res = {
+            "metric": METRIC, "value": round(value, 3), "unit": "MP/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+i32",
+            "data": "synthetic (sinusoids + checker + N(0,6) noise, seed 1234+rank), in-memory baseline TIFF",
+            "config": {"workload": "C2: 6000x4000 RGB8 TIFF -> JPX, lossy 9/7 3 bpp, Kakadu recipe "
+                                   "(6 levels, 6 layers, 512^2 tiles, 64^2 blocks, RPCL, SOP/EPH/PLT, TP=R)",
+                       "image": "6000x4000x3 u8", "per_gpu_images_per_step": 1,
+                       "parallelism": f"replicas x{world}", "out_bytes": int(avg["out_bytes"]),
+                       "bpp": round(8 * avg["out_bytes"] / npx, 4)},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2),
+                         "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": round(ach * 1e9 / HBM_PEAK, 5), "traffic": None,
+                         "avg_launch_ms": round(kern[dom], 4)},
+            "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
+                             "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                             "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
+                             "alg_bytes_per_px": round(dwt_bytes_per_px(C, 1, L), 3),
+                             "stage_ms": round(avg["dwt_ms"], 4)},
+            "stages_ms": {k: round(avg[k], 4) for k in ("ingest_ms", "dwt_ms", "quant_ms", "t1_ms",
+                                                        "pcrd_ms", "d2h_ms", "t2_ms", "total_ms")},
+            "t1": {"codeblocks": int(avg["codeblocks"]), "coded_passes": int(avg["coded_passes"]),
+                   "mq_bytes": int(avg["t1_bytes"])},
+        }
+    return res, img, world, rank, enc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lossless", action="store_true")
+    args = ap.parse_args()
+    res, img, world, rank, enc = run(args)
+    if rank == 0 and world == 1:
+        if not args.no_lossless:
+            res["lossless_c3"] = lossless_c3(enc)
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_oracle(img)
+            nproc = min(16, os.cpu_count() or 1)
+            res["cpu_converter"] = cpu_converter_opj(img, nproc)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def lossless_c3(enc, steps=2):
+    """C3 (configs[2]): 10000x8000 RGB16 lossless 5/3, 1024^2 tiles -- reported beside."""
+    import torch
+
+    import jp2hip
+    import imaging as im
+    img = make_image("c3", seed=2)
+    tif = im.tiff_bytes(img, rows_per_strip=64)
+    lay, offs = jp2hip.tiff_layout(tif)
+    d_src = torch.frombuffer(bytearray(tif), dtype=torch.uint8).cuda()
+    rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
+    out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)
+    dt = (time.perf_counter() - t0) / steps
+    npx = img.shape[0] * img.shape[1]
+    return {"workload": "C3: 10000x8000 RGB16 lossless 5/3, 1024^2 tiles", "mp_per_s": round(npx / 1e6 / dt, 3),
+            "ms": round(dt * 1e3, 2), "bpp": round(8 * len(out) / npx, 4), "t1_ms": round(st.t1_ms, 3),
+            "dwt_ms": round(st.dwt_ms, 3)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+"""GPU parity: libjp2hip (through the C ABI) against the CPU oracle.
+
+Bit-exact is the bar for both conversions: the integer path (5/3, RCT, tier-1,
+tier-2) is deterministic, and the 9/7 / ICT path is computed in fp32 with the
+oracle's operation order and no FMA contraction, so the whole code-stream must
+match byte for byte.  Lossless output must also decode (OpenJPEG) to the
+source pixels; lossy quality is pinned through the oracle's opj yardstick
+(tests/golden/golden.json).
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import imaging as im
+import jp2hip
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+
+def _img(h, w, nc, bits, seed):
+    if bits == 16:
+        return im.synth_u16(h, w, comps=nc, seed=seed)
+    a = im.synth_rgb8(h, w, seed=seed)
+    if nc == 1:
+        return a[..., 0].copy()
+    if nc == 2:
+        return np.dstack([a[..., 0], a[..., 2]])
+    if nc == 4:
+        return np.dstack([a, (a[..., 1] // 3 + 40).astype(np.uint8)])
+    return a
+
+
+CASES = [
+    # h, w, nc, bits, lossless, levels, tile
+    (200, 300, 3, 8, True, 6, 512),
+    (200, 300, 3, 8, False, 6, 512),
+    (1, 1, 3, 8, True, 6, 512),
+    (3, 130, 1, 8, False, 6, 512),
+    (130, 3, 1, 8, True, 6, 512),
+    (517, 1030, 3, 8, True, 6, 512),
+    (517, 1030, 3, 8, False, 6, 512),
+    (300, 260, 4, 8, True, 6, 512),
+    (300, 260, 4, 8, False, 6, 512),
+    (257, 333, 2, 8, True, 5, 256),
+    (700, 900, 3, 16, True, 6, 1024),
+    (700, 900, 3, 16, False, 6, 512),
+    (600, 777, 1, 16, False, 7, 512),
+    (600, 777, 1, 16, True, 7, 512),
+    (150, 250, 3, 8, True, 0, 512),
+    (450, 350, 3, 8, False, 2, 128),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}_{c[3]}b_{'ll' if c[4] else 'ly'}_L{c[5]}_T{c[6]}"
+                                             for c in CASES])
+def test_codestream_identical_to_oracle(encoder, case):
+    h, w, nc, bits, lossless, levels, tile = case
+    img = _img(h, w, nc, bits, seed=h * 7 + w)
+    conv = jp2hip.LOSSLESS if lossless else jp2hip.LOSSY
+    rc = jp2hip.recipe(conv, levels=levels, tile_w=tile, tile_h=tile)
+    got, st = encoder.encode_tiff(im.tiff_bytes(img), conv, rc)
+    want = ol.encode(img, ol.copy_recipe(rc))
+    assert got == want
+    if lossless:
+        assert np.array_equal(im.decode_opj(got), img)
+
+
+def test_testjpx_pixels_lossless(encoder, testjpx_pixels, golden):
+    """C1: the reference fixture's pixels through the GPU converter path."""
+    rc = jp2hip.recipe(jp2hip.LOSSLESS, format=jp2hip.FORMAT_J2K)
+    got, st = encoder.encode_tiff(im.tiff_bytes(testjpx_pixels), jp2hip.LOSSLESS, rc)
+    assert got == ol.encode(testjpx_pixels, ol.copy_recipe(rc))
+    g = golden["testjpx"]
+    seg = im.main_header_segments(got)
+    assert (seg["ff51"].hex(), seg["ff52"].hex(), seg["ff5c"].hex()) == (g["siz"], g["cod"], g["qcd"])
+    assert im.count_marker(got, b"\xff\x91") == g["sop"]
+    assert len(im.tile_parts(got)) == g["tileparts"]
+    assert np.array_equal(im.decode_pillow(got), testjpx_pixels)
+    assert len(got) > g["min_size_assert"]
+
+
+@pytest.mark.parametrize("case", [0, 2])
+def test_golden_lossy_cases(encoder, golden, case):
+    c = golden["lossy"][case]
+    img = im.synth_rgb8(1024, 1536, seed=1234) if case == 0 else im.synth_u16(1024, 1024, comps=1, seed=5)
+    rc = jp2hip.recipe(jp2hip.LOSSY, levels=c["levels"], format=jp2hip.FORMAT_J2K)
+    got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSY, rc)
+    assert len(got) == c["oracle_bytes"]
+    dec = im.decode_opj(got, ".j2k")
+    ps = im.psnr(img, dec, c["bits"])
+    assert abs(ps - c["oracle_psnr"]) < 1e-3
+    assert ps >= c["opj_psnr"] - 0.1
+
+
+def test_c2_full_size_identical_and_on_rate(encoder):
+    """C2 at full size: 6000x4000 RGB8 lossy 3 bpp."""
+    img = im.synth_rgb8(4000, 6000, seed=1234)
+    rc = jp2hip.recipe(jp2hip.LOSSY)
+    got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSY, rc)
+    cs = im.codestream(got)
+    assert len(cs) <= 3.0 * 6000 * 4000 / 8
+    assert len(cs) >= 0.97 * 3.0 * 6000 * 4000 / 8
+    assert got == ol.encode(img, ol.copy_recipe(rc))
+    assert im.psnr(img, im.decode_pillow(got)) > 30
+
+
+def test_c3_full_size_lossless_roundtrip(encoder):
+    """C3 at full size: 10000x8000 RGB16 lossless, 1024^2 tiles -> decode exact."""
+    img = im.synth_u16(8000, 10000, comps=3, seed=2)
+    rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
+    got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSLESS, rc)
+    assert np.array_equal(im.decode_opj(got), img)
+
+
+def test_deterministic_and_reusable_context(encoder):
+    img = _img(333, 444, 3, 8, seed=9)
+    tif = im.tiff_bytes(img)
+    a, _ = encoder.encode_tiff(tif, jp2hip.LOSSY)
+    big = im.tiff_bytes(_img(900, 1300, 3, 8, seed=10))
+    encoder.encode_tiff(big, jp2hip.LOSSLESS)
+    b, _ = encoder.encode_tiff(tif, jp2hip.LOSSY)
+    assert a == b
+
+
+def test_tiff_variants_same_output(encoder):
+    img = _img(190, 270, 3, 8, seed=4)
+    ref, _ = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSLESS)
+    for kw in ({"planar": True}, {"big_endian": True}, {"rows_per_strip": 1}, {"rows_per_strip": 190}):
+        got, _ = encoder.encode_tiff(im.tiff_bytes(img, **kw), jp2hip.LOSSLESS)
+        assert got == ref, kw
+    g16 = _img(190, 270, 1, 16, seed=5)
+    a, _ = encoder.encode_tiff(im.tiff_bytes(g16), jp2hip.LOSSLESS)
+    b, _ = encoder.encode_tiff(im.tiff_bytes(g16, big_endian=True), jp2hip.LOSSLESS)
+    assert a == b
+
+
+def test_encode_file_atomic(encoder, tmp_path):
+    img = _img(120, 160, 3, 8, seed=6)
+    src = tmp_path / "in.tif"
+    src.write_bytes(im.tiff_bytes(img))
+    out = tmp_path / "out.jpx"
+    encoder.encode_file(str(src), str(out), jp2hip.LOSSLESS)
+    assert np.array_equal(im.decode_pillow(out.read_bytes()), img)
+    bad = tmp_path / "bad.tif"
+    bad.write_bytes(b"II*\0garbage")
+    out2 = tmp_path / "never.jpx"
+    with pytest.raises(jp2hip.Jp2hipError):
+        encoder.encode_file(str(bad), str(out2), jp2hip.LOSSLESS)
+    assert not out2.exists()
+    assert not any(p.name.startswith("never.jpx") for p in tmp_path.iterdir())
+
+
+def test_gpu_converter_like_kakadu_converter_test(tmp_path, testjpx_pixels):
+    """Mirror of KakaduConverterTest.testConvert (KakaduConverterTest.java:96-115)."""
+    from jp2hip.converters import Conversion, ConverterFactory, GpuConverter
+    tif = tmp_path / "test.tif"
+    tif.write_bytes(im.tiff_bytes(testjpx_pixels))
+    conv = ConverterFactory.get_converter(GpuConverter)
+    for image_id in ("ark:/21198/zz0019pp86", "熵"):
+        jpx = conv.convert(image_id, tif, Conversion.LOSSLESS)
+        assert jpx.exists() and jpx.name.endswith(".jpx")
+        assert jpx.stat().st_size > 30000
+        assert np.array_equal(im.decode_pillow(jpx.read_bytes()), testjpx_pixels)
+        jpx.unlink()
+    with pytest.raises(IOError, match="Failed to convert TIFF to JP2"):
+        conv.convert("missing", tmp_path / "nope.tif", Conversion.LOSSY)
+    ConverterFactory.reset()
+
+
+def test_concurrent_callers(tmp_path):
+    from jp2hip.converters import Conversion, GpuConverter
+    conv = GpuConverter(devices=[0, 0])
+    imgs = [_img(200 + 37 * i, 300, 3, 8, seed=i) for i in range(4)]
+    paths = []
+    for i, a in enumerate(imgs):
+        p = tmp_path / f"in{i}.tif"
+        p.write_bytes(im.tiff_bytes(a))
+        paths.append(p)
+    results = {}
+
+    def work(i):
+        results[i] = conv.convert(f"id{i}", paths[i], Conversion.LOSSLESS).read_bytes()
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i, a in enumerate(imgs):
+        assert np.array_equal(im.decode_pillow(results[i]), a)
+    conv.close()
