@@ -90,7 +90,7 @@ typedef struct jp2hip_stats {
     double ingest_ms;     /* strip gather + level shift + RCT/ICT kernel      */
     double dwt_ms;        /* all DWT kernels                                  */
     double quant_ms;      /* quantisation + bit-plane kernel                  */
-    double t1_ms;         /* EBCOT tier-1 kernel                              */
+    double t1_ms;         /* EBCOT tier-1 kernels                             */
     double pcrd_ms;       /* hull + threshold selection kernels               */
     double d2h_ms;        /* metadata + compressed bytes download             */
     double t2_ms;         /* host tier-2 / codestream assembly                */
@@ -100,6 +100,8 @@ typedef struct jp2hip_stats {
     int64_t out_bytes;
     int32_t rate_iterations;
     int32_t reserved;
+    double t1_cm_ms;      /* tier-1 context-modelling kernel (part of t1_ms)  */
+    double t1_mq_ms;      /* tier-1 MQ-coder kernel (part of t1_ms)           */
 } jp2hip_stats;
 
 const char *jp2hip_version(void);

@@ -238,7 +238,9 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         stats->ingest_ms = st.ingest;
         stats->dwt_ms = st.dwt;
         stats->quant_ms = st.quant;
-        stats->t1_ms = st.t1;
+        stats->t1_ms = st.t1_cm + st.t1_mq;
+        stats->t1_cm_ms = st.t1_cm;
+        stats->t1_mq_ms = st.t1_mq;
         stats->pcrd_ms = st.pcrd;
         stats->d2h_ms = prof ? st.d2h : gather_ms;
         stats->t2_ms = t2ms;

@@ -16,8 +16,45 @@ struct DevBuf {
 };
 
 struct StageTimes {
-    double ingest = 0, dwt = 0, quant = 0, t1 = 0, pcrd = 0, d2h = 0;
+    double ingest = 0, dwt = 0, quant = 0, t1_cm = 0, t1_mq = 0, pcrd = 0, d2h = 0;
 };
+
+// tier-1 kernels (t1.hip)
+struct T1CmArgs {
+    const int2 *items;  // (block, plane)
+    int nitems;
+    const BlockDesc *blocks;
+    const uint64_t *bp;
+    const int32_t *sm;
+    const uint8_t *P;
+    uint8_t *stream;
+    const uint64_t *slot_off;
+    uint4 *counts;    // [block][32] (end of SPP, end of MRP, end of CUP)
+    int64_t *dspp;    // [block][32]
+    int lossless;
+};
+struct T1MqArgs {
+    const BlockDesc *blocks;
+    const int32_t *order;
+    int nblocks;
+    const uint8_t *P;
+    const uint8_t *stream;
+    const uint64_t *slot_off;
+    const uint4 *counts;
+    const int64_t *dspp, *dref, *dsig;
+    uint8_t *out;
+    int32_t *rates;
+    int64_t *dists;
+    uint8_t *npasses;
+    int32_t *lengths;
+    int *err;
+    int lanes;  // blocks per wavefront (1..64)
+    int64_t *dbg;  // optional per-block census [block][4] (debug)
+    int variant;   // debug timing probes (0 in production)
+};
+void launch_t1_cm(const T1CmArgs &a, hipStream_t st);
+void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
+uint32_t t1_plane_stream_cap(int w, int h);
 
 // Owns all device memory of a context; buffers only grow, so repeated
 // encodes of the same geometry never allocate.
@@ -50,16 +87,21 @@ class GpuEncoder {
   private:
     // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
-    static constexpr int kNumEvents = 10;
+    static constexpr int kNumEvents = 12;
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
-        nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src;
+        nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
+        segkey, segkey2, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        dbgbuf;
+    int nseg = 0;
     uint8_t *h_packed = nullptr;
     size_t h_packed_cap = 0;
     std::vector<int32_t> h_lengths;
     std::vector<uint8_t> h_npasses, h_P;
+    std::vector<int2> h_items;
+    std::vector<uint64_t> h_slot;
 };
 
 }  // namespace jp2hip

@@ -16,6 +16,7 @@
 // Floating point: built with -ffp-contract=off; every 9/7 / ICT expression is
 // written in the same order as the oracle so the lossy path is bit-exact.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -25,6 +26,7 @@
 #include <string>
 #include <vector>
 
+#include "device_common.h"
 #include "gpu_encoder.h"
 
 namespace jp2hip {
@@ -234,34 +236,6 @@ __global__ void __launch_bounds__(256) k_dwt_horz(DwtArgs a) {
 }
 
 // --------------------------------------------------------------------------
-// Distortion bookkeeping (identical integer definition in the oracle):
-// squared error in half-units of mid-point reconstruction from plane p up.
-// --------------------------------------------------------------------------
-__device__ __forceinline__ int64_t dist_at(uint32_t v, int p, bool lossless) {
-    int64_t t2 = 2 * (int64_t)v + (lossless ? 0 : 1);
-    int64_t r2 = 0;
-    if ((v >> p) != 0) {
-        r2 = 2 * (int64_t)((v >> p) << p);
-        if (!(lossless && p == 0)) r2 += (int64_t)1 << p;
-    }
-    int64_t e = t2 - r2;
-    return e * e;
-}
-__device__ __forceinline__ int64_t dist_gain(uint32_t v, int p, bool lossless) {
-    return dist_at(v, p + 1, lossless) - dist_at(v, p, lossless);
-}
-
-__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        int lo = __shfl_xor((int)(uint32_t)v, o, 64);
-        int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), o, 64);
-        v += (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-    }
-    return v;
-}
-
-// --------------------------------------------------------------------------
 // S4: quantisation + bit-planes.  One wavefront per code-block; lane = column.
 // Layout per block (uint64 words): B[p][64 rows] for p < Mb, then
 // S[p][64 rows] = OR_{q>=p} B[q], then sign[64 rows].
@@ -350,427 +324,6 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
 }
 
 // --------------------------------------------------------------------------
-// S5: EBCOT tier-1 (Annex D) + MQ coder (Annex C).
-//
-// One lane encodes one code-block.  Significance state lives in 64-bit row
-// masks (bit c = column c); a stripe (4 rows) is modelled with whole-row
-// bit operations and only coded samples are visited.  SPP membership is the
-// least fixed point of the causal neighbourhood rule, found by iterating the
-// stripe's mask equations; MRP and CUP contexts are closed-form because the
-// significance after CUP of plane p is exactly S[p].
-// --------------------------------------------------------------------------
-enum { CX_RL = 17, CX_UNI = 18 };
-
-__device__ __forceinline__ int zc_ctx(int band, int pat) {
-    int UL = pat & 1, U = (pat >> 1) & 1, UR = (pat >> 2) & 1, Lf = (pat >> 3) & 1;
-    int Rt = (pat >> 4) & 1, DL = (pat >> 5) & 1, D = (pat >> 6) & 1, DR = (pat >> 7) & 1;
-    int h = Lf + Rt, v = U + D, dg = UL + UR + DL + DR;
-    if (band == 1) { int t = h; h = v; v = t; }
-    if (band == 3) {
-        int hv = h + v;
-        if (dg >= 3) return 8;
-        if (dg == 2) return hv >= 1 ? 7 : 6;
-        if (dg == 1) return hv >= 2 ? 5 : (hv == 1 ? 4 : 3);
-        return hv >= 2 ? 2 : (hv == 1 ? 1 : 0);
-    }
-    if (h == 2) return 8;
-    if (h == 1) return v >= 1 ? 7 : (dg >= 1 ? 6 : 5);
-    if (v == 2) return 4;
-    if (v == 1) return 3;
-    if (dg >= 2) return 2;
-    return dg == 1 ? 1 : 0;
-}
-
-// pattern: Lsig Lneg Rsig Rneg Usig Uneg Dsig Dneg -> (ctx << 1) | xorbit
-__device__ __forceinline__ int sc_lut(int pat) {
-    auto contrib = [](int sig, int neg) { return sig ? (neg ? -1 : 1) : 0; };
-    int hc = contrib(pat & 1, (pat >> 1) & 1) + contrib((pat >> 2) & 1, (pat >> 3) & 1);
-    int vc = contrib((pat >> 4) & 1, (pat >> 5) & 1) + contrib((pat >> 6) & 1, (pat >> 7) & 1);
-    hc = hc < -1 ? -1 : (hc > 1 ? 1 : hc);
-    vc = vc < -1 ? -1 : (vc > 1 ? 1 : vc);
-    int ctx, xr;
-    if (hc == 1) { xr = 0; ctx = vc == 1 ? 13 : (vc == 0 ? 12 : 11); }
-    else if (hc == 0) { xr = vc == -1; ctx = vc == 0 ? 9 : 10; }
-    else { xr = 1; ctx = vc == 1 ? 11 : (vc == 0 ? 12 : 13); }
-    return (ctx << 1) | xr;
-}
-
-__constant__ uint16_t c_qe[47] = {
-    0x5601, 0x3401, 0x1801, 0x0AC1, 0x0521, 0x0221, 0x5601, 0x5401, 0x4801, 0x3801, 0x3001, 0x2401,
-    0x1C01, 0x1601, 0x5601, 0x5401, 0x5101, 0x4801, 0x3801, 0x3401, 0x3001, 0x2801, 0x2401, 0x2201,
-    0x1C01, 0x1801, 0x1601, 0x1401, 0x1201, 0x1101, 0x0AC1, 0x09C1, 0x08A1, 0x0521, 0x0441, 0x02A1,
-    0x0221, 0x0141, 0x0111, 0x0085, 0x0049, 0x0025, 0x0015, 0x0009, 0x0005, 0x0001, 0x5601};
-__constant__ uint8_t c_nmps[47] = {1,  2,  3,  4,  5,  38, 7,  8,  9,  10, 11, 12, 13, 29, 15, 16,
-                                   17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32,
-                                   33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 45, 46};
-__constant__ uint8_t c_nlps[47] = {1,  6,  9,  12, 29, 33, 6,  14, 14, 14, 17, 18, 20, 21, 14, 14,
-                                   15, 16, 17, 18, 19, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29,
-                                   30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 46};
-
-struct Mq {
-    uint32_t C, A, B;
-    int CT, bp, cap;
-    uint8_t *out;
-};
-
-__device__ __forceinline__ void mq_byteout(Mq &m) {
-    uint32_t B = m.B;
-    if (B != 0xFF && m.C >= 0x8000000u) {  // carry into the pending byte
-        B++;
-        m.C &= 0x7FFFFFFu;
-    }
-    if (m.bp >= 0 && m.bp < m.cap) m.out[m.bp] = (uint8_t)B;
-    m.bp++;
-    if (B == 0xFF) {
-        m.B = m.C >> 20;
-        m.C &= 0xFFFFFu;
-        m.CT = 7;
-    } else {
-        m.B = m.C >> 19;
-        m.C &= 0x7FFFFu;
-        m.CT = 8;
-    }
-}
-
-__device__ __forceinline__ void mq_encode(Mq &m, uint8_t *cst, const uint32_t *tab, int d) {
-    uint32_t st = *cst;
-    uint32_t t = tab[st >> 1];
-    uint32_t qe = t & 0xFFFFu;
-    uint32_t mps = st & 1u;
-    m.A -= qe;
-    if ((uint32_t)d == mps) {
-        if (m.A & 0x8000u) {
-            m.C += qe;
-            return;
-        }
-        if (m.A < qe) m.A = qe;
-        else m.C += qe;
-        st = (((t >> 16) & 63u) << 1) | mps;
-    } else {
-        if (m.A < qe) m.C += qe;
-        else m.A = qe;
-        mps ^= (t >> 28) & 1u;
-        st = (((t >> 22) & 63u) << 1) | mps;
-    }
-    *cst = (uint8_t)st;
-    int n = __clz(m.A) - 16;
-    while (n > 0) {
-        int s = min(n, m.CT);
-        m.A <<= s;
-        m.C <<= s;
-        m.CT -= s;
-        n -= s;
-        if (m.CT == 0) mq_byteout(m);
-    }
-}
-
-__device__ __forceinline__ int mq_flush(Mq &m) {
-    uint32_t tempc = m.C + m.A;
-    m.C |= 0xFFFFu;
-    if (m.C >= tempc) m.C -= 0x8000u;
-    m.C <<= m.CT;
-    mq_byteout(m);
-    m.C <<= m.CT;
-    mq_byteout(m);
-    if (m.B != 0xFF) {
-        if (m.bp >= 0 && m.bp < m.cap) m.out[m.bp] = (uint8_t)m.B;
-        m.bp++;
-    }
-    return m.bp;
-}
-
-__device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m >> c) & 1u; }
-
-// 8-neighbour significance pattern of (row with masks) at column c.
-// up: UPb (UL,U) UPa (UR); mid: MIDb (L) MIDa (R); down: DNb (DL) DNa (D,DR)
-__device__ __forceinline__ int pattern8(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
-                                        uint64_t DNb, uint64_t DNa, int c) {
-    return (int)(bit(UPb << 1, c) | (bit(UPb, c) << 1) | (bit(UPa >> 1, c) << 2) |
-                 (bit(MIDb << 1, c) << 3) | (bit(MIDa >> 1, c) << 4) | (bit(DNb << 1, c) << 5) |
-                 (bit(DNa, c) << 6) | (bit(DNa >> 1, c) << 7));
-}
-__device__ __forceinline__ int pattern_sign(uint64_t UPb, uint64_t MIDb, uint64_t MIDa, uint64_t DNa,
-                                            uint64_t sgU, uint64_t sgM, uint64_t sgD, int c) {
-    return (int)(bit(MIDb << 1, c) | (bit(sgM << 1, c) << 1) | (bit(MIDa >> 1, c) << 2) |
-                 (bit(sgM >> 1, c) << 3) | (bit(UPb, c) << 4) | (bit(sgU, c) << 5) |
-                 (bit(DNa, c) << 6) | (bit(sgD, c) << 7));
-}
-__device__ __forceinline__ uint64_t nbhd(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
-                                         uint64_t DNb, uint64_t DNa) {
-    return (UPb << 1) | UPb | (UPa >> 1) | (MIDb << 1) | (MIDa >> 1) | (DNb << 1) | DNa | (DNa >> 1);
-}
-
-struct T1Args {
-    const BlockDesc *blocks;
-    const int32_t *order;
-    int nblocks;
-    const uint64_t *bp;
-    const int32_t *sm;
-    const int64_t *dref, *dsig;
-    const uint8_t *P;
-    uint8_t *out;
-    int32_t *rates;  // [block][kMaxPasses]
-    int64_t *dists;  // [block][kMaxPasses]
-    uint8_t *npasses;
-    int32_t *lengths;
-    int lossless;
-    int *err;
-};
-
-// Row-mask helpers for stripe s.  Index i in 0..5 = rows r0-1 .. r0+4.
-#define ROWS6(dst, expr)                     \
-    _Pragma("unroll") for (int i = 0; i < 6; i++) { \
-        int r = r0 - 1 + i;                   \
-        dst[i] = (r >= 0 && r < h) ? (expr) : 0ull; \
-    }
-
-__global__ void __launch_bounds__(64) k_t1(T1Args a) {
-    __shared__ uint64_t Nsh[64 * 64];
-    __shared__ uint8_t cxs[19 * 64];
-    __shared__ uint8_t lzc[4 * 256];
-    __shared__ uint8_t lsc[256];
-    __shared__ uint32_t mqt[48];
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 1024; i += 64) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
-    for (int i = lane; i < 256; i += 64) lsc[i] = (uint8_t)sc_lut(i);
-    if (lane < 47)
-        mqt[lane] = (uint32_t)c_qe[lane] | ((uint32_t)c_nmps[lane] << 16) |
-                    ((uint32_t)c_nlps[lane] << 22) |
-                    ((uint32_t)(lane == 0 || lane == 6 || lane == 14) << 28);
-    __syncthreads();
-    const int gi = blockIdx.x * 64 + lane;
-    if (gi >= a.nblocks) return;
-    const int b = a.order[gi];
-    const BlockDesc d = a.blocks[b];
-    const int P = a.P[b];
-    if (P == 0) {
-        a.npasses[b] = 0;
-        a.lengths[b] = 0;
-        return;
-    }
-    const bool lossless = a.lossless != 0;
-    const int w = d.w, h = d.h, Mb = d.Mb;
-    const uint64_t V = (w >= 64) ? ~0ull : ((1ull << w) - 1ull);
-    const uint64_t *BP = a.bp + d.bp_off;
-    const uint64_t *SP = BP + (size_t)Mb * 64;
-    const uint64_t *SGp = BP + (size_t)2 * Mb * 64;
-    const int32_t *SM = a.sm + d.sm_off;
-    const uint8_t *zl = lzc + d.band * 256;
-    uint8_t *cx = cxs + lane;
-#pragma unroll
-    for (int k = 0; k < 19; k++) cx[k * 64] = 0;
-    cx[0] = 4 << 1;
-    cx[CX_RL * 64] = 3 << 1;
-    cx[CX_UNI * 64] = 46 << 1;
-    Mq m;
-    m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
-    m.cap = (int)d.out_cap;
-    m.out = a.out + d.out_off;
-    int32_t *R = a.rates + (size_t)b * kMaxPasses;
-    int64_t *D = a.dists + (size_t)b * kMaxPasses;
-    int np = 0;
-    uint64_t *Ncol = Nsh + lane;  // Ncol[r * 64]
-    const int nstripes = (h + 3) >> 2;
-
-    for (int p = P - 1; p >= 0; --p) {
-        const uint64_t *Bp = BP + (size_t)p * 64;
-        const uint64_t *S0p = SP + (size_t)p * 64;
-        const bool has1 = p + 1 < P, has2 = p + 2 < P;
-        const uint64_t *S1p = SP + (size_t)(p + 1) * 64;
-        const uint64_t *S2p = SP + (size_t)(p + 2) * 64;
-        int64_t dspp = 0;
-        if (p < P - 1) {
-            // ---------------- significance propagation ----------------
-            for (int s = 0; s < nstripes; s++) {
-                const int r0 = s * 4, nr = min(4, h - r0);
-                uint64_t s1[6], sg[6], bt[4], n[4] = {0, 0, 0, 0}, mem[4];
-                ROWS6(s1, has1 ? S1p[r] : 0ull);
-                ROWS6(sg, SGp[r]);
-#pragma unroll
-                for (int k = 0; k < 4; k++) bt[k] = (k < nr) ? Bp[r0 + k] : 0ull;
-                const uint64_t bfprev = (r0 > 0) ? (s1[0] | Ncol[(r0 - 1) * 64]) : 0ull;
-                for (;;) {
-                    bool changed = false;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        if (k >= nr) { mem[k] = 0; continue; }
-                        uint64_t UPb = (k == 0) ? bfprev : (s1[k] | n[k - 1]);
-                        uint64_t UPa = (k == 0) ? bfprev : s1[k];
-                        uint64_t MIDb = s1[k + 1] | n[k], MIDa = s1[k + 1];
-                        uint64_t DNb = (k == 3) ? s1[5] : (s1[k + 2] | n[k + 1]);
-                        uint64_t DNa = s1[k + 2];
-                        mem[k] = ~s1[k + 1] & V & nbhd(UPb, UPa, MIDb, MIDa, DNb, DNa);
-                        uint64_t nn = mem[k] & bt[k];
-                        if (nn != n[k]) { n[k] = nn; changed = true; }
-                    }
-                    if (!changed) break;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (k < nr) Ncol[(r0 + k) * 64] = n[k];
-                uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
-                while (colmask) {
-                    const int c = __ffsll((unsigned long long)colmask) - 1;
-                    colmask &= colmask - 1;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        if (k >= nr || !bit(mem[k], c)) continue;
-                        uint64_t UPb = (k == 0) ? bfprev : (s1[k] | n[k - 1]);
-                        uint64_t UPa = (k == 0) ? bfprev : s1[k];
-                        uint64_t MIDb = s1[k + 1] | n[k], MIDa = s1[k + 1];
-                        uint64_t DNb = (k == 3) ? s1[5] : (s1[k + 2] | n[k + 1]);
-                        uint64_t DNa = s1[k + 2];
-                        int pat = pattern8(UPb, UPa, MIDb, MIDa, DNb, DNa, c);
-                        int bv = (int)bit(bt[k], c);
-                        mq_encode(m, cx + zl[pat] * 64, mqt, bv);
-                        if (bv) {
-                            int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[k], sg[k + 1], sg[k + 2], c)];
-                            uint32_t word = (uint32_t)SM[(r0 + k) * 64 + c];
-                            mq_encode(m, cx + (sp >> 1) * 64, mqt, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
-                            dspp += dist_gain(word & 0x7FFFFFFFu, p, lossless);
-                        }
-                    }
-                }
-            }
-            R[np] = m.bp + 3;
-            D[np] = dspp;
-            np++;
-            // ---------------- magnitude refinement ----------------
-            for (int s = 0; s < nstripes; s++) {
-                const int r0 = s * 4, nr = min(4, h - r0);
-                uint64_t post[6], bt[4], mem[4], fr[4];
-                ROWS6(post, S1p[r] | Ncol[r * 64]);
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    bool in = k < nr;
-                    bt[k] = in ? Bp[r0 + k] : 0ull;
-                    uint64_t s1k = in ? S1p[r0 + k] : 0ull;
-                    mem[k] = s1k & V;
-                    fr[k] = s1k & ~((in && has2) ? S2p[r0 + k] : 0ull);
-                }
-                uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
-                while (colmask) {
-                    const int c = __ffsll((unsigned long long)colmask) - 1;
-                    colmask &= colmask - 1;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        if (k >= nr || !bit(mem[k], c)) continue;
-                        int ctx;
-                        if (bit(fr[k], c)) {
-                            int pat = pattern8(post[k], post[k], post[k + 1], post[k + 1], post[k + 2],
-                                               post[k + 2], c);
-                            ctx = pat ? 15 : 14;
-                        } else {
-                            ctx = 16;
-                        }
-                        mq_encode(m, cx + ctx * 64, mqt, (int)bit(bt[k], c));
-                    }
-                }
-            }
-            R[np] = m.bp + 3;
-            D[np] = a.dref[(size_t)b * 32 + p];
-            np++;
-        }
-        // ---------------- cleanup ----------------
-        const bool spp = p < P - 1;
-        for (int s = 0; s < nstripes; s++) {
-            const int r0 = s * 4, nr = min(4, h - r0);
-            uint64_t s1[6], post[6], s0[6], sg[6], bt[4], mem[4];
-            ROWS6(s1, has1 ? S1p[r] : 0ull);
-            ROWS6(post, s1[i] | (spp ? Ncol[r * 64] : 0ull));
-            ROWS6(s0, S0p[r]);
-            ROWS6(sg, SGp[r]);
-#pragma unroll
-            for (int k = 0; k < 4; k++) bt[k] = (k < nr) ? Bp[r0 + k] : 0ull;
-            // SPP membership with the final new-significance masks
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (k >= nr) { mem[k] = 0; continue; }
-                uint64_t c_spp = 0;
-                if (spp) {
-                    uint64_t UPb = post[k], UPa = (k == 0) ? post[0] : s1[k];
-                    uint64_t MIDb = post[k + 1], MIDa = s1[k + 1];
-                    uint64_t DNb = (k == 3) ? s1[5] : post[k + 2];
-                    uint64_t DNa = s1[k + 2];
-                    c_spp = ~s1[k + 1] & V & nbhd(UPb, UPa, MIDb, MIDa, DNb, DNa);
-                }
-                mem[k] = ~s1[k + 1] & ~c_spp & V;
-            }
-            uint64_t rl = 0;
-            if (nr == 4) {
-                uint64_t z = (s0[0] << 1) | s0[0] | (s0[0] >> 1) |
-                             ((s0[1] | s0[2] | s0[3] | s0[4]) << 1) |
-                             ((post[1] | post[2] | post[3] | post[4]) >> 1) |
-                             (post[5] << 1) | post[5] | (post[5] >> 1);
-                rl = mem[0] & mem[1] & mem[2] & mem[3] & ~z;
-            }
-            uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
-            while (colmask) {
-                const int c = __ffsll((unsigned long long)colmask) - 1;
-                colmask &= colmask - 1;
-                int kstart = 0;
-                if (bit(rl, c)) {
-                    int r = 4;
-#pragma unroll
-                    for (int k = 3; k >= 0; k--)
-                        if (bit(bt[k], c)) r = k;
-                    if (r == 4) {
-                        mq_encode(m, cx + CX_RL * 64, mqt, 0);
-                        continue;
-                    }
-                    mq_encode(m, cx + CX_RL * 64, mqt, 1);
-                    mq_encode(m, cx + CX_UNI * 64, mqt, r >> 1);
-                    mq_encode(m, cx + CX_UNI * 64, mqt, r & 1);
-                    // sign of sample r: neighbours per the before/after rule
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        if (k != r) continue;
-                        uint64_t UPb = s0[k];
-                        uint64_t MIDb = s0[k + 1], MIDa = post[k + 1];
-                        uint64_t DNa = post[k + 2];
-                        int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[k], sg[k + 1], sg[k + 2], c)];
-                        uint32_t word = (uint32_t)SM[(r0 + k) * 64 + c];
-                        mq_encode(m, cx + (sp >> 1) * 64, mqt, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
-                    }
-                    kstart = r + 1;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    if (k < kstart || k >= nr || !bit(mem[k], c)) continue;
-                    uint64_t UPb = s0[k], UPa = (k == 0) ? s0[0] : post[k];
-                    uint64_t MIDb = s0[k + 1], MIDa = post[k + 1];
-                    uint64_t DNb = (k == 3) ? post[5] : s0[k + 2];
-                    uint64_t DNa = post[k + 2];
-                    int pat = pattern8(UPb, UPa, MIDb, MIDa, DNb, DNa, c);
-                    int bv = (int)bit(bt[k], c);
-                    mq_encode(m, cx + zl[pat] * 64, mqt, bv);
-                    if (bv) {
-                        int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[k], sg[k + 1], sg[k + 2], c)];
-                        uint32_t word = (uint32_t)SM[(r0 + k) * 64 + c];
-                        mq_encode(m, cx + (sp >> 1) * 64, mqt, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
-                    }
-                }
-            }
-        }
-        R[np] = m.bp + 3;
-        D[np] = a.dsig[(size_t)b * 32 + p] - dspp;
-        np++;
-    }
-    const int len = mq_flush(m);
-    if (len > m.cap) {
-        atomicOr(a.err, 1);
-    }
-    R[np - 1] = len;
-    for (int i = 0; i < np; i++) {
-        int r = min(R[i], len);
-        if (r > 1 && r <= m.cap && m.out[r - 1] == 0xFF) r--;
-        R[i] = r;
-    }
-    a.npasses[b] = (uint8_t)np;
-    a.lengths[b] = len;
-}
-
-// --------------------------------------------------------------------------
 // S6: PCRD-opt.  Hull per block (thread per block), then one workgroup
 // finds, for every layer at once, the smallest slope key whose total rate
 // fits the layer budget (63-step bisection over the key space).
@@ -821,78 +374,90 @@ __global__ void __launch_bounds__(256) k_hull(HullArgs a) {
     a.nhull[b] = (uint8_t)nh;
 }
 
-struct SelectArgs {
-    int nblocks, layers, lossless;
-    const uint8_t *nhull;
-    const uint8_t *hpass;
-    const uint64_t *hkey;
-    const uint8_t *npasses;
-    const int32_t *rates;
-    const int64_t *budget;  // [layers]
-    uint8_t *nl;            // [block][layers]
-    int32_t *lrate;         // [block][layers]
-};
+// Layer thresholds.  The oracle's rule (oracle/jp2_oracle.c select_threshold)
+// is: walk hull segments in decreasing slope-key order, group equal keys, and
+// take whole groups while the running byte total fits the budget.  Here the
+// segments of all blocks are radix-sorted once per encode (hipcub), their
+// sizes prefix-summed, and each budget is resolved by one binary search.
+__global__ void __launch_bounds__(256) k_seg_count(int nblocks, const uint8_t *nhull, int32_t *nseg) {
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nblocks) nseg[b] = max(0, (int)nhull[b] - 1);
+}
 
-// rate of block b at the last hull point whose key >= K
-__device__ __forceinline__ int hull_pick(const SelectArgs &a, int b, uint64_t K) {
-    int nh = a.nhull[b];
-    const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
-    // keys strictly decrease with the hull index (i >= 1)
-    int lo = 1, hi = nh;  // find first i in [1,nh) with hk[i] < K
+__global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nhull, const uint8_t *hpass,
+                                                  const uint64_t *hkey, const int32_t *rates,
+                                                  const int32_t *segoff, uint64_t *keys, int64_t *vals) {
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    int nh = nhull[b];
+    const uint8_t *hp = hpass + (size_t)b * (kMaxPasses + 1);
+    const uint64_t *hk = hkey + (size_t)b * (kMaxPasses + 1);
+    const int32_t *R = rates + (size_t)b * kMaxPasses;
+    int o = segoff[b];
+    for (int i = 1; i < nh; i++) {
+        keys[o + i - 1] = hk[i];
+        vals[o + i - 1] = (int64_t)(R[hp[i] - 1] - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
+    }
+}
+
+// one thread per layer: threshold key K (UINT64_MAX = nothing fits)
+__global__ void k_thresh(int nseg, int layers, const uint64_t *keys, const int64_t *cum,
+                         const int64_t *budget, uint64_t *K) {
+    int l = threadIdx.x;
+    if (l >= layers) return;
+    int64_t bgt = budget[l];
+    int lo = 0, hi = nseg;  // first index with cum > bgt
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (cum[mid] <= bgt) lo = mid + 1;
+        else hi = mid;
+    }
+    int j = lo - 1;
+    if (j >= 0 && j + 1 < nseg && keys[j + 1] == keys[j]) {
+        uint64_t kj = keys[j];
+        int l2 = 0, h2 = j;  // first index whose key == kj (keys descending)
+        while (l2 < h2) {
+            int mid = (l2 + h2) >> 1;
+            if (keys[mid] > kj) l2 = mid + 1;
+            else h2 = mid;
+        }
+        j = l2 - 1;
+    }
+    K[l] = (j >= 0) ? keys[j] : 0xFFFFFFFFFFFFFFFFull;
+}
+
+// last hull index whose key >= K (0 = nothing); hull keys strictly decrease
+__device__ __forceinline__ int hull_pick(const uint64_t *hk, int nh, uint64_t K) {
+    int lo = 1, hi = nh;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
         if (hk[mid] >= K) lo = mid + 1;
         else hi = mid;
     }
-    return lo - 1;  // hull index (0 = nothing)
+    return lo - 1;
 }
 
-__global__ void __launch_bounds__(1024) k_select(SelectArgs a) {
-    __shared__ uint64_t lo[kMaxLayers], hi[kMaxLayers];
-    __shared__ int64_t part[32][kMaxLayers];
+struct ApplyArgs {
+    int nblocks, layers, lossless;
+    const uint8_t *nhull, *hpass, *npasses;
+    const uint64_t *hkey, *K;
+    const int32_t *rates;
+    uint8_t *nl;      // [block][layers]
+    int32_t *lrate;   // [block][layers]
+};
+
+__global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nblocks) return;
     const int L = a.layers;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid < L) { lo[tid] = 0; hi[tid] = 0x7FF0000000000000ull; }
-    __syncthreads();
-    for (int it = 0; it < 64; it++) {
-        int64_t acc[kMaxLayers];
-        uint64_t mid[kMaxLayers];
-        for (int l = 0; l < L; l++) { acc[l] = 0; mid[l] = lo[l] + ((hi[l] - lo[l]) >> 1); }
-        for (int b = tid; b < a.nblocks; b += blockDim.x) {
-            const int32_t *R = a.rates + (size_t)b * kMaxPasses;
-            const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
-            for (int l = 0; l < L; l++) {
-                int hi2 = hull_pick(a, b, mid[l]);
-                int n = hp[hi2];
-                acc[l] += n ? R[n - 1] : 0;
-            }
-        }
-        for (int l = 0; l < L; l++) {
-            int64_t v = wave_sum64(acc[l]);
-            if (lane == 0) part[wv][l] = v;
-        }
-        __syncthreads();
-        if (tid < L) {
-            int64_t s = 0;
-            for (int q = 0; q < (int)(blockDim.x >> 6); q++) s += part[q][tid];
-            if (lo[tid] < hi[tid]) {
-                uint64_t md = lo[tid] + ((hi[tid] - lo[tid]) >> 1);
-                if (s <= a.budget[tid]) hi[tid] = md;
-                else lo[tid] = md + 1;
-            }
-        }
-        __syncthreads();
-    }
-    for (int b = tid; b < a.nblocks; b += blockDim.x) {
-        const int32_t *R = a.rates + (size_t)b * kMaxPasses;
-        const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
-        for (int l = 0; l < L; l++) {
-            int n;
-            if (a.lossless && l == L - 1) n = a.npasses[b];
-            else n = hp[hull_pick(a, b, hi[l])];
-            a.nl[(size_t)b * L + l] = (uint8_t)n;
-            a.lrate[(size_t)b * L + l] = n ? R[n - 1] : 0;
-        }
+    const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
+    const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
+    const int32_t *R = a.rates + (size_t)b * kMaxPasses;
+    int nh = a.nhull[b];
+    for (int l = 0; l < L; l++) {
+        int n = (a.lossless && l == L - 1) ? (int)a.npasses[b] : (int)hp[hull_pick(hk, nh, a.K[l])];
+        a.nl[(size_t)b * L + l] = (uint8_t)n;
+        a.lrate[(size_t)b * L + l] = n ? R[n - 1] : 0;
     }
 }
 
@@ -931,7 +496,9 @@ static bool ensure(DevBuf &b, size_t count, std::string &err) {
 GpuEncoder::~GpuEncoder() {
     DevBuf *all[] = {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
-                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src};
+                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &segcnt, &segoff, &segkey,
+                     &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
+                     &stream_buf, &counts, &dspp, &dbgbuf};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1067,24 +634,79 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (nb) hipLaunchKernelGGL(k_quant, dim3(nb), dim3(64), 0, stream, qa);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[3], stream));
-    // S5
-    T1Args ta;
-    ta.blocks = (const BlockDesc *)blocks.ptr;
-    ta.order = (const int32_t *)order.ptr;
-    ta.nblocks = nb;
-    ta.bp = (const uint64_t *)bp.ptr;
-    ta.sm = (const int32_t *)sm.ptr;
-    ta.dref = (const int64_t *)dref.ptr;
-    ta.dsig = (const int64_t *)dsig.ptr;
-    ta.P = (const uint8_t *)P.ptr;
-    ta.out = (uint8_t *)t1out.ptr;
-    ta.rates = (int32_t *)rates.ptr;
-    ta.dists = (int64_t *)dists.ptr;
-    ta.npasses = (uint8_t *)npasses.ptr;
-    ta.lengths = (int32_t *)lengths.ptr;
-    ta.lossless = plan.rc.reversible;
-    ta.err = (int *)this->err.ptr;
-    if (nb) hipLaunchKernelGGL(k_t1, dim3((nb + 63) / 64), dim3(64), 0, stream, ta);
+    // S5: tier-1.  Items (block, plane) ordered by plane depth from the top,
+    // then by block shape, so a wavefront's lanes do similar work.
+    h_P.resize(nb);
+    HIPCHECK(hipMemcpyAsync(h_P.data(), P.ptr, nb, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    h_slot.resize(nb);
+    uint64_t stream_bytes = 0;
+    int maxP = 0;
+    for (int i = 0; i < nb; i++) {
+        h_slot[i] = stream_bytes;
+        stream_bytes += (uint64_t)h_P[i] * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
+        maxP = std::max(maxP, (int)h_P[i]);
+    }
+    h_items.clear();
+    for (int k = 0; k < maxP; k++)
+        for (int i = 0; i < nb; i++) {
+            int bb = plan.t1_order[i];
+            if (h_P[bb] > k) h_items.push_back(make_int2(bb, h_P[bb] - 1 - k));
+        }
+    const int nitems = (int)h_items.size();
+    if (!ensure<int2>(items, std::max(nitems, 1), err) || !ensure<uint64_t>(slotoff, nb, err) ||
+        !ensure<uint8_t>(stream_buf, stream_bytes, err) || !ensure<uint4>(counts, (size_t)nb * 32, err) ||
+        !ensure<int64_t>(dspp, (size_t)nb * 32, err))
+        return false;
+    if (nitems) HIPCHECK(hipMemcpyAsync(items.ptr, h_items.data(), sizeof(int2) * nitems, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(slotoff.ptr, h_slot.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipEventRecord(ev[10], stream));
+    T1CmArgs ca;
+    ca.items = (const int2 *)items.ptr;
+    ca.nitems = nitems;
+    ca.blocks = (const BlockDesc *)blocks.ptr;
+    ca.bp = (const uint64_t *)bp.ptr;
+    ca.sm = (const int32_t *)sm.ptr;
+    ca.P = (const uint8_t *)P.ptr;
+    ca.stream = (uint8_t *)stream_buf.ptr;
+    ca.slot_off = (const uint64_t *)slotoff.ptr;
+    ca.counts = (uint4 *)counts.ptr;
+    ca.dspp = (int64_t *)dspp.ptr;
+    ca.lossless = plan.rc.reversible;
+    launch_t1_cm(ca, stream);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventRecord(ev[11], stream));
+    T1MqArgs ma;
+    ma.blocks = (const BlockDesc *)blocks.ptr;
+    ma.order = (const int32_t *)order.ptr;
+    ma.nblocks = nb;
+    ma.P = (const uint8_t *)P.ptr;
+    ma.stream = (const uint8_t *)stream_buf.ptr;
+    ma.slot_off = (const uint64_t *)slotoff.ptr;
+    ma.counts = (const uint4 *)counts.ptr;
+    ma.dspp = (const int64_t *)dspp.ptr;
+    ma.dref = (const int64_t *)dref.ptr;
+    ma.dsig = (const int64_t *)dsig.ptr;
+    ma.out = (uint8_t *)t1out.ptr;
+    ma.rates = (int32_t *)rates.ptr;
+    ma.dists = (int64_t *)dists.ptr;
+    ma.npasses = (uint8_t *)npasses.ptr;
+    ma.lengths = (int32_t *)lengths.ptr;
+    ma.err = (int *)this->err.ptr;
+    {
+        const char *e = getenv("JP2HIP_MQ_LANES");
+        ma.lanes = std::max(1, std::min(64, e ? atoi(e) : 8));
+    }
+    {
+        const char *e = getenv("JP2HIP_MQ_VARIANT");
+        ma.variant = e ? atoi(e) : 0;
+    }
+    ma.dbg = nullptr;
+    if (dd) {
+        if (!ensure<int64_t>(dbgbuf, (size_t)nb * 4, err)) return false;
+        ma.dbg = (int64_t *)dbgbuf.ptr;
+    }
+    launch_t1_mq(ma, stream);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[4], stream));
     // S6a hulls
@@ -1099,6 +721,43 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ha.hkey = (uint64_t *)hkey.ptr;
     if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + 255) / 256), dim3(256), 0, stream, ha);
     HIPCHECK(hipGetLastError());
+    // hull segments of all blocks, sorted by slope key (descending), sizes prefix-summed
+    if (!ensure<int32_t>(segcnt, nb, err) || !ensure<int32_t>(segoff, nb, err)) return false;
+    if (nb) hipLaunchKernelGGL(k_seg_count, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
+                               (const uint8_t *)nhull.ptr, (int32_t *)segcnt.ptr);
+    {
+        size_t tb = 0;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr, nb, stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr, nb, stream));
+    }
+    int32_t tail[2] = {0, 0};
+    if (nb) {
+        HIPCHECK(hipMemcpyAsync(&tail[0], (int32_t *)segoff.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(&tail[1], (int32_t *)segcnt.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
+    }
+    HIPCHECK(hipStreamSynchronize(stream));
+    nseg = tail[0] + tail[1];
+    if (!ensure<uint64_t>(segkey, std::max(nseg, 1), err) || !ensure<uint64_t>(segkey2, std::max(nseg, 1), err) ||
+        !ensure<int64_t>(segval, std::max(nseg, 1), err) || !ensure<int64_t>(segval2, std::max(nseg, 1), err) ||
+        !ensure<int64_t>(segcum, std::max(nseg, 1), err) || !ensure<uint64_t>(thr, kMaxLayers, err))
+        return false;
+    if (nb) hipLaunchKernelGGL(k_seg_emit, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
+                               (const uint8_t *)nhull.ptr, (const uint8_t *)hpass.ptr,
+                               (const uint64_t *)hkey.ptr, (const int32_t *)rates.ptr,
+                               (const int32_t *)segoff.ptr, (uint64_t *)segkey.ptr, (int64_t *)segval.ptr);
+    if (nseg > 0) {
+        size_t tb = 0;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,
+                                                              (int64_t *)segval.ptr, (int64_t *)segval2.ptr, nseg, 0, 64, stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(cubtmp.ptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,
+                                                              (int64_t *)segval.ptr, (int64_t *)segval2.ptr, nseg, 0, 64, stream));
+        tb = 0;
+        HIPCHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceScan::InclusiveSum(cubtmp.ptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
+    }
     HIPCHECK(hipEventRecord(ev[5], stream));
     // totals needed on the host for the budgets
     h_lengths.resize(nb);
@@ -1126,13 +785,15 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!dump(dd, "dref.bin", dref, (size_t)nb * 32 * 8, err)) return false;
         if (!dump(dd, "dsig.bin", dsig, (size_t)nb * 32 * 8, err)) return false;
         if (!dump(dd, "bp.bin", bp, plan.bp_words * 8, err)) return false;
+        if (!dump(dd, "mqdbg.bin", dbgbuf, (size_t)nb * 4 * 8, err)) return false;
     }
     if (profile) {
         float t;
         HIPCHECK(hipEventElapsedTime(&t, ev[0], ev[1])); st.ingest = t;
         HIPCHECK(hipEventElapsedTime(&t, ev[1], ev[2])); st.dwt = t;
         HIPCHECK(hipEventElapsedTime(&t, ev[2], ev[3])); st.quant = t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[3], ev[4])); st.t1 = t;
+        HIPCHECK(hipEventElapsedTime(&t, ev[10], ev[11])); st.t1_cm = t;
+        HIPCHECK(hipEventElapsedTime(&t, ev[11], ev[4])); st.t1_mq = t;
         HIPCHECK(hipEventElapsedTime(&t, ev[4], ev[5])); st.pcrd = t;
     }
     return true;
@@ -1145,20 +806,23 @@ bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets,
     const int nb = (int)plan.blocks.size();
     const int L = plan.rc.layers;
     HIPCHECK(hipMemcpyAsync(budget.ptr, budgets.data(), sizeof(int64_t) * L, hipMemcpyHostToDevice, stream));
-    SelectArgs sa;
-    sa.nblocks = nb;
-    sa.layers = L;
-    sa.lossless = plan.rc.rate_bpp <= 0.0;
-    sa.nhull = (const uint8_t *)nhull.ptr;
-    sa.hpass = (const uint8_t *)hpass.ptr;
-    sa.hkey = (const uint64_t *)hkey.ptr;
-    sa.npasses = (const uint8_t *)npasses.ptr;
-    sa.rates = (const int32_t *)rates.ptr;
-    sa.budget = (const int64_t *)budget.ptr;
-    sa.nl = (uint8_t *)nl.ptr;
-    sa.lrate = (int32_t *)lrate.ptr;
     HIPCHECK(hipEventRecord(ev[6], stream));
-    if (nb) hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, stream, sa);
+    hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
+                       (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr);
+    HIPCHECK(hipGetLastError());
+    ApplyArgs aa;
+    aa.nblocks = nb;
+    aa.layers = L;
+    aa.lossless = plan.rc.rate_bpp <= 0.0;
+    aa.nhull = (const uint8_t *)nhull.ptr;
+    aa.hpass = (const uint8_t *)hpass.ptr;
+    aa.npasses = (const uint8_t *)npasses.ptr;
+    aa.hkey = (const uint64_t *)hkey.ptr;
+    aa.K = (const uint64_t *)thr.ptr;
+    aa.rates = (const int32_t *)rates.ptr;
+    aa.nl = (uint8_t *)nl.ptr;
+    aa.lrate = (int32_t *)lrate.ptr;
+    if (nb) hipLaunchKernelGGL(k_apply, dim3((nb + 255) / 256), dim3(256), 0, stream, aa);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[7], stream));
     h_nl.resize((size_t)nb * L);

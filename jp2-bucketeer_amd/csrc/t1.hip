@@ -1,0 +1,578 @@
+// t1.hip -- EBCOT tier-1 (ISO/IEC 15444-1 Annex D) and the MQ coder (Annex C)
+// for gfx950, split in two kernels so the serial part is as short as possible:
+//
+//   k_t1_cm  context modelling, one lane per (code-block, bit-plane).
+//            Significance lives in 64-bit row masks (bit c = column c); a
+//            stripe (4 rows) is modelled with whole-row bit operations.  The
+//            state at the start of plane p is known from the bit-planes
+//            (S[p+1] = OR of planes above p), so planes are independent:
+//              - SPP membership is the least fixed point of the causal
+//                neighbourhood rule (iterated on the stripe's masks);
+//              - MRP neighbours all see the post-SPP state S[p+1] | N;
+//              - CUP neighbours see S[p] (already visited) or S[p+1] | N
+//                (not yet visited): closed form, no sample-serial state.
+//            Output: the (context, decision) byte stream of the plane's
+//            passes plus per-pass counts and the SPP distortion decrease.
+//   k_t1_mq  one lane per code-block: runs the MQ coder over the block's
+//            streams in pass order, records the truncation length after every
+//            pass, terminates the codeword (Annex C.2.9 FLUSH).
+//
+// The decision order, contexts, truncation lengths and distortion values are
+// those of the oracle's sample-at-a-time coder (oracle/jp2_oracle.c,
+// oracle_t1_encode); the parity tests compare them byte for byte.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "gpu_encoder.h"
+
+namespace jp2hip {
+
+enum { CX_RL = 17, CX_UNI = 18 };
+
+// zero-coding context (Table D.1) from the 8-neighbour pattern
+// bits: UL U UR L R DL D DR
+__device__ __forceinline__ int zc_ctx(int band, int pat) {
+    int UL = pat & 1, U = (pat >> 1) & 1, UR = (pat >> 2) & 1, Lf = (pat >> 3) & 1;
+    int Rt = (pat >> 4) & 1, DL = (pat >> 5) & 1, D = (pat >> 6) & 1, DR = (pat >> 7) & 1;
+    int h = Lf + Rt, v = U + D, dg = UL + UR + DL + DR;
+    if (band == 1) { int t = h; h = v; v = t; }
+    if (band == 3) {
+        int hv = h + v;
+        if (dg >= 3) return 8;
+        if (dg == 2) return hv >= 1 ? 7 : 6;
+        if (dg == 1) return hv >= 2 ? 5 : (hv == 1 ? 4 : 3);
+        return hv >= 2 ? 2 : (hv == 1 ? 1 : 0);
+    }
+    if (h == 2) return 8;
+    if (h == 1) return v >= 1 ? 7 : (dg >= 1 ? 6 : 5);
+    if (v == 2) return 4;
+    if (v == 1) return 3;
+    if (dg >= 2) return 2;
+    return dg == 1 ? 1 : 0;
+}
+
+// sign-coding context (Tables D.2/D.3): pattern Lsig Lneg Rsig Rneg Usig Uneg
+// Dsig Dneg -> (ctx << 1) | xorbit
+__device__ __forceinline__ int sc_lut(int pat) {
+    auto contrib = [](int sig, int neg) { return sig ? (neg ? -1 : 1) : 0; };
+    int hc = contrib(pat & 1, (pat >> 1) & 1) + contrib((pat >> 2) & 1, (pat >> 3) & 1);
+    int vc = contrib((pat >> 4) & 1, (pat >> 5) & 1) + contrib((pat >> 6) & 1, (pat >> 7) & 1);
+    hc = hc < -1 ? -1 : (hc > 1 ? 1 : hc);
+    vc = vc < -1 ? -1 : (vc > 1 ? 1 : vc);
+    int ctx, xr;
+    if (hc == 1) { xr = 0; ctx = vc == 1 ? 13 : (vc == 0 ? 12 : 11); }
+    else if (hc == 0) { xr = vc == -1; ctx = vc == 0 ? 9 : 10; }
+    else { xr = 1; ctx = vc == 1 ? 11 : (vc == 0 ? 12 : 13); }
+    return (ctx << 1) | xr;
+}
+
+__device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m >> c) & 1u; }
+
+// 8-neighbour pattern of a sample at column c.  Neighbour rows come as a
+// "before" mask (positions already visited in this pass) and an "after" mask.
+// up: UPb (UL,U) UPa (UR); mid: MIDb (L) MIDa (R); down: DNb (DL) DNa (D,DR)
+__device__ __forceinline__ int pattern8(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
+                                        uint64_t DNb, uint64_t DNa, int c) {
+    return (int)(bit(UPb << 1, c) | (bit(UPb, c) << 1) | (bit(UPa >> 1, c) << 2) |
+                 (bit(MIDb << 1, c) << 3) | (bit(MIDa >> 1, c) << 4) | (bit(DNb << 1, c) << 5) |
+                 (bit(DNa, c) << 6) | (bit(DNa >> 1, c) << 7));
+}
+__device__ __forceinline__ int pattern_sign(uint64_t UPb, uint64_t MIDb, uint64_t MIDa, uint64_t DNa,
+                                            uint64_t sgU, uint64_t sgM, uint64_t sgD, int c) {
+    return (int)(bit(MIDb << 1, c) | (bit(sgM << 1, c) << 1) | (bit(MIDa >> 1, c) << 2) |
+                 (bit(sgM >> 1, c) << 3) | (bit(UPb, c) << 4) | (bit(sgU, c) << 5) |
+                 (bit(DNa, c) << 6) | (bit(sgD, c) << 7));
+}
+__device__ __forceinline__ uint64_t nbhd(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
+                                         uint64_t DNb, uint64_t DNa) {
+    return (UPb << 1) | UPb | (UPa >> 1) | (MIDb << 1) | (MIDa >> 1) | (DNb << 1) | DNa | (DNa >> 1);
+}
+
+// bytes reserved per (block, plane) for the three passes' decisions:
+// at most w*h coding decisions + w*h sign decisions + 3 per run-length column
+// (each pass starts on a 16-byte boundary; the MQ kernel reads up to two
+// 16-byte chunks past the end of a pass)
+__host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
+    return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
+}
+
+// decision stream writer: byte = (context << 1) | decision, packed 4 per word
+struct Emit {
+    uint32_t *base;
+    uint32_t acc;
+    int n;
+    __device__ __forceinline__ void put(int cx, int d) {
+        acc |= (uint32_t)((cx << 1) | d) << ((n & 3) * 8);
+        n++;
+        if ((n & 3) == 0) {
+            base[(n >> 2) - 1] = acc;
+            acc = 0;
+        }
+    }
+    // close the current pass: flush the partial word, next pass at 16 bytes
+    __device__ __forceinline__ void align16() {
+        if (n & 3) base[n >> 2] = acc;
+        acc = 0;
+        n = (n + 15) & ~15;
+    }
+};
+
+#define ROWS6(dst, expr)                                  \
+    _Pragma("unroll") for (int i = 0; i < 6; i++) {       \
+        int r = r0 - 1 + i;                               \
+        dst[i] = (r >= 0 && r < h) ? (expr) : 0ull;       \
+    }
+
+__global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
+    __shared__ uint64_t Nsh[64 * 64];
+    __shared__ uint8_t lzc[4 * 256];
+    __shared__ uint8_t lsc[256];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 1024; i += 64) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
+    for (int i = lane; i < 256; i += 64) lsc[i] = (uint8_t)sc_lut(i);
+    __syncthreads();
+    const int gi = blockIdx.x * 64 + lane;
+    if (gi >= a.nitems) return;
+    const int2 item = a.items[gi];
+    const int b = item.x, p = item.y;
+    const BlockDesc d = a.blocks[b];
+    const int P = a.P[b];
+    const int k = P - 1 - p;  // plane index counted from the block's top plane
+    const bool lossless = a.lossless != 0;
+    const int w = d.w, h = d.h, Mb = d.Mb;
+    const uint64_t V = (w >= 64) ? ~0ull : ((1ull << w) - 1ull);
+    const uint64_t *BP = a.bp + d.bp_off;
+    const uint64_t *SP = BP + (size_t)Mb * 64;
+    const uint64_t *SGp = BP + (size_t)2 * Mb * 64;
+    const int32_t *SM = a.sm + d.sm_off;
+    const uint8_t *zl = lzc + d.band * 256;
+    uint64_t *Ncol = Nsh + lane;  // Ncol[r * 64]
+    const int nstripes = (h + 3) >> 2;
+    const uint64_t *Bp = BP + (size_t)p * 64;
+    const uint64_t *S0p = SP + (size_t)p * 64;
+    const bool has1 = p + 1 < P, has2 = p + 2 < P;
+    const uint64_t *S1p = SP + (size_t)(p + 1) * 64;
+    const uint64_t *S2p = SP + (size_t)(p + 2) * 64;
+    Emit em;
+    em.base = (uint32_t *)(a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h));
+    em.acc = 0;
+    em.n = 0;
+    int64_t dspp = 0;
+    int n_spp = 0, n_mrp = 0;
+    const bool spp = p < P - 1;
+    if (spp) {
+        // ---------------- significance propagation ----------------
+        for (int s = 0; s < nstripes; s++) {
+            const int r0 = s * 4, nr = min(4, h - r0);
+            uint64_t s1[6], sg[6], bt[4], n[4] = {0, 0, 0, 0}, mem[4];
+            ROWS6(s1, S1p[r]);
+            ROWS6(sg, SGp[r]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) bt[q] = (q < nr) ? Bp[r0 + q] : 0ull;
+            const uint64_t bfprev = (r0 > 0) ? (s1[0] | Ncol[(r0 - 1) * 64]) : 0ull;
+            for (;;) {
+                bool changed = false;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (q >= nr) { mem[q] = 0; continue; }
+                    uint64_t UPb = (q == 0) ? bfprev : (s1[q] | n[q - 1]);
+                    uint64_t UPa = (q == 0) ? bfprev : s1[q];
+                    uint64_t MIDb = s1[q + 1] | n[q], MIDa = s1[q + 1];
+                    uint64_t DNb = (q == 3) ? s1[5] : (s1[q + 2] | n[q + 1]);
+                    uint64_t DNa = s1[q + 2];
+                    mem[q] = ~s1[q + 1] & V & nbhd(UPb, UPa, MIDb, MIDa, DNb, DNa);
+                    uint64_t nn = mem[q] & bt[q];
+                    if (nn != n[q]) { n[q] = nn; changed = true; }
+                }
+                if (!changed) break;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (q < nr) Ncol[(r0 + q) * 64] = n[q];
+            uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
+            while (colmask) {
+                const int c = __ffsll((unsigned long long)colmask) - 1;
+                colmask &= colmask - 1;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (q >= nr || !bit(mem[q], c)) continue;
+                    uint64_t UPb = (q == 0) ? bfprev : (s1[q] | n[q - 1]);
+                    uint64_t UPa = (q == 0) ? bfprev : s1[q];
+                    uint64_t MIDb = s1[q + 1] | n[q], MIDa = s1[q + 1];
+                    uint64_t DNb = (q == 3) ? s1[5] : (s1[q + 2] | n[q + 1]);
+                    uint64_t DNa = s1[q + 2];
+                    int bv = (int)bit(bt[q], c);
+                    em.put(zl[pattern8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
+                    if (bv) {
+                        int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
+                        uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
+                        em.put(sp >> 1, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
+                        dspp += dist_gain(word & 0x7FFFFFFFu, p, lossless);
+                    }
+                }
+            }
+        }
+        n_spp = em.n;
+        em.align16();
+        // ---------------- magnitude refinement ----------------
+        for (int s = 0; s < nstripes; s++) {
+            const int r0 = s * 4, nr = min(4, h - r0);
+            uint64_t post[6], bt[4], mem[4], fr[4];
+            ROWS6(post, S1p[r] | Ncol[r * 64]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                bool in = q < nr;
+                bt[q] = in ? Bp[r0 + q] : 0ull;
+                uint64_t s1q = in ? S1p[r0 + q] : 0ull;
+                mem[q] = s1q & V;
+                fr[q] = s1q & ~((in && has2) ? S2p[r0 + q] : 0ull);
+            }
+            uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
+            while (colmask) {
+                const int c = __ffsll((unsigned long long)colmask) - 1;
+                colmask &= colmask - 1;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (q >= nr || !bit(mem[q], c)) continue;
+                    int ctx = 16;
+                    if (bit(fr[q], c))
+                        ctx = pattern8(post[q], post[q], post[q + 1], post[q + 1], post[q + 2], post[q + 2], c) ? 15 : 14;
+                    em.put(ctx, (int)bit(bt[q], c));
+                }
+            }
+        }
+        n_mrp = em.n - ((n_spp + 15) & ~15);
+        em.align16();
+    }
+    const int cup0 = em.n;
+    // ---------------- cleanup ----------------
+    for (int s = 0; s < nstripes; s++) {
+        const int r0 = s * 4, nr = min(4, h - r0);
+        uint64_t s1[6], post[6], s0[6], sg[6], bt[4], mem[4];
+        ROWS6(s1, has1 ? S1p[r] : 0ull);
+        ROWS6(post, s1[i] | (spp ? Ncol[r * 64] : 0ull));
+        ROWS6(s0, S0p[r]);
+        ROWS6(sg, SGp[r]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) bt[q] = (q < nr) ? Bp[r0 + q] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (q >= nr) { mem[q] = 0; continue; }
+            uint64_t c_spp = 0;
+            if (spp) {  // SPP membership with the final new-significance masks
+                uint64_t UPb = post[q], UPa = (q == 0) ? post[0] : s1[q];
+                uint64_t MIDb = post[q + 1], MIDa = s1[q + 1];
+                uint64_t DNb = (q == 3) ? s1[5] : post[q + 2];
+                uint64_t DNa = s1[q + 2];
+                c_spp = ~s1[q + 1] & V & nbhd(UPb, UPa, MIDb, MIDa, DNb, DNa);
+            }
+            mem[q] = ~s1[q + 1] & ~c_spp & V;
+        }
+        uint64_t rl = 0;
+        if (nr == 4) {
+            uint64_t z = (s0[0] << 1) | s0[0] | (s0[0] >> 1) | ((s0[1] | s0[2] | s0[3] | s0[4]) << 1) |
+                         ((post[1] | post[2] | post[3] | post[4]) >> 1) | (post[5] << 1) | post[5] |
+                         (post[5] >> 1);
+            rl = mem[0] & mem[1] & mem[2] & mem[3] & ~z;
+        }
+        uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
+        while (colmask) {
+            const int c = __ffsll((unsigned long long)colmask) - 1;
+            colmask &= colmask - 1;
+            int qstart = 0;
+            if (bit(rl, c)) {
+                int r = 4;
+#pragma unroll
+                for (int q = 3; q >= 0; q--)
+                    if (bit(bt[q], c)) r = q;
+                if (r == 4) {
+                    em.put(CX_RL, 0);
+                    continue;
+                }
+                em.put(CX_RL, 1);
+                em.put(CX_UNI, r >> 1);
+                em.put(CX_UNI, r & 1);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (q != r) continue;
+                    int sp = lsc[pattern_sign(s0[q], s0[q + 1], post[q + 1], post[q + 2], sg[q], sg[q + 1], sg[q + 2], c)];
+                    uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
+                    em.put(sp >> 1, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
+                }
+                qstart = r + 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (q < qstart || q >= nr || !bit(mem[q], c)) continue;
+                uint64_t UPb = s0[q], UPa = (q == 0) ? s0[0] : post[q];
+                uint64_t MIDb = s0[q + 1], MIDa = post[q + 1];
+                uint64_t DNb = (q == 3) ? post[5] : s0[q + 2];
+                uint64_t DNa = post[q + 2];
+                int bv = (int)bit(bt[q], c);
+                em.put(zl[pattern8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
+                if (bv) {
+                    int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
+                    uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
+                    em.put(sp >> 1, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
+                }
+            }
+        }
+    }
+    const int n_cup = em.n - cup0;
+    em.align16();
+    uint4 cnt;  // decisions per pass; pass streams start at 16-byte boundaries
+    cnt.x = (uint32_t)n_spp;
+    cnt.y = (uint32_t)n_mrp;
+    cnt.z = (uint32_t)n_cup;
+    cnt.w = 0;
+    a.counts[(size_t)b * 32 + k] = cnt;
+    a.dspp[(size_t)b * 32 + k] = dspp;
+}
+
+// --------------------------------------------------------------------------
+// MQ coder
+// --------------------------------------------------------------------------
+__constant__ uint16_t c_qe[47] = {
+    0x5601, 0x3401, 0x1801, 0x0AC1, 0x0521, 0x0221, 0x5601, 0x5401, 0x4801, 0x3801, 0x3001, 0x2401,
+    0x1C01, 0x1601, 0x5601, 0x5401, 0x5101, 0x4801, 0x3801, 0x3401, 0x3001, 0x2801, 0x2401, 0x2201,
+    0x1C01, 0x1801, 0x1601, 0x1401, 0x1201, 0x1101, 0x0AC1, 0x09C1, 0x08A1, 0x0521, 0x0441, 0x02A1,
+    0x0221, 0x0141, 0x0111, 0x0085, 0x0049, 0x0025, 0x0015, 0x0009, 0x0005, 0x0001, 0x5601};
+__constant__ uint8_t c_nmps[47] = {1,  2,  3,  4,  5,  38, 7,  8,  9,  10, 11, 12, 13, 29, 15, 16,
+                                   17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32,
+                                   33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 45, 46};
+__constant__ uint8_t c_nlps[47] = {1,  6,  9,  12, 29, 33, 6,  14, 14, 14, 17, 18, 20, 21, 14, 14,
+                                   15, 16, 17, 18, 19, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29,
+                                   30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 46};
+
+struct Mq {
+    uint32_t C, A, B;
+    int CT, bp, cap;
+    uint8_t *out;
+};
+
+__device__ __forceinline__ void mq_byteout(Mq &m) {
+    uint32_t B = m.B;
+    if (B != 0xFF && m.C >= 0x8000000u) {  // carry into the pending byte
+        B++;
+        m.C &= 0x7FFFFFFu;
+    }
+    if (m.bp >= 0 && m.bp < m.cap) m.out[m.bp] = (uint8_t)B;
+    m.bp++;
+    if (B == 0xFF) {
+        m.B = m.C >> 20;
+        m.C &= 0xFFFFFu;
+        m.CT = 7;
+    } else {
+        m.B = m.C >> 19;
+        m.C &= 0x7FFFFu;
+        m.CT = 8;
+    }
+}
+
+// Context state = the 32-bit table word of its current index (Qe | NMPS << 16 |
+// NLPS << 22 | SWITCH << 28) with the MPS symbol in bit 31.
+//
+// One decision, straight-line except for the (rare per lane) byte-out: the
+// CODEMPS/CODELPS procedures of Annex C.2 fold into one select -- the
+// interval keeps A-Qe exactly when "MPS" xor "conditional exchange" -- and the
+// context moves to NMPS/NLPS exactly when renormalisation happens.  `t` is the
+// context's state word (read ahead by the caller); returns the new state word.
+__device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint32_t *tab, const uint32_t d) {
+    const uint32_t qe = t & 0xFFFFu;
+    const uint32_t mps = t >> 31;
+    const uint32_t A1 = m.A - qe;
+    const bool isM = d == mps;
+    const bool keep = isM != (A1 < qe);
+    const uint32_t An = keep ? A1 : qe;
+    m.C += keep ? qe : 0u;
+    const bool ren = (!isM) || (A1 < 0x8000u);
+    const uint32_t idx = (t >> (isM ? 16 : 22)) & 63u;
+    const uint32_t nm = mps ^ ((isM ? 0u : 1u) & (t >> 28));
+    const uint32_t tw = tab[idx] | (nm << 31);
+    const int n = __clz(An) - 16;
+    m.A = An << n;
+    if (__builtin_expect(n < m.CT, 1)) {
+        m.C <<= n;
+        m.CT -= n;
+    } else {
+        int r = n;
+        do {
+            m.C <<= m.CT;
+            r -= m.CT;
+            mq_byteout(m);
+        } while (r >= m.CT);
+        m.C <<= r;
+        m.CT -= r;
+    }
+    return ren ? tw : t;
+}
+
+__device__ __forceinline__ int mq_flush(Mq &m) {
+    uint32_t tempc = m.C + m.A;
+    m.C |= 0xFFFFu;
+    if (m.C >= tempc) m.C -= 0x8000u;
+    m.C <<= m.CT;
+    mq_byteout(m);
+    m.C <<= m.CT;
+    mq_byteout(m);
+    if (m.B != 0xFF) {
+        if (m.bp >= 0 && m.bp < m.cap) m.out[m.bp] = (uint8_t)m.B;
+        m.bp++;
+    }
+    return m.bp;
+}
+
+// word k (0..3) of a 16-byte chunk, by value (no address taken: a dynamic
+// index into a local vector would be lowered to scratch memory)
+__device__ __forceinline__ uint32_t comp4(uint4 c, int k) {
+    const uint32_t lo = (k & 1) ? c.y : c.x;
+    const uint32_t hi = (k & 1) ? c.w : c.z;
+    return (k & 2) ? hi : lo;
+}
+
+// Code one decision with context state `t` (read ahead by the caller), store
+// the context's new state, and return the state of the next decision's
+// context: `nt` as read ahead, unless it is the same context.
+__device__ __forceinline__ uint32_t mq_dec(Mq &m, uint32_t *cx, const uint32_t *tab, const uint32_t byte,
+                                           const uint32_t t, const uint32_t nbyte, const uint32_t nt) {
+    const uint32_t tn = mq_step(m, t, tab, byte & 1u);
+    cx[(byte >> 1) * 64] = tn;
+    return ((nbyte >> 1) == (byte >> 1)) ? tn : nt;
+}
+
+// Up to 16 decisions of one chunk (`left` of them remain in the pass).  Byte
+// positions are compile-time after unrolling; the next decision's context
+// state is read one decision ahead (within the chunk).
+__device__ __forceinline__ bool mq_chunk16(Mq &m, uint32_t *cx, const uint32_t *tab, const uint4 cur,
+                                           int &left) {
+    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+    uint32_t t = cx[min((w[0] & 0xFFu) >> 1, 18u) * 64];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (j >= left) {
+            left = 0;
+            return true;
+        }
+        const uint32_t byte = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+        uint32_t nbyte = 0, nt = 0;
+        if (j < 15) {
+            nbyte = (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu;
+            nt = cx[min(nbyte >> 1, 18u) * 64];  // may be past the pass end
+        }
+        t = mq_dec(m, cx, tab, byte, t, nbyte, nt);
+    }
+    left -= 16;
+    return left <= 0;
+}
+
+// MQ-code one pass's decision stream (16-byte aligned, `n` decisions).  Two
+// chunk buffers alternate so each load has a whole chunk of coding to land
+// behind before it is used.
+__device__ __forceinline__ void mq_pass(Mq &m, uint32_t *cx, const uint32_t *tab, const uint4 *s4, int n) {
+    if (n <= 0) return;
+    uint4 ca = s4[0];
+    uint4 cb = s4[1];
+    int chunk = 0;
+    int left = n;
+    for (;;) {
+        if (mq_chunk16(m, cx, tab, ca, left)) break;
+        ca = s4[chunk + 2];
+        chunk++;
+        if (mq_chunk16(m, cx, tab, cb, left)) break;
+        cb = s4[chunk + 2];
+        chunk++;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
+    __shared__ uint32_t cxs[19 * 64];
+    __shared__ uint32_t mqt[48];
+    const int lane = threadIdx.x;
+    if (lane < 47)
+        mqt[lane] = (uint32_t)c_qe[lane] | ((uint32_t)c_nmps[lane] << 16) | ((uint32_t)c_nlps[lane] << 22) |
+                    ((uint32_t)(lane == 0 || lane == 6 || lane == 14) << 28);
+    __syncthreads();
+    // only the first `lanes` lanes of each wave take a block: fewer lanes per
+    // wave means less divergence in the serial coder and more waves per SIMD
+    if (lane >= a.lanes) return;
+    const int gi = blockIdx.x * a.lanes + lane;
+    if (gi >= a.nblocks) return;
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+    const uint64_t w0 = wall_clock64();
+    const int b = a.order[gi];
+    const BlockDesc d = a.blocks[b];
+    const int P = a.P[b];
+    if (P == 0) {
+        a.npasses[b] = 0;
+        a.lengths[b] = 0;
+        return;
+    }
+    uint32_t *cx = cxs + lane;
+#pragma unroll
+    for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];
+    cx[0] = mqt[4];
+    cx[CX_RL * 64] = mqt[3];
+    cx[CX_UNI * 64] = mqt[46];
+    Mq m;
+    m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
+    m.cap = (a.variant & 1) ? 0 : (int)d.out_cap;  // variant 1: timing probe without output stores
+    m.out = a.out + d.out_off;
+    int32_t *R = a.rates + (size_t)b * kMaxPasses;
+    int64_t *D = a.dists + (size_t)b * kMaxPasses;
+    const uint32_t cap = plane_stream_cap(d.w, d.h);
+    const uint8_t *sbase = a.stream + a.slot_off[b];
+    int np = 0;
+    for (int k = 0; k < P; k++) {
+        const int p = P - 1 - k;
+        const uint4 *s = (const uint4 *)(sbase + (size_t)k * cap);
+        const uint4 cnt = a.counts[(size_t)b * 32 + k];
+        const int64_t dspp = a.dspp[(size_t)b * 32 + k];
+        const int o_mrp = ((int)cnt.x + 15) & ~15;
+        const int o_cup = (o_mrp + (int)cnt.y + 15) & ~15;
+        if (k > 0) {
+            mq_pass(m, cx, mqt, s, (int)cnt.x);
+            R[np] = m.bp + 3;
+            D[np] = dspp;
+            np++;
+            mq_pass(m, cx, mqt, s + (o_mrp >> 4), (int)cnt.y);
+            R[np] = m.bp + 3;
+            D[np] = a.dref[(size_t)b * 32 + p];
+            np++;
+        }
+        mq_pass(m, cx, mqt, s + (o_cup >> 4), (int)cnt.z);
+        R[np] = m.bp + 3;
+        D[np] = a.dsig[(size_t)b * 32 + p] - dspp;
+        np++;
+    }
+    const int len = mq_flush(m);
+    if (len > m.cap && !(a.variant & 1)) atomicOr(a.err, 1);
+    R[np - 1] = len;
+    for (int i = 0; i < np; i++) {
+        int r = min(R[i], len);
+        if (r > 1 && r <= m.cap && m.out[r - 1] == 0xFF) r--;
+        R[i] = r;
+    }
+    a.npasses[b] = (uint8_t)np;
+    a.lengths[b] = len;
+    if (a.dbg) {  // debug census: decisions, shader cycles, 100 MHz ticks
+        int64_t ndec = 0;
+        for (int k = 0; k < P; k++) {
+            const uint4 c4 = a.counts[(size_t)b * 32 + k];
+            ndec += c4.x + c4.y + c4.z;
+        }
+        a.dbg[(size_t)b * 4 + 0] = ndec;
+        a.dbg[(size_t)b * 4 + 1] = (int64_t)(__builtin_amdgcn_s_memtime() - c0);
+        a.dbg[(size_t)b * 4 + 2] = (int64_t)(wall_clock64() - w0);
+        a.dbg[(size_t)b * 4 + 3] = gi;
+    }
+}
+
+void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
+    if (a.nitems) hipLaunchKernelGGL(k_t1_cm, dim3((a.nitems + 63) / 64), dim3(64), 0, st, a);
+}
+void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
+    if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + a.lanes - 1) / a.lanes), dim3(64), 0, st, a);
+}
+uint32_t t1_plane_stream_cap(int w, int h) { return plane_stream_cap(w, h); }
+
+}  // namespace jp2hip

@@ -485,7 +485,11 @@ static void mq_renorm(mqenc *m) {
     } while ((m->A & 0x8000) == 0);
 }
 
+static int64_t g_decisions; /* debug counter (oracle_debug_decisions) */
+int64_t oracle_debug_decisions(void) { int64_t v = g_decisions; g_decisions = 0; return v; }
+
 static void mq_encode(mqenc *m, int cx, int d) {
+    g_decisions++;
     int i = m->I[cx];
     uint32_t qe = QE[i];
     m->A -= qe;
@@ -984,8 +988,17 @@ static int code_tilecomp(encoder *E, tileinfo *T, int c, void *buf, int tw, int 
                             }
                             int cap = b->w * b->h * 8 + 256;
                             b->data = (uint8_t *)malloc((size_t)cap);
+                            int64_t dec0 = g_decisions;
                             int np = oracle_t1_encode(sm, b->w, b->h, band, rc->reversible, b->data, cap,
                                                       &b->len, b->rates, b->dd, &b->P);
+                            if (getenv("ORACLE_T1_STATS")) {
+                                FILE *sf = fopen(getenv("ORACLE_T1_STATS"), "a");
+                                if (sf) {
+                                    fprintf(sf, "%d %d %d %d %d %d %lld %d\n", c, d, band, b->w, b->h, b->P,
+                                            (long long)(g_decisions - dec0), b->len);
+                                    fclose(sf);
+                                }
+                            }
                             free(sm);
                             if (np < 0) return -1;
                             b->npasses = np;

@@ -75,6 +75,9 @@ int oracle_t1_encode(const int32_t *sm, int w, int h, int band, int lossless,
                      uint8_t *out_bytes, int cap, int *out_len,
                      int32_t *rates, int64_t *dists, int *nplanes);
 
+/* Debug: MQ decisions coded since the previous call (workload analysis). */
+int64_t oracle_debug_decisions(void);
+
 void oracle_free(void *p);
 const char *oracle_last_error(void);
 
