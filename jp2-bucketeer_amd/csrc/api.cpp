@@ -30,6 +30,7 @@ struct jp2hip_ctx {
     jp2hip::GpuEncoder gpu;
     jp2hip_config cfg;
     int threads = 1;
+    jp2hip::T2State t2;  // tier-2 arenas, reused call to call
 };
 
 namespace {
@@ -155,9 +156,10 @@ void default_recipe(jp2hip_recipe *r, int conversion) {
     r->comment = 1;
 }
 
-// The whole encode with the source already in device memory.
+// The whole encode with the source already in device memory.  On success
+// *out is a malloc'd buffer holding the complete file.
 int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *lay,
-                int conversion, const jp2hip_recipe *recipe, std::vector<uint8_t> &file,
+                int conversion, const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
                 jp2hip_stats *stats, double t_start, double h2d_ms) {
     using namespace jp2hip;
     if (conversion != JP2HIP_LOSSY && conversion != JP2HIP_LOSSLESS)
@@ -185,14 +187,22 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     in.data = nullptr;
     in.data_off = nullptr;
     in.threads = ctx->threads;
+    T2State &t2 = ctx->t2;
     double t2ms = 0;
     int iters = 0;
+    int64_t cs_bytes = 0;
     if (rc.rate_bpp <= 0.0) {
+        // lossless: layer l keeps every pass whose slope clears total >> (L-1-l)
         int64_t total = 0;
         for (int b = 0; b < nb; b++) total += len[b];
         for (int l = 0; l < L; l++) budgets[l] = total >> (L - 1 - l);
         if (!ctx->gpu.select(plan, budgets, h_nl, h_lrate, prof, st, err)) return fail(err);
         iters = 1;
+        in.nl = h_nl.data();
+        in.lrate = h_lrate.data();
+        const double t0 = now_ms();
+        cs_bytes = t2_headers(in, t2);
+        t2ms += now_ms() - t0;
     } else {
         const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
         int64_t budget = target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
@@ -203,15 +213,14 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
             iters++;
             in.nl = h_nl.data();
             in.lrate = h_lrate.data();
-            double t0 = now_ms();
-            int64_t size = t2_write(in, nullptr);
+            const double t0 = now_ms();
+            cs_bytes = t2_headers(in, t2);
             t2ms += now_ms() - t0;
-            if (size <= target) break;
-            budget -= (size - target) << it;  // exponential back-off, as the oracle
+            if (cs_bytes <= target) break;
+            budget -= (cs_bytes - target) << it;  // exponential back-off, as the oracle
         }
     }
-    in.nl = h_nl.data();
-    in.lrate = h_lrate.data();
+    // t2 now describes the final layer table; fetch the bytes it includes
     std::vector<int32_t> final_len((size_t)nb);
     std::vector<uint64_t> offs((size_t)nb);
     uint64_t total = 0;
@@ -221,16 +230,21 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         total += (uint64_t)final_len[b];
     }
     const uint8_t *data = nullptr;
-    double tg = now_ms();
+    const double tg = now_ms();
     if (!ctx->gpu.gather(plan, final_len, offs, total, &data, prof, st, err)) return fail(err);
-    double gather_ms = now_ms() - tg;
+    const double gather_ms = now_ms() - tg;
     in.data = data;
     in.data_off = offs.data();
-    double t0 = now_ms();
-    std::vector<uint8_t> cs;
-    t2_write(in, &cs);
-    wrap_file(plan, cs, file);
+    const double t0 = now_ms();
+    const size_t fh = file_header_bytes(plan);
+    const size_t n = fh + (size_t)cs_bytes;
+    uint8_t *buf = (uint8_t *)std::malloc(n);
+    if (!buf) return fail("out of memory");
+    write_file_header(plan, (uint64_t)cs_bytes, buf);
+    t2_emit(in, t2, buf + fh);
     t2ms += now_ms() - t0;
+    *out = buf;
+    *out_len = n;
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         stats->total_ms = now_ms() - t_start;
@@ -249,7 +263,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         ctx->gpu.t1_total_bytes(tb, tp);
         stats->t1_bytes = tb;
         stats->coded_passes = tp;
-        stats->out_bytes = (int64_t)file.size();
+        stats->out_bytes = (int64_t)n;
         stats->rate_iterations = iters;
     }
     return 0;
@@ -329,13 +343,7 @@ int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len, con
     *out_len = 0;
     double t0 = now_ms();
     std::lock_guard<std::mutex> lk(ctx->mu);
-    std::vector<uint8_t> file;
-    if (encode_core(ctx, d_src, src_len, layout, conversion, recipe, file, stats, t0, 0.0)) return -1;
-    *out = (uint8_t *)std::malloc(file.size() ? file.size() : 1);
-    if (!*out) return fail("out of memory");
-    std::memcpy(*out, file.data(), file.size());
-    *out_len = file.size();
-    return 0;
+    return encode_core(ctx, d_src, src_len, layout, conversion, recipe, out, out_len, stats, t0, 0.0);
 }
 
 int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int conversion,
@@ -352,13 +360,7 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
     double th = now_ms();
     if (!ctx->gpu.upload_source(tiff, len, err)) return fail(err);
     double h2d = now_ms() - th;
-    std::vector<uint8_t> file;
-    if (encode_core(ctx, ctx->gpu.source(), len, &lay, conversion, recipe, file, stats, t0, h2d)) return -1;
-    *out = (uint8_t *)std::malloc(file.size() ? file.size() : 1);
-    if (!*out) return fail("out of memory");
-    std::memcpy(*out, file.data(), file.size());
-    *out_len = file.size();
-    return 0;
+    return encode_core(ctx, ctx->gpu.source(), len, &lay, conversion, recipe, out, out_len, stats, t0, h2d);
 }
 
 int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path, const char *out_path, int conversion,

@@ -83,20 +83,56 @@ bool build_plan(Plan &plan, const jp2hip_recipe &rc, int w, int h, int nc, int b
 
 int prec_log2(const jp2hip_recipe &rc, int r, bool vertical);
 
-// Tier-2: writes the whole codestream (main header .. EOC).  `data` holds the
-// included bytes of every block back to back at `data_off[b]`.
+// Tier-2 inputs: the layer table chosen by PCRD.  `data` holds the included
+// bytes of every block back to back at `data_off[b]` (needed by t2_emit only).
 struct T2Input {
     const Plan *plan;
     const uint8_t *P;           // coded bit-planes per block
     const uint8_t *nl;          // [block][layers] cumulative passes per layer
     const int32_t *lrate;       // [block][layers] cumulative bytes per layer
-    const uint8_t *data;        // may be null for a size-only pass
+    const uint8_t *data;
     const uint64_t *data_off;
     int threads;
 };
-// returns total codestream size; fills out when out != nullptr
-int64_t t2_write(const T2Input &in, std::vector<uint8_t> *out);
 
-void wrap_file(const Plan &plan, const std::vector<uint8_t> &cs, std::vector<uint8_t> &file);
+struct TagNode {
+    int32_t parent, value, low;
+    int32_t known;
+};
+
+// Per-tile result of the header pass (reused across calls; no reallocation
+// once warm).
+struct T2Tile {
+    std::vector<uint8_t> hdr;        // coded packet headers, back to back
+    std::vector<uint32_t> hdr_end;   // per packet: end offset in hdr
+    std::vector<uint32_t> pk_len;    // per packet: SOP + header + EPH + body bytes
+    std::vector<uint32_t> pk_cend;   // per packet: end index (in triples) into contrib
+    std::vector<uint32_t> contrib;   // (block, first byte, end byte) of each body piece
+    std::vector<int32_t> tp_npk;     // packets per tile-part
+    std::vector<uint64_t> tp_bytes;  // Psot per tile-part
+    std::vector<int32_t> tree;       // tag-tree roots per (c, r, precinct, band)
+    uint64_t bytes = 0;
+};
+struct T2Worker {
+    std::vector<int32_t> lblock;     // indexed by block (a tile touches only its own)
+    std::vector<int8_t> incl;
+    std::vector<TagNode> nodes;
+};
+struct T2State {
+    std::vector<uint8_t> main;       // main header (SOC .. COM)
+    std::vector<T2Tile> tiles;
+    std::vector<T2Worker> workers;
+    int64_t total = 0;               // code-stream bytes, SOC .. EOC
+};
+
+// Header pass: codes every packet header, returns the code-stream size.
+int64_t t2_headers(const T2Input &in, T2State &st);
+// Writes the code-stream described by the last t2_headers() into dst
+// (st.total bytes); in.data / in.data_off must be set.
+void t2_emit(const T2Input &in, const T2State &st, uint8_t *dst);
+
+// JP2 / JPX boxes in front of the code-stream (0 bytes for raw J2K).
+size_t file_header_bytes(const Plan &plan);
+void write_file_header(const Plan &plan, uint64_t cs_bytes, uint8_t *dst);
 
 }  // namespace jp2hip
