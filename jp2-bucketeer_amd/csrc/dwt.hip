@@ -1,0 +1,436 @@
+// dwt.hip -- S1+S2+S3: TIFF ingest fused into the first DWT level, then the
+// remaining levels (ISO/IEC 15444-1 Annex F, vertical lifting then
+// horizontal lifting per level, symmetric extension, even start everywhere).
+//
+// Two kernels, both HBM-bound (B_dwt = C*[s + 4 + (8/3)(1 -
+// 4^-(L-1))] bytes per pixel):
+//
+//   k_dwt_band<REV, INGEST, RB>  one decomposition level.  A workgroup owns
+//       a band of RB output rows of one tile-component region; each thread
+//       holds one column's rows [r0-4, r0+RB+4) in registers for the
+//       vertical lifting (the 4-row halo on each side absorbs the lifting
+//       footprint, so the RB kept rows are exact) and vertical scaling; the
+//       kept rows go through LDS for horizontal lifting and scaling, and the
+//       de-interleaved write: HL/LH/HH go
+//       straight to their final Mallat position in `dst`, LL goes to a
+//       compact scratch plane that the next level reads.  With INGEST the
+//       band is read from the TIFF strips resident in HBM (level shift, RCT
+//       or ICT for this component), so level 1 reads s bytes/sample and
+//       writes 4: exactly the B_dwt term.
+//   k_dwt_tail<REV>  the remaining levels once a level's region fits in
+//       64 KiB of LDS (128x128 words): one workgroup per tile-component runs
+//       every remaining level in LDS and writes only final coefficients.
+//
+// Each coefficient is computed with the same expressions, in the same order,
+// as oracle/jp2_oracle.c (fwd53_1d / fwd97_1d, oracle_fdwt): the halo rows
+// reproduce exactly the values the full-column lifting would produce, so the
+// output is bit-identical (built with -ffp-contract=off).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gpu_encoder.h"
+
+namespace jp2hip {
+
+#define A97 (-1.586134342059924f)
+#define B97 (-0.052980118572961f)
+#define G97 (0.882911075530934f)
+#define D97 (0.443506852043971f)
+#define K97 (1.230174104914001f)
+#define INVK97 (0.8128930661159609f)
+
+constexpr int kDwtThreads = 256;
+constexpr int kDwtHalo = 4;           // >= lifting steps (9/7: 4, 5/3: 2)
+constexpr int kDwtLdsWords = 16384;   // 64 KiB: band workgroups for rows <= 1024, tail
+constexpr int kDwtLdsWordsWide = 32768;  // 128 KiB: band workgroups for rows of 2048 / 4096 (8 rows)
+
+// One lifting step over the LDS rows [ya, yb) of a column set (vertical) or
+// over one row (horizontal).  Sample i of parity `par` is updated from
+// i-1 / i+1 with symmetric extension at the true signal ends 0 and n-1; a
+// sample whose neighbour lies outside the staged window [ya, yb) is left
+// stale (it is halo and never written out).
+template <bool REV>
+__device__ __forceinline__ void lift_update(void *buf, int idx, int lidx, int ridx, int step) {
+    if (REV) {
+        int32_t *x = (int32_t *)buf;
+        if (step == 0) x[idx] -= (x[lidx] + x[ridx]) >> 1;
+        else x[idx] += (x[lidx] + x[ridx] + 2) >> 2;
+    } else {
+        float *x = (float *)buf;
+        const float cf = step == 0 ? A97 : (step == 1 ? B97 : (step == 2 ? G97 : D97));
+        float t = x[lidx] + x[ridx];
+        t = cf * t;
+        x[idx] = x[idx] + t;
+    }
+}
+
+// Vertical lifting of staged rows [ya, yb) (global row numbers, signal
+// length H), W columns, row stride ld, rows stored from LDS row 0 = ya.
+template <bool REV>
+__device__ __forceinline__ void lift_vertical(void *lds, int ya, int yb, int H, int W, int ld) {
+    if (H < 2) return;
+    const int nsteps = REV ? 2 : 4;
+    const int tid = threadIdx.x;
+    for (int s = 0; s < nsteps; s++) {
+        const int par = (s & 1) ? 0 : 1;  // odd rows first
+        const int y0 = ya + ((ya & 1) != par ? 1 : 0);
+        const int nr = (yb - y0 + 1) / 2;
+        for (int it = tid; it < nr * W; it += kDwtThreads) {
+            const int k = it / W, x = it - k * W;
+            const int y = y0 + 2 * k;
+            int l = y > 0 ? y - 1 : y + 1;
+            int r = y + 1 < H ? y + 1 : y - 1;
+            if (l < ya || r < ya || l >= yb || r >= yb) continue;
+            lift_update<REV>(lds, (y - ya) * ld + x, (l - ya) * ld + x, (r - ya) * ld + x, s);
+        }
+        __syncthreads();
+    }
+}
+
+// Horizontal lifting of `nrows` full rows of length W starting at LDS row
+// `row0`, row stride ld.
+template <bool REV>
+__device__ __forceinline__ void lift_horizontal(void *lds, int row0, int nrows, int W, int ld) {
+    if (W < 2) return;
+    const int nsteps = REV ? 2 : 4;
+    const int tid = threadIdx.x;
+    for (int s = 0; s < nsteps; s++) {
+        const int par = (s & 1) ? 0 : 1;
+        const int cnt = par ? W / 2 : (W + 1) / 2;
+        for (int it = tid; it < nrows * cnt; it += kDwtThreads) {
+            const int k = it / cnt, j = it - k * cnt;
+            const int x = par + 2 * j;
+            const int l = x > 0 ? x - 1 : x + 1;
+            const int r = x + 1 < W ? x + 1 : x - 1;
+            const int base = (row0 + k) * ld;
+            lift_update<REV>(lds, base + x, base + l, base + r, s);
+        }
+        __syncthreads();
+    }
+}
+
+struct DwtBandArgs {
+    // INGEST source: TIFF strips in HBM
+    const uint8_t *tif;
+    const uint64_t *strip_off;
+    int rps, img_w, nc, bits, planar, big_endian, mct, spp_strips;
+    int ntx, tile_w, tile_h;
+    // non-INGEST source: LL of the previous level (compact scratch planes)
+    const void *src;
+    int src_stride;
+    size_t src_tc;
+    // outputs
+    void *dst;            // final Mallat planes
+    int plane_w;
+    size_t plane;
+    void *ll;             // LL scratch (nullptr: LL is final, goes to dst)
+    int ll_stride;
+    size_t ll_tc;
+    const int32_t *tc_w, *tc_h;
+    int level, R;
+};
+
+__device__ __forceinline__ int32_t tiff_sample(const DwtBandArgs &a, size_t rowoff, int x, int c) {
+    size_t off = rowoff + (size_t)(a.planar == 2 ? x : x * a.nc + c) * (a.bits >> 3);
+    if (a.bits == 8) return (int32_t)a.tif[off];
+    uint32_t b0 = a.tif[off], b1 = a.tif[off + 1];
+    return (int32_t)(a.big_endian ? ((b0 << 8) | b1) : (b0 | (b1 << 8)));
+}
+
+// One source sample of the band kernel's staging loop, level-shifted and
+// colour-transformed (INGEST) or read from the previous level's LL.
+template <bool REV, bool INGEST>
+__device__ __forceinline__ int32_t band_load(const DwtBandArgs &a, int tc, int y, int x) {
+    if (!INGEST) {
+        const int32_t *s = (const int32_t *)a.src + (size_t)tc * a.src_tc;
+        return s[(size_t)y * a.src_stride + x];
+    }
+    const int c = tc % a.nc, t = tc / a.nc;
+    const int gx = (t % a.ntx) * a.tile_w + x, gy = (t / a.ntx) * a.tile_h + y;
+    const int32_t off = 1 << (a.bits - 1);
+    const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : a.nc) * (a.bits >> 3);
+    const int strip = gy / a.rps;
+    const size_t ly = (size_t)(gy - strip * a.rps) * row_bytes;
+    if (!(a.mct && a.nc >= 3 && c < 3)) {
+        const uint64_t so = a.strip_off[a.planar == 2 ? (size_t)c * a.spp_strips + strip : (size_t)strip];
+        const int32_t v = tiff_sample(a, so + ly, gx, c) - off;
+        return REV ? v : __float_as_int((float)v);
+    }
+    int32_t sm[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const uint64_t so = a.strip_off[a.planar == 2 ? (size_t)q * a.spp_strips + strip : (size_t)strip];
+        sm[q] = tiff_sample(a, so + ly, gx, q) - off;
+    }
+    if (REV) return c == 0 ? (sm[0] + 2 * sm[1] + sm[2]) >> 2 : (c == 1 ? sm[2] - sm[1] : sm[0] - sm[1]);
+    const float R = (float)sm[0], G = (float)sm[1], B = (float)sm[2];
+    float f;
+    if (c == 0) { f = 0.299f * R; f = f + 0.587f * G; f = f + 0.114f * B; }
+    else if (c == 1) { f = -0.16875f * R; f = f - 0.33126f * G; f = f + 0.5f * B; }
+    else { f = 0.5f * R; f = f - 0.41869f * G; f = f - 0.08131f * B; }
+    return __float_as_int(f);
+}
+
+// Vertical lifting of one column held in registers: v[i] is row
+// y = y0 + i (y0 even, rows outside [0, H) are don't-care).  Symmetric
+// extension at rows 0 and H-1; samples whose footprint leaves the window
+// come out wrong and are never kept.
+template <bool REV, int NR>
+__device__ __forceinline__ void lift_regs(int32_t (&v)[NR], int y0, int H) {
+    const int nsteps = REV ? 2 : 4;
+#pragma unroll
+    for (int s = 0; s < nsteps; s++) {
+        const int par = (s & 1) ? 0 : 1;
+#pragma unroll
+        for (int i = par; i < NR; i += 2) {
+            const int y = y0 + i;
+            const int im = i > 0 ? i - 1 : i + 1, ip = i + 1 < NR ? i + 1 : i - 1;
+            const int32_t l = (y == 0) ? v[ip] : v[im];
+            const int32_t r = (y + 1 < H) ? v[ip] : v[im];
+            if (REV) {
+                if (s == 0) v[i] -= (l + r) >> 1;
+                else v[i] += (l + r + 2) >> 2;
+            } else {
+                const float cf = s == 0 ? A97 : (s == 1 ? B97 : (s == 2 ? G97 : D97));
+                float t = __int_as_float(l) + __int_as_float(r);
+                t = cf * t;
+                v[i] = __float_as_int(__int_as_float(v[i]) + t);
+            }
+        }
+    }
+}
+
+// One decomposition level for a band of RB output rows of one
+// tile-component: vertical lifting in registers (thread = column, window of
+// RB + 2*halo rows), the RB kept rows through LDS for horizontal lifting,
+// then the de-interleaved write.
+template <bool REV, bool INGEST, int RB>
+__global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
+    extern __shared__ int32_t lds[];
+    constexpr int NR = RB + 2 * kDwtHalo;
+    const int tc = blockIdx.y;
+    const int sh = a.level - 1;
+    const int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh;
+    const int H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
+    const int r0 = blockIdx.x * RB;
+    if (r0 >= H) return;
+    const int nkeep = min(RB, H - r0);
+    const int y0 = r0 - kDwtHalo;
+    const int tid = threadIdx.x;
+    const int ld = W;
+    // ---- vertical: one column per thread, in registers ----
+    for (int x = tid; x < W; x += kDwtThreads) {
+        int32_t v[NR];
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const int y = y0 + i;
+            v[i] = (y >= 0 && y < H) ? band_load<REV, INGEST>(a, tc, y, x) : 0;
+        }
+        if (H > 1) {
+            lift_regs<REV, NR>(v, y0, H);
+            if (!REV) {
+#pragma unroll
+                for (int i = kDwtHalo; i < kDwtHalo + RB; i++)
+                    v[i] = __float_as_int(__int_as_float(v[i]) * ((i & 1) ? K97 : INVK97));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RB; i++)
+            if (i < nkeep) lds[i * ld + x] = v[kDwtHalo + i];
+    }
+    __syncthreads();
+    // ---- horizontal lifting of the kept rows ----
+    if (W > 1) {
+        const int nsteps = REV ? 2 : 4;
+        for (int s = 0; s < nsteps; s++) {
+            const int par = (s & 1) ? 0 : 1;
+            const int cnt = par ? W / 2 : (W + 1) / 2;
+            for (int k = 0; k < nkeep; k++) {
+                const int base = k * ld;
+                for (int j = tid; j < cnt; j += kDwtThreads) {
+                    const int x = par + 2 * j;
+                    const int l = x > 0 ? x - 1 : x + 1;
+                    const int r = x + 1 < W ? x + 1 : x - 1;
+                    lift_update<REV>(lds, base + x, base + l, base + r, s);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // ---- scale + de-interleave + write ----
+    const int nlv = (H + 1) / 2, nlh = (W + 1) / 2;
+    int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
+    int32_t *ll = a.ll ? (int32_t *)a.ll + (size_t)tc * a.ll_tc : nullptr;
+    for (int k = 0; k < nkeep; k++) {
+        const int y = r0 + k;
+        const bool ylo = (y & 1) == 0;
+        int32_t *drow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
+        int32_t *lrow = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : drow;
+        for (int j = tid; j < W; j += kDwtThreads) {
+            const bool lo = j < nlh;
+            const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
+            int32_t v = lds[k * ld + x];
+            if (!REV && W > 1) v = __float_as_int(__int_as_float(v) * (lo ? INVK97 : K97));
+            (lo ? lrow : drow)[j] = v;
+        }
+    }
+}
+
+struct DwtTailArgs {
+    const void *src;      // LL of level `level`-1, compact scratch planes
+    int src_stride;
+    size_t src_tc;
+    void *dst;
+    int plane_w;
+    size_t plane;
+    const int32_t *tc_w, *tc_h;
+    int level, levels;
+};
+
+// Levels level..levels of one tile-component, entirely in LDS.
+template <bool REV>
+__global__ void __launch_bounds__(kDwtThreads) k_dwt_tail(DwtTailArgs a) {
+    __shared__ int32_t lds[kDwtLdsWords];
+    const int tc = blockIdx.x;
+    const int tid = threadIdx.x;
+    int sh = a.level - 1;
+    int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh;
+    int H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
+    {
+        const int32_t *s = (const int32_t *)a.src + (size_t)tc * a.src_tc;
+        for (int it = tid; it < W * H; it += kDwtThreads) {
+            const int y = it / W, x = it - y * W;
+            lds[it] = s[(size_t)y * a.src_stride + x];
+        }
+    }
+    __syncthreads();
+    int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
+    for (int lv = a.level; lv <= a.levels; lv++) {
+        const int ld = W;
+        lift_vertical<REV>(lds, 0, H, H, W, ld);
+        if (!REV && H > 1) {
+            float *f = (float *)lds;
+            for (int it = tid; it < W * H; it += kDwtThreads) {
+                const int y = it / W;
+                f[it] = (y & 1) ? f[it] * K97 : f[it] * INVK97;
+            }
+            __syncthreads();
+        }
+        lift_horizontal<REV>(lds, 0, H, W, ld);
+        const int nlv = (H + 1) / 2, nlh = (W + 1) / 2;
+        const bool last = lv == a.levels;
+        // high bands (and the final LL) straight to HBM
+        for (int it = tid; it < W * H; it += kDwtThreads) {
+            const int y = it / W, j = it - y * W;
+            const bool lo = j < nlh, ylo = (y & 1) == 0;
+            if (lo && ylo && !last) continue;
+            const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
+            int32_t v = lds[y * ld + x];
+            if (!REV && W > 1) {
+                float f = __int_as_float(v);
+                f = lo ? f * INVK97 : f * K97;
+                v = __float_as_int(f);
+            }
+            dst[(size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w + j] = v;
+        }
+        if (last) break;
+        // compact LL (rows 2i, columns 2j, scaled) to the front of LDS
+        constexpr int kPer = kDwtLdsWords / 4 / kDwtThreads;  // LL <= 4096 words
+        int32_t keep[kPer];
+        const int nll = nlv * nlh;
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const int it = tid + q * kDwtThreads;
+            if (it < nll) {
+                const int i = it / nlh, j = it - i * nlh;
+                int32_t v = lds[(2 * i) * ld + 2 * j];
+                if (!REV && W > 1) v = __float_as_int(__int_as_float(v) * INVK97);
+                keep[q] = v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const int it = tid + q * kDwtThreads;
+            if (it < nll) lds[it] = keep[q];
+        }
+        __syncthreads();
+        W = nlh;
+        H = nlv;
+    }
+}
+
+template <bool REV, bool INGEST, int RB>
+static void launch_band(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    static bool wide = false;  // opt in to > 64 KiB dynamic LDS once per instance
+    if (lds > (size_t)kDwtLdsWords * 4 && !wide) {
+        (void)hipFuncSetAttribute((const void *)k_dwt_band<REV, INGEST, RB>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwtLdsWordsWide * 4);
+        wide = true;
+    }
+    hipLaunchKernelGGL((k_dwt_band<REV, INGEST, RB>), g, dim3(kDwtThreads), lds, st, a);
+}
+template <bool REV, bool INGEST>
+static void launch_band_rb(int RB, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    if (RB == 16) launch_band<REV, INGEST, 16>(g, lds, st, a);
+    else launch_band<REV, INGEST, 8>(g, lds, st, a);
+}
+
+// Ingest + all DWT levels on `st`.  Returns false on a launch error.
+bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
+    DwtBandArgs a;
+    a.tif = (const uint8_t *)p.tif;
+    a.strip_off = p.strip_off;
+    a.rps = p.rps; a.img_w = p.img_w; a.nc = p.nc; a.bits = p.bits; a.planar = p.planar;
+    a.big_endian = p.big_endian; a.mct = p.mct; a.spp_strips = p.spp_strips;
+    a.ntx = p.ntx; a.tile_w = p.tile_w; a.tile_h = p.tile_h;
+    a.dst = p.coef;
+    a.plane_w = p.plane_w;
+    a.plane = (size_t)p.plane_w * p.plane_h;
+    a.tc_w = p.tc_w; a.tc_h = p.tc_h;
+    const int ll_stride = (p.plane_w + 1) / 2;
+    const size_t ll_tc = (size_t)ll_stride * ((p.plane_h + 1) / 2);
+    void *scratch[2] = {p.scratch0, p.scratch1};
+    for (int lv = 1; lv <= p.levels; lv++) {
+        const int maxW = (p.plane_w + (1 << (lv - 1)) - 1) >> (lv - 1);
+        const int maxH = (p.plane_h + (1 << (lv - 1)) - 1) >> (lv - 1);
+        if (lv >= 2 && maxW * maxH <= kDwtLdsWords && ((maxW + 1) / 2) * ((maxH + 1) / 2) <= kDwtLdsWords / 4) {
+            DwtTailArgs t;
+            t.src = scratch[(lv - 1) & 1];
+            t.src_stride = ll_stride;
+            t.src_tc = ll_tc;
+            t.dst = p.coef;
+            t.plane_w = p.plane_w;
+            t.plane = a.plane;
+            t.tc_w = p.tc_w; t.tc_h = p.tc_h;
+            t.level = lv; t.levels = p.levels;
+            if (p.reversible) hipLaunchKernelGGL(k_dwt_tail<true>, dim3(p.ntc), dim3(kDwtThreads), 0, st, t);
+            else hipLaunchKernelGGL(k_dwt_tail<false>, dim3(p.ntc), dim3(kDwtThreads), 0, st, t);
+            return hipGetLastError() == hipSuccess;
+        }
+        // kept rows per workgroup: 16, or 8 for rows wider than 2048
+        const int R = maxW <= 2048 ? 16 : 8;
+        a.level = lv;
+        a.R = R;
+        a.src = scratch[(lv - 1) & 1];
+        a.src_stride = ll_stride;
+        a.src_tc = ll_tc;
+        a.ll = lv == p.levels ? nullptr : scratch[lv & 1];
+        a.ll_stride = ll_stride;
+        a.ll_tc = ll_tc;
+        const size_t lds = (size_t)R * maxW * 4;
+        dim3 g((maxH + R - 1) / R, p.ntc);
+        if (lv == 1) {
+            if (p.reversible) launch_band_rb<true, true>(R, g, lds, st, a);
+            else launch_band_rb<false, true>(R, g, lds, st, a);
+        } else {
+            if (p.reversible) launch_band_rb<true, false>(R, g, lds, st, a);
+            else launch_band_rb<false, false>(R, g, lds, st, a);
+        }
+        if (hipGetLastError() != hipSuccess) return false;
+    }
+    return true;
+}
+
+}  // namespace jp2hip

@@ -50,9 +50,21 @@ struct T1MqArgs {
     int *err;
     int lanes;  // blocks per wavefront (1..64)
     int64_t *dbg;  // optional per-block census [block][4] (debug)
-    int variant;   // debug timing probes (0 in production)
 };
+// fused ingest + DWT (dwt.hip)
+struct DwtLaunch {
+    const void *tif;
+    const uint64_t *strip_off;
+    int rps, img_w, nc, bits, planar, big_endian, mct, spp_strips;
+    int ntx, tile_w, tile_h, plane_w, plane_h, ntc, levels, reversible;
+    const int32_t *tc_w, *tc_h;
+    void *coef, *scratch0, *scratch1;  // scratch: ntc * ceil(plane_w/2) * ceil(plane_h/2) words each
+};
+bool launch_dwt(const DwtLaunch &p, hipStream_t st);
+
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st);
+void launch_t1_keys(int nblocks, const uint8_t *P, const uint4 *counts, uint32_t *keys, int32_t *vals,
+                    hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
 uint32_t t1_plane_stream_cap(int w, int h);
 
@@ -93,7 +105,7 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        segkey, segkey2, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
         dbgbuf;
     int nseg = 0;
     uint8_t *h_packed = nullptr;

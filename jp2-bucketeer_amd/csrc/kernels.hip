@@ -2,13 +2,11 @@
 //
 // Stage map (reference stage: kdu_compress invoked at
 // KakaduConverter.java:61-71):
-//   k_ingest     S1+S2  TIFF strips in HBM -> tile-component planes, level
-//                       shift, RCT (int) / ICT (fp32)
-//   k_dwt_vert   S3     one decomposition level, columns (LDS strip)
-//   k_dwt_horz   S3     one decomposition level, rows (LDS rows)
+//   (dwt.hip)    S1-S3  TIFF strips in HBM -> level shift, RCT (int) / ICT
+//                       (fp32) fused into DWT level 1; LDS-staged levels
+//   k_ingest     S1+S2  stand-alone ingest, used only when levels == 0
 //   k_quant      S4     deadzone quantiser + bit-plane masks via wave ballot
-//   k_t1         S5     EBCOT tier-1 + MQ coder, one lane per code-block,
-//                       bit-parallel (64-bit row mask) context modelling
+//   (t1.hip)     S5     EBCOT tier-1: context modelling + MQ coder
 //   k_hull/k_select S6  PCRD-opt convex hulls + global slope thresholds
 //   k_compact           gather the included bytes for the D2H copy
 // Tier-2 (S7/S8) runs on host threads (t2.cpp).
@@ -102,136 +100,6 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; c++)
             if (c < a.nc) o[base + (size_t)c * plane] = f[c];
-    }
-}
-
-// --------------------------------------------------------------------------
-// S3: DWT.  Lifting per Annex F; symmetric extension; even start everywhere.
-// --------------------------------------------------------------------------
-#define A97 (-1.586134342059924f)
-#define B97 (-0.052980118572961f)
-#define G97 (0.882911075530934f)
-#define D97 (0.443506852043971f)
-#define K97 (1.230174104914001f)
-#define INVK97 (0.8128930661159609f)
-
-// In-LDS lifting over n samples at x[i*stride], executed by `nthr` threads
-// with thread index t; `lines` independent signals at base offsets line*lstride.
-template <bool REV>
-__device__ __forceinline__ void lift_lines(void *buf, int n, int lines, int stride, int lstride,
-                                           int t, int nthr) {
-    if (n < 2) return;
-    int nodd = n / 2, neven = (n + 1) / 2;
-    if (REV) {
-        int32_t *x = (int32_t *)buf;
-        for (int it = t; it < nodd * lines; it += nthr) {
-            int line = it / nodd, i = 2 * (it - line * nodd) + 1;
-            int32_t *p = x + line * lstride;
-            int32_t l = p[(i - 1) * stride], r = (i + 1 < n) ? p[(i + 1) * stride] : l;
-            p[i * stride] -= (l + r) >> 1;
-        }
-        __syncthreads();
-        for (int it = t; it < neven * lines; it += nthr) {
-            int line = it / neven, i = 2 * (it - line * neven);
-            int32_t *p = x + line * lstride;
-            int32_t l = (i > 0) ? p[(i - 1) * stride] : p[(i + 1) * stride];
-            int32_t r = (i + 1 < n) ? p[(i + 1) * stride] : p[(i - 1) * stride];
-            p[i * stride] += (l + r + 2) >> 2;
-        }
-        __syncthreads();
-    } else {
-        float *x = (float *)buf;
-        const float coef[4] = {A97, B97, G97, D97};
-#pragma unroll
-        for (int step = 0; step < 4; step++) {
-            bool odd = (step & 1) == 0;
-            int cnt = odd ? nodd : neven;
-            float cf = coef[step];
-            for (int it = t; it < cnt * lines; it += nthr) {
-                int line = it / cnt, j = it - line * cnt;
-                int i = odd ? 2 * j + 1 : 2 * j;
-                float *p = x + line * lstride;
-                float l = (i > 0) ? p[(i - 1) * stride] : p[(i + 1) * stride];
-                float r = (i + 1 < n) ? p[(i + 1) * stride] : p[(i - 1) * stride];
-                float tt = l + r;
-                tt = cf * tt;
-                p[i * stride] = p[i * stride] + tt;
-            }
-            __syncthreads();
-        }
-    }
-}
-
-struct DwtArgs {
-    void *coef;
-    const int32_t *tc_w, *tc_h;
-    int plane_w, plane_h, level;  // level d >= 1 being produced
-    int cw;                       // columns per strip (vertical kernel)
-};
-
-// Columns: one workgroup = `cw` columns x all rows of the current region.
-template <bool REV>
-__global__ void __launch_bounds__(256) k_dwt_vert(DwtArgs a) {
-    extern __shared__ int32_t lds[];
-    int tc = blockIdx.y;
-    int sh = a.level - 1;
-    int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh, H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
-    int x0 = blockIdx.x * a.cw;
-    if (x0 >= W) return;
-    int ncol = min(a.cw, W - x0);
-    int ld = a.cw + 1;
-    int32_t *g = (int32_t *)a.coef + (size_t)tc * a.plane_w * a.plane_h + x0;
-    for (int it = threadIdx.x; it < H * a.cw; it += blockDim.x) {
-        int y = it / a.cw, c = it - y * a.cw;
-        if (c < ncol) lds[y * ld + c] = g[(size_t)y * a.plane_w + c];
-    }
-    __syncthreads();
-    lift_lines<REV>(lds, H, ncol, ld, 1, threadIdx.x, blockDim.x);
-    int nl = (H + 1) / 2;
-    for (int it = threadIdx.x; it < H * a.cw; it += blockDim.x) {
-        int y = it / a.cw, c = it - y * a.cw;
-        if (c >= ncol) continue;
-        int src = (y < nl) ? 2 * y : 2 * (y - nl) + 1;
-        int32_t v = lds[src * ld + c];
-        if (!REV && H > 1) {
-            float f = __int_as_float(v);
-            f = (y < nl) ? f * INVK97 : f * K97;
-            v = __float_as_int(f);
-        }
-        g[(size_t)y * a.plane_w + c] = v;
-    }
-}
-
-// Rows: one workgroup = 4 rows of the current region.
-template <bool REV>
-__global__ void __launch_bounds__(256) k_dwt_horz(DwtArgs a) {
-    extern __shared__ int32_t lds[];
-    constexpr int ROWS = 4;
-    int tc = blockIdx.y;
-    int sh = a.level - 1;
-    int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh, H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
-    int y0 = blockIdx.x * ROWS;
-    if (y0 >= H) return;
-    int nrow = min(ROWS, H - y0);
-    int ld = W + 1;
-    int32_t *g = (int32_t *)a.coef + (size_t)tc * a.plane_w * a.plane_h + (size_t)y0 * a.plane_w;
-    for (int it = threadIdx.x; it < nrow * W; it += blockDim.x) {
-        int r = it / W, x = it - r * W;
-        lds[r * ld + x] = g[(size_t)r * a.plane_w + x];
-    }
-    __syncthreads();
-    lift_lines<REV>(lds, W, nrow, 1, ld, threadIdx.x, blockDim.x);
-    int nl = (W + 1) / 2;
-    for (int it = threadIdx.x; it < nrow * W; it += blockDim.x) {
-        int r = it / W, x = it - r * W;
-        int src = (x < nl) ? 2 * x : 2 * (x - nl) + 1;
-        int32_t v = lds[r * ld + src];
-        if (!REV && W > 1) {
-            float f = __int_as_float(v);
-            f = (x < nl) ? f * INVK97 : f * K97;
-            v = __float_as_int(f);
-        }
-        g[(size_t)r * a.plane_w + x] = v;
     }
 }
 
@@ -496,7 +364,7 @@ static bool ensure(DevBuf &b, size_t count, std::string &err) {
 GpuEncoder::~GpuEncoder() {
     DevBuf *all[] = {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
-                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &segcnt, &segoff, &segkey,
+                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
                      &stream_buf, &counts, &dspp, &dbgbuf};
     for (DevBuf *b : all)
@@ -540,7 +408,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
                            bool profile, StageTimes &st, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     const int nb = (int)plan.blocks.size();
-    const bool rev = plan.rc.reversible != 0;
     size_t plane = (size_t)plan.plane_w * plan.plane_h;
     if (!ensure<int32_t>(coef, plane * plan.ntc, err)) return false;
     if (!ensure<BlockDesc>(blocks, nb, err)) return false;
@@ -568,7 +435,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<uint64_t>(strips, lay.nstrips, err)) return false;
 
     HIPCHECK(hipMemcpyAsync(blocks.ptr, plan.blocks.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(order.ptr, plan.t1_order.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync(weight.ptr, plan.weight.data(), sizeof(double) * nb, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, hipMemcpyHostToDevice, stream));
@@ -576,47 +442,44 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
 
     HIPCHECK(hipEventRecord(ev[0], stream));
-    // S1+S2
-    IngestArgs ia;
-    ia.src = (const uint8_t *)d_src;
-    ia.strip_off = (const uint64_t *)strips.ptr;
-    ia.rps = lay.rows_per_strip;
-    ia.w = plan.w; ia.h = plan.h; ia.nc = plan.nc; ia.bits = plan.bits;
-    ia.planar = lay.planar; ia.big_endian = lay.big_endian;
-    ia.mct = plan.rc.mct; ia.reversible = plan.rc.reversible;
-    ia.ntx = plan.ntx; ia.tile_w = plan.rc.tile_w; ia.tile_h = plan.rc.tile_h;
-    ia.plane_w = plan.plane_w; ia.plane_h = plan.plane_h;
-    ia.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
-    ia.coef = coef.ptr;
-    dim3 gi((plan.w + 63) / 64, (plan.h + 3) / 4);
-    hipLaunchKernelGGL(k_ingest, gi, dim3(256), 0, stream, ia);
-    HIPCHECK(hipGetLastError());
-    const char *dd = getenv("JP2HIP_DUMP_DIR");
-    if (dd && !dump(dd, "ingest.bin", coef, plane * plan.ntc * 4, err)) return false;
     HIPCHECK(hipEventRecord(ev[1], stream));
-    // S3
-    for (int lv = 1; lv <= plan.rc.levels; lv++) {
-        DwtArgs da;
-        da.coef = coef.ptr;
-        da.tc_w = (const int32_t *)tcw.ptr;
-        da.tc_h = (const int32_t *)tch.ptr;
-        da.plane_w = plan.plane_w;
-        da.plane_h = plan.plane_h;
-        da.level = lv;
-        int maxW = (plan.plane_w + (1 << (lv - 1)) - 1) >> (lv - 1);
-        int maxH = (plan.plane_h + (1 << (lv - 1)) - 1) >> (lv - 1);
-        int cw = std::max(1, std::min(64, 8192 / std::max(1, maxH)));
-        da.cw = cw;
-        size_t lds_v = (size_t)maxH * (cw + 1) * 4;
-        dim3 gv((maxW + cw - 1) / cw, plan.ntc);
-        if (rev) hipLaunchKernelGGL(k_dwt_vert<true>, gv, dim3(256), lds_v, stream, da);
-        else hipLaunchKernelGGL(k_dwt_vert<false>, gv, dim3(256), lds_v, stream, da);
+    const char *dd = getenv("JP2HIP_DUMP_DIR");
+    if (plan.rc.levels == 0) {
+        // S1+S2 only: no decomposition
+        IngestArgs ia;
+        ia.src = (const uint8_t *)d_src;
+        ia.strip_off = (const uint64_t *)strips.ptr;
+        ia.rps = lay.rows_per_strip;
+        ia.w = plan.w; ia.h = plan.h; ia.nc = plan.nc; ia.bits = plan.bits;
+        ia.planar = lay.planar; ia.big_endian = lay.big_endian;
+        ia.mct = plan.rc.mct; ia.reversible = plan.rc.reversible;
+        ia.ntx = plan.ntx; ia.tile_w = plan.rc.tile_w; ia.tile_h = plan.rc.tile_h;
+        ia.plane_w = plan.plane_w; ia.plane_h = plan.plane_h;
+        ia.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
+        ia.coef = coef.ptr;
+        dim3 gi((plan.w + 63) / 64, (plan.h + 3) / 4);
+        hipLaunchKernelGGL(k_ingest, gi, dim3(256), 0, stream, ia);
         HIPCHECK(hipGetLastError());
-        size_t lds_h = (size_t)4 * (maxW + 1) * 4;
-        dim3 gh((maxH + 3) / 4, plan.ntc);
-        if (rev) hipLaunchKernelGGL(k_dwt_horz<true>, gh, dim3(256), lds_h, stream, da);
-        else hipLaunchKernelGGL(k_dwt_horz<false>, gh, dim3(256), lds_h, stream, da);
-        HIPCHECK(hipGetLastError());
+    } else {
+        // S1+S2+S3 fused: ingest inside DWT level 1 (dwt.hip)
+        const size_t llw = (size_t)((plan.plane_w + 1) / 2) * ((plan.plane_h + 1) / 2) * plan.ntc;
+        if (!ensure<int32_t>(llbuf0, llw, err) || !ensure<int32_t>(llbuf1, llw, err)) return false;
+        DwtLaunch dl;
+        dl.tif = d_src;
+        dl.strip_off = (const uint64_t *)strips.ptr;
+        dl.rps = lay.rows_per_strip;
+        dl.img_w = plan.w; dl.nc = plan.nc; dl.bits = plan.bits;
+        dl.planar = lay.planar; dl.big_endian = lay.big_endian; dl.mct = plan.rc.mct;
+        dl.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
+        dl.ntx = plan.ntx; dl.tile_w = plan.rc.tile_w; dl.tile_h = plan.rc.tile_h;
+        dl.plane_w = plan.plane_w; dl.plane_h = plan.plane_h; dl.ntc = plan.ntc;
+        dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
+        dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
+        dl.coef = coef.ptr; dl.scratch0 = llbuf0.ptr; dl.scratch1 = llbuf1.ptr;
+        if (!launch_dwt(dl, stream)) {
+            err = std::string("DWT launch failed: ") + hipGetErrorString(hipGetLastError());
+            return false;
+        }
     }
     HIPCHECK(hipEventRecord(ev[2], stream));
     if (dd && !dump(dd, "dwt.bin", coef, plane * plan.ntc * 4, err)) return false;
@@ -675,6 +538,20 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ca.lossless = plan.rc.reversible;
     launch_t1_cm(ca, stream);
     HIPCHECK(hipGetLastError());
+    // MQ lane order: blocks by decreasing decision count
+    if (!ensure<uint32_t>(ordkey, nb, err) || !ensure<uint32_t>(ordkey2, nb, err) || !ensure<int32_t>(ordval, nb, err))
+        return false;
+    launch_t1_keys(nb, (const uint8_t *)P.ptr, (const uint4 *)counts.ptr, (uint32_t *)ordkey.ptr,
+                   (int32_t *)ordval.ptr, stream);
+    HIPCHECK(hipGetLastError());
+    if (nb) {
+        size_t tb = 0;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (uint32_t *)ordkey.ptr, (uint32_t *)ordkey2.ptr,
+                                                    (int32_t *)ordval.ptr, (int32_t *)order.ptr, nb, 0, 32, stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp.ptr, tb, (uint32_t *)ordkey.ptr, (uint32_t *)ordkey2.ptr,
+                                                    (int32_t *)ordval.ptr, (int32_t *)order.ptr, nb, 0, 32, stream));
+    }
     HIPCHECK(hipEventRecord(ev[11], stream));
     T1MqArgs ma;
     ma.blocks = (const BlockDesc *)blocks.ptr;
@@ -696,10 +573,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     {
         const char *e = getenv("JP2HIP_MQ_LANES");
         ma.lanes = std::max(1, std::min(64, e ? atoi(e) : 8));
-    }
-    {
-        const char *e = getenv("JP2HIP_MQ_VARIANT");
-        ma.variant = e ? atoi(e) : 0;
     }
     ma.dbg = nullptr;
     if (dd) {

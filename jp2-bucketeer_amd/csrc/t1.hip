@@ -68,26 +68,6 @@ __device__ __forceinline__ int sc_lut(int pat) {
 
 __device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m >> c) & 1u; }
 
-// 8-neighbour pattern of a sample at column c.  Neighbour rows come as a
-// "before" mask (positions already visited in this pass) and an "after" mask.
-// up: UPb (UL,U) UPa (UR); mid: MIDb (L) MIDa (R); down: DNb (DL) DNa (D,DR)
-__device__ __forceinline__ int pattern8(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
-                                        uint64_t DNb, uint64_t DNa, int c) {
-    return (int)(bit(UPb << 1, c) | (bit(UPb, c) << 1) | (bit(UPa >> 1, c) << 2) |
-                 (bit(MIDb << 1, c) << 3) | (bit(MIDa >> 1, c) << 4) | (bit(DNb << 1, c) << 5) |
-                 (bit(DNa, c) << 6) | (bit(DNa >> 1, c) << 7));
-}
-__device__ __forceinline__ int pattern_sign(uint64_t UPb, uint64_t MIDb, uint64_t MIDa, uint64_t DNa,
-                                            uint64_t sgU, uint64_t sgM, uint64_t sgD, int c) {
-    return (int)(bit(MIDb << 1, c) | (bit(sgM << 1, c) << 1) | (bit(MIDa >> 1, c) << 2) |
-                 (bit(sgM >> 1, c) << 3) | (bit(UPb, c) << 4) | (bit(sgU, c) << 5) |
-                 (bit(DNa, c) << 6) | (bit(sgD, c) << 7));
-}
-__device__ __forceinline__ uint64_t nbhd(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
-                                         uint64_t DNb, uint64_t DNa) {
-    return (UPb << 1) | UPb | (UPa >> 1) | (MIDb << 1) | (MIDa >> 1) | (DNb << 1) | DNa | (DNa >> 1);
-}
-
 // bytes reserved per (block, plane) for the three passes' decisions:
 // at most w*h coding decisions + w*h sign decisions + 3 per run-length column
 // (each pass starts on a 16-byte boundary; the MQ kernel reads up to two
@@ -96,26 +76,57 @@ __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
     return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
 }
 
-// decision stream writer: byte = (context << 1) | decision, packed 4 per word
-struct Emit {
-    uint32_t *base;
-    uint32_t acc;
+// 3-bit window of mask m around column c: bit0 = column c-1, bit1 = c,
+// bit2 = c+1 (columns outside 0..63 read as 0)
+__device__ __forceinline__ uint32_t win3(uint64_t m, int c) {
+    return (uint32_t)(c == 0 ? (m << 1) : (m >> (c - 1))) & 7u;
+}
+
+// Zero-coding pattern (bits UL U UR L R DL D DR) of the sample at column c
+// from the "visited" (b) and "not yet visited" (a) masks of the rows above,
+// at and below it.
+__device__ __forceinline__ uint32_t pat8(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
+                                         uint64_t DNb, uint64_t DNa, int c) {
+    const uint32_t ub = win3(UPb, c), ua = win3(UPa, c), mb = win3(MIDb, c), ma = win3(MIDa, c);
+    const uint32_t db = win3(DNb, c), da = win3(DNa, c);
+    return (ub & 3u) | (ua & 4u) | ((mb & 1u) << 3) | ((ma & 4u) << 2) | ((db & 1u) << 5) | ((da & 6u) << 5);
+}
+// Sign-coding pattern Lsig Lneg Rsig Rneg Usig Uneg Dsig Dneg.
+__device__ __forceinline__ uint32_t pats(uint64_t UPb, uint64_t MIDb, uint64_t MIDa, uint64_t DNa, uint64_t sgU,
+                                         uint64_t sgM, uint64_t sgD, int c) {
+    const uint32_t mb = win3(MIDb, c), ma = win3(MIDa, c), sm = win3(sgM, c);
+    return (mb & 1u) | ((sm & 1u) << 1) | ((ma & 4u)) | ((sm & 4u) << 1) | (bit(UPb, c) << 4) |
+           (bit(sgU, c) << 5) | (bit(DNa, c) << 6) | (bit(sgD, c) << 7);
+}
+__device__ __forceinline__ uint64_t nbhd(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
+                                         uint64_t DNb, uint64_t DNa) {
+    return (UPb << 1) | UPb | (UPa >> 1) | (MIDb << 1) | (MIDa >> 1) | (DNb << 1) | DNa | (DNa >> 1);
+}
+
+// A lane's decisions inside one stripe (<= 10), as bytes (context << 1) | d.
+struct LaneDec {
+    uint64_t lo, hi;
     int n;
-    __device__ __forceinline__ void put(int cx, int d) {
-        acc |= (uint32_t)((cx << 1) | d) << ((n & 3) * 8);
+    __device__ __forceinline__ void put(uint32_t cx, uint32_t d) {
+        const uint64_t byte = (uint64_t)((cx << 1) | d);
+        if (n < 8) lo |= byte << (n * 8);
+        else hi |= byte << ((n - 8) * 8);
         n++;
-        if ((n & 3) == 0) {
-            base[(n >> 2) - 1] = acc;
-            acc = 0;
-        }
-    }
-    // close the current pass: flush the partial word, next pass at 16 bytes
-    __device__ __forceinline__ void align16() {
-        if (n & 3) base[n >> 2] = acc;
-        acc = 0;
-        n = (n + 15) & ~15;
     }
 };
+
+// Stripe hand-off: the lanes' decisions go out in column order (lane c =
+// column c): exclusive prefix of the per-lane counts over the wave, then
+// each lane stores its bytes.  Returns the stripe's decision count.
+__device__ __forceinline__ int flush_stripe(uint8_t *out, int base, const LaneDec &e, int lane) {
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t b0 = __ballot(e.n & 1), b1 = __ballot(e.n & 2), b2 = __ballot(e.n & 4), b3 = __ballot(e.n & 8);
+    const int excl = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt) + 8 * __popcll(b3 & lt);
+    const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3);
+    uint8_t *o = out + base + excl;
+    for (int i = 0; i < e.n; i++) o[i] = (uint8_t)(i < 8 ? (e.lo >> (i * 8)) : (e.hi >> ((i - 8) * 8)));
+    return total;
+}
 
 #define ROWS6(dst, expr)                                  \
     _Pragma("unroll") for (int i = 0; i < 6; i++) {       \
@@ -123,15 +134,27 @@ struct Emit {
         dst[i] = (r >= 0 && r < h) ? (expr) : 0ull;       \
     }
 
-__global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
-    __shared__ uint64_t Nsh[64 * 64];
+// Context modelling: one wavefront per (code-block, bit-plane) item, lane =
+// column.  The stripe's significance state is a handful of 64-bit row masks,
+// identical in every lane (wave-uniform: SALU-friendly); each lane forms the
+// contexts of its own column's <= 4 samples from them, and the stripe's
+// decisions are laid out in scan order (column-major) by a wave prefix sum.
+//   SPP: membership is the least fixed point of the causal neighbourhood
+//        rule over the stripe's masks (new significance N feeds the samples
+//        visited after it);
+//   MRP: neighbours see the post-SPP state S[p+1] | N;
+//   CUP: visited neighbours see S[p], the others S[p+1] | N (closed form).
+constexpr int kCmWaves = 4;  // items per workgroup
+__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
+    __shared__ uint64_t Nsh[kCmWaves][64];
     __shared__ uint8_t lzc[4 * 256];
     __shared__ uint8_t lsc[256];
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 1024; i += 64) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
-    for (int i = lane; i < 256; i += 64) lsc[i] = (uint8_t)sc_lut(i);
+    for (int i = threadIdx.x; i < 1024; i += 64 * kCmWaves) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
+    for (int i = threadIdx.x; i < 256; i += 64 * kCmWaves) lsc[i] = (uint8_t)sc_lut(i);
     __syncthreads();
-    const int gi = blockIdx.x * 64 + lane;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gi = blockIdx.x * kCmWaves + wv;
     if (gi >= a.nitems) return;
     const int2 item = a.items[gi];
     const int b = item.x, p = item.y;
@@ -140,28 +163,27 @@ __global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
     const int k = P - 1 - p;  // plane index counted from the block's top plane
     const bool lossless = a.lossless != 0;
     const int w = d.w, h = d.h, Mb = d.Mb;
+    const int c = lane;
     const uint64_t V = (w >= 64) ? ~0ull : ((1ull << w) - 1ull);
     const uint64_t *BP = a.bp + d.bp_off;
     const uint64_t *SP = BP + (size_t)Mb * 64;
     const uint64_t *SGp = BP + (size_t)2 * Mb * 64;
     const int32_t *SM = a.sm + d.sm_off;
     const uint8_t *zl = lzc + d.band * 256;
-    uint64_t *Ncol = Nsh + lane;  // Ncol[r * 64]
+    uint64_t *N = Nsh[wv];
     const int nstripes = (h + 3) >> 2;
     const uint64_t *Bp = BP + (size_t)p * 64;
     const uint64_t *S0p = SP + (size_t)p * 64;
     const bool has1 = p + 1 < P, has2 = p + 2 < P;
     const uint64_t *S1p = SP + (size_t)(p + 1) * 64;
     const uint64_t *S2p = SP + (size_t)(p + 2) * 64;
-    Emit em;
-    em.base = (uint32_t *)(a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h));
-    em.acc = 0;
-    em.n = 0;
+    uint8_t *out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
     int64_t dspp = 0;
-    int n_spp = 0, n_mrp = 0;
+    int n_spp = 0, n_mrp = 0, pos = 0;
     const bool spp = p < P - 1;
     if (spp) {
         // ---------------- significance propagation ----------------
+        uint64_t nprev = 0;
         for (int s = 0; s < nstripes; s++) {
             const int r0 = s * 4, nr = min(4, h - r0);
             uint64_t s1[6], sg[6], bt[4], n[4] = {0, 0, 0, 0}, mem[4];
@@ -169,7 +191,7 @@ __global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
             ROWS6(sg, SGp[r]);
 #pragma unroll
             for (int q = 0; q < 4; q++) bt[q] = (q < nr) ? Bp[r0 + q] : 0ull;
-            const uint64_t bfprev = (r0 > 0) ? (s1[0] | Ncol[(r0 - 1) * 64]) : 0ull;
+            const uint64_t bfprev = (r0 > 0) ? (s1[0] | nprev) : 0ull;
             for (;;) {
                 bool changed = false;
 #pragma unroll
@@ -188,37 +210,36 @@ __global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (q < nr) Ncol[(r0 + q) * 64] = n[q];
-            uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
-            while (colmask) {
-                const int c = __ffsll((unsigned long long)colmask) - 1;
-                colmask &= colmask - 1;
+                if (q < nr) N[r0 + q] = n[q];
+            nprev = n[3];
+            LaneDec e{0, 0, 0};
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (q >= nr || !bit(mem[q], c)) continue;
-                    uint64_t UPb = (q == 0) ? bfprev : (s1[q] | n[q - 1]);
-                    uint64_t UPa = (q == 0) ? bfprev : s1[q];
-                    uint64_t MIDb = s1[q + 1] | n[q], MIDa = s1[q + 1];
-                    uint64_t DNb = (q == 3) ? s1[5] : (s1[q + 2] | n[q + 1]);
-                    uint64_t DNa = s1[q + 2];
-                    int bv = (int)bit(bt[q], c);
-                    em.put(zl[pattern8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
-                    if (bv) {
-                        int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
-                        uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
-                        em.put(sp >> 1, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
-                        dspp += dist_gain(word & 0x7FFFFFFFu, p, lossless);
-                    }
+            for (int q = 0; q < 4; q++) {
+                if (q >= nr || !bit(mem[q], c)) continue;
+                uint64_t UPb = (q == 0) ? bfprev : (s1[q] | n[q - 1]);
+                uint64_t UPa = (q == 0) ? bfprev : s1[q];
+                uint64_t MIDb = s1[q + 1] | n[q], MIDa = s1[q + 1];
+                uint64_t DNb = (q == 3) ? s1[5] : (s1[q + 2] | n[q + 1]);
+                uint64_t DNa = s1[q + 2];
+                const uint32_t bv = bit(bt[q], c);
+                e.put(zl[pat8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
+                if (bv) {
+                    const uint32_t sp = lsc[pats(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
+                    const uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
+                    e.put(sp >> 1, (word >> 31) ^ (sp & 1u));
+                    dspp += dist_gain(word & 0x7FFFFFFFu, p, lossless);
                 }
             }
+            pos += flush_stripe(out, pos, e, lane);
         }
-        n_spp = em.n;
-        em.align16();
+        n_spp = pos;
+        pos = (pos + 15) & ~15;
+        const int mrp0 = pos;
         // ---------------- magnitude refinement ----------------
         for (int s = 0; s < nstripes; s++) {
             const int r0 = s * 4, nr = min(4, h - r0);
             uint64_t post[6], bt[4], mem[4], fr[4];
-            ROWS6(post, S1p[r] | Ncol[r * 64]);
+            ROWS6(post, S1p[r] | N[r]);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 bool in = q < nr;
@@ -227,30 +248,26 @@ __global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
                 mem[q] = s1q & V;
                 fr[q] = s1q & ~((in && has2) ? S2p[r0 + q] : 0ull);
             }
-            uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
-            while (colmask) {
-                const int c = __ffsll((unsigned long long)colmask) - 1;
-                colmask &= colmask - 1;
+            LaneDec e{0, 0, 0};
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (q >= nr || !bit(mem[q], c)) continue;
-                    int ctx = 16;
-                    if (bit(fr[q], c))
-                        ctx = pattern8(post[q], post[q], post[q + 1], post[q + 1], post[q + 2], post[q + 2], c) ? 15 : 14;
-                    em.put(ctx, (int)bit(bt[q], c));
-                }
+            for (int q = 0; q < 4; q++) {
+                if (q >= nr || !bit(mem[q], c)) continue;
+                uint32_t ctx = 16;
+                if (bit(fr[q], c)) ctx = pat8(post[q], post[q], post[q + 1], post[q + 1], post[q + 2], post[q + 2], c) ? 15 : 14;
+                e.put(ctx, bit(bt[q], c));
             }
+            pos += flush_stripe(out, pos, e, lane);
         }
-        n_mrp = em.n - ((n_spp + 15) & ~15);
-        em.align16();
+        n_mrp = pos - mrp0;
+        pos = (pos + 15) & ~15;
     }
-    const int cup0 = em.n;
+    const int cup0 = pos;
     // ---------------- cleanup ----------------
     for (int s = 0; s < nstripes; s++) {
         const int r0 = s * 4, nr = min(4, h - r0);
         uint64_t s1[6], post[6], s0[6], sg[6], bt[4], mem[4];
         ROWS6(s1, has1 ? S1p[r] : 0ull);
-        ROWS6(post, s1[i] | (spp ? Ncol[r * 64] : 0ull));
+        ROWS6(post, s1[i] | (spp ? N[r] : 0ull));
         ROWS6(s0, S0p[r]);
         ROWS6(sg, SGp[r]);
 #pragma unroll
@@ -275,58 +292,58 @@ __global__ void __launch_bounds__(64) k_t1_cm(T1CmArgs a) {
                          (post[5] >> 1);
             rl = mem[0] & mem[1] & mem[2] & mem[3] & ~z;
         }
-        uint64_t colmask = mem[0] | mem[1] | mem[2] | mem[3];
-        while (colmask) {
-            const int c = __ffsll((unsigned long long)colmask) - 1;
-            colmask &= colmask - 1;
-            int qstart = 0;
-            if (bit(rl, c)) {
-                int r = 4;
+        LaneDec e{0, 0, 0};
+        int qstart = 0;
+        if (bit(rl, c)) {
+            int r = 4;
 #pragma unroll
-                for (int q = 3; q >= 0; q--)
-                    if (bit(bt[q], c)) r = q;
-                if (r == 4) {
-                    em.put(CX_RL, 0);
-                    continue;
-                }
-                em.put(CX_RL, 1);
-                em.put(CX_UNI, r >> 1);
-                em.put(CX_UNI, r & 1);
+            for (int q = 3; q >= 0; q--)
+                if (bit(bt[q], c)) r = q;
+            if (r == 4) {
+                e.put(CX_RL, 0);
+                qstart = 4;
+            } else {
+                e.put(CX_RL, 1);
+                e.put(CX_UNI, (uint32_t)r >> 1);
+                e.put(CX_UNI, (uint32_t)r & 1u);
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     if (q != r) continue;
-                    int sp = lsc[pattern_sign(s0[q], s0[q + 1], post[q + 1], post[q + 2], sg[q], sg[q + 1], sg[q + 2], c)];
-                    uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
-                    em.put(sp >> 1, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
+                    const uint32_t sp = lsc[pats(s0[q], s0[q + 1], post[q + 1], post[q + 2], sg[q], sg[q + 1], sg[q + 2], c)];
+                    const uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
+                    e.put(sp >> 1, (word >> 31) ^ (sp & 1u));
                 }
                 qstart = r + 1;
             }
+        }
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (q < qstart || q >= nr || !bit(mem[q], c)) continue;
-                uint64_t UPb = s0[q], UPa = (q == 0) ? s0[0] : post[q];
-                uint64_t MIDb = s0[q + 1], MIDa = post[q + 1];
-                uint64_t DNb = (q == 3) ? post[5] : s0[q + 2];
-                uint64_t DNa = post[q + 2];
-                int bv = (int)bit(bt[q], c);
-                em.put(zl[pattern8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
-                if (bv) {
-                    int sp = lsc[pattern_sign(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
-                    uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
-                    em.put(sp >> 1, (int)((word >> 31) ^ (uint32_t)(sp & 1)));
-                }
+        for (int q = 0; q < 4; q++) {
+            if (q < qstart || q >= nr || !bit(mem[q], c)) continue;
+            uint64_t UPb = s0[q], UPa = (q == 0) ? s0[0] : post[q];
+            uint64_t MIDb = s0[q + 1], MIDa = post[q + 1];
+            uint64_t DNb = (q == 3) ? post[5] : s0[q + 2];
+            uint64_t DNa = post[q + 2];
+            const uint32_t bv = bit(bt[q], c);
+            e.put(zl[pat8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
+            if (bv) {
+                const uint32_t sp = lsc[pats(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
+                const uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
+                e.put(sp >> 1, (word >> 31) ^ (sp & 1u));
             }
         }
+        pos += flush_stripe(out, pos, e, lane);
     }
-    const int n_cup = em.n - cup0;
-    em.align16();
-    uint4 cnt;  // decisions per pass; pass streams start at 16-byte boundaries
-    cnt.x = (uint32_t)n_spp;
-    cnt.y = (uint32_t)n_mrp;
-    cnt.z = (uint32_t)n_cup;
-    cnt.w = 0;
-    a.counts[(size_t)b * 32 + k] = cnt;
-    a.dspp[(size_t)b * 32 + k] = dspp;
+    const int n_cup = pos - cup0;
+    dspp = wave_sum64(dspp);
+    if (lane == 0) {
+        uint4 cnt;  // decisions per pass; pass streams start at 16-byte boundaries
+        cnt.x = (uint32_t)n_spp;
+        cnt.y = (uint32_t)n_mrp;
+        cnt.z = (uint32_t)n_cup;
+        cnt.w = 0;
+        a.counts[(size_t)b * 32 + k] = cnt;
+        a.dspp[(size_t)b * 32 + k] = dspp;
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -422,14 +439,6 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
     return m.bp;
 }
 
-// word k (0..3) of a 16-byte chunk, by value (no address taken: a dynamic
-// index into a local vector would be lowered to scratch memory)
-__device__ __forceinline__ uint32_t comp4(uint4 c, int k) {
-    const uint32_t lo = (k & 1) ? c.y : c.x;
-    const uint32_t hi = (k & 1) ? c.w : c.z;
-    return (k & 2) ? hi : lo;
-}
-
 // Code one decision with context state `t` (read ahead by the caller), store
 // the context's new state, and return the state of the next decision's
 // context: `nt` as read ahead, unless it is the same context.
@@ -440,50 +449,17 @@ __device__ __forceinline__ uint32_t mq_dec(Mq &m, uint32_t *cx, const uint32_t *
     return ((nbyte >> 1) == (byte >> 1)) ? tn : nt;
 }
 
-// Up to 16 decisions of one chunk (`left` of them remain in the pass).  Byte
-// positions are compile-time after unrolling; the next decision's context
-// state is read one decision ahead (within the chunk).
-__device__ __forceinline__ bool mq_chunk16(Mq &m, uint32_t *cx, const uint32_t *tab, const uint4 cur,
-                                           int &left) {
-    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
-    uint32_t t = cx[min((w[0] & 0xFFu) >> 1, 18u) * 64];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        if (j >= left) {
-            left = 0;
-            return true;
-        }
-        const uint32_t byte = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
-        uint32_t nbyte = 0, nt = 0;
-        if (j < 15) {
-            nbyte = (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu;
-            nt = cx[min(nbyte >> 1, 18u) * 64];  // may be past the pass end
-        }
-        t = mq_dec(m, cx, tab, byte, t, nbyte, nt);
-    }
-    left -= 16;
-    return left <= 0;
-}
-
-// MQ-code one pass's decision stream (16-byte aligned, `n` decisions).  Two
-// chunk buffers alternate so each load has a whole chunk of coding to land
-// behind before it is used.
-__device__ __forceinline__ void mq_pass(Mq &m, uint32_t *cx, const uint32_t *tab, const uint4 *s4, int n) {
-    if (n <= 0) return;
-    uint4 ca = s4[0];
-    uint4 cb = s4[1];
-    int chunk = 0;
-    int left = n;
-    for (;;) {
-        if (mq_chunk16(m, cx, tab, ca, left)) break;
-        ca = s4[chunk + 2];
-        chunk++;
-        if (mq_chunk16(m, cx, tab, cb, left)) break;
-        cb = s4[chunk + 2];
-        chunk++;
-    }
-}
-
+// One lane codes one code-block.  The block's passes are segments of the
+// decision streams (each 16-byte aligned, see k_t1_cm); the lane walks them
+// with ONE data-driven loop -- a chunk of up to 16 decisions per iteration;
+// the segment switch and the per-pass rate record are data, not control
+// flow -- so all lanes of a wave execute the same instruction stream
+// whatever pass each is in.  Blocks are ordered by decision count
+// (k_t1_keys + radix sort), so the lanes of a wave finish together.
+//
+// Segment s of a block with P coded planes: s = 0 is the top plane's cleanup
+// pass; s >= 1 is pass (s+2)%3 (0 SPP, 1 MRP, 2 CUP) of plane k = (s+2)/3,
+// planes counted from the top.
 __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     __shared__ uint32_t cxs[19 * 64];
     __shared__ uint32_t mqt[48];
@@ -492,12 +468,10 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
         mqt[lane] = (uint32_t)c_qe[lane] | ((uint32_t)c_nmps[lane] << 16) | ((uint32_t)c_nlps[lane] << 22) |
                     ((uint32_t)(lane == 0 || lane == 6 || lane == 14) << 28);
     __syncthreads();
-    // only the first `lanes` lanes of each wave take a block: fewer lanes per
-    // wave means less divergence in the serial coder and more waves per SIMD
+    // only the first `lanes` lanes of each wave take a block
     if (lane >= a.lanes) return;
     const int gi = blockIdx.x * a.lanes + lane;
     if (gi >= a.nblocks) return;
-    const uint64_t c0 = __builtin_amdgcn_s_memtime();
     const uint64_t w0 = wall_clock64();
     const int b = a.order[gi];
     const BlockDesc d = a.blocks[b];
@@ -515,60 +489,106 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     cx[CX_UNI * 64] = mqt[46];
     Mq m;
     m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
-    m.cap = (a.variant & 1) ? 0 : (int)d.out_cap;  // variant 1: timing probe without output stores
+    m.cap = (int)d.out_cap;
     m.out = a.out + d.out_off;
     int32_t *R = a.rates + (size_t)b * kMaxPasses;
     int64_t *D = a.dists + (size_t)b * kMaxPasses;
     const uint32_t cap = plane_stream_cap(d.w, d.h);
     const uint8_t *sbase = a.stream + a.slot_off[b];
-    int np = 0;
-    for (int k = 0; k < P; k++) {
-        const int p = P - 1 - k;
-        const uint4 *s = (const uint4 *)(sbase + (size_t)k * cap);
-        const uint4 cnt = a.counts[(size_t)b * 32 + k];
-        const int64_t dspp = a.dspp[(size_t)b * 32 + k];
-        const int o_mrp = ((int)cnt.x + 15) & ~15;
-        const int o_cup = (o_mrp + (int)cnt.y + 15) & ~15;
-        if (k > 0) {
-            mq_pass(m, cx, mqt, s, (int)cnt.x);
-            R[np] = m.bp + 3;
-            D[np] = dspp;
-            np++;
-            mq_pass(m, cx, mqt, s + (o_mrp >> 4), (int)cnt.y);
-            R[np] = m.bp + 3;
-            D[np] = a.dref[(size_t)b * 32 + p];
-            np++;
+    const uint4 *cntp = a.counts + (size_t)b * 32;
+    const int64_t *dspp = a.dspp + (size_t)b * 32;
+    const int64_t *dref = a.dref + (size_t)b * 32;
+    const int64_t *dsig = a.dsig + (size_t)b * 32;
+    const int nseg = 3 * P - 2;
+    int s = 0, k = 0, pass = 2;
+    uint4 cnt = cntp[0];
+    const uint4 *ptr = (const uint4 *)sbase;  // top plane: cleanup at offset 0
+    int left = (int)cnt.z;
+    int64_t ndec = left;
+    uint4 cur = ptr[0];
+    for (;;) {
+        // close finished segments (empty passes close at once)
+        while (left <= 0 && s < nseg) {
+            const int p = P - 1 - k;
+            R[s] = m.bp + 3;
+            D[s] = pass == 0 ? dspp[k] : (pass == 1 ? dref[p] : dsig[p] - dspp[k]);
+            if (++s >= nseg) break;
+            pass = pass == 2 ? 0 : pass + 1;
+            if (pass == 0) {
+                k++;
+                cnt = cntp[k];
+            }
+            const int o_mrp = ((int)cnt.x + 15) & ~15;
+            const int o_cup = (o_mrp + (int)cnt.y + 15) & ~15;
+            ptr = (const uint4 *)(sbase + (size_t)k * cap + (pass == 0 ? 0 : (pass == 1 ? o_mrp : o_cup)));
+            left = pass == 0 ? (int)cnt.x : (pass == 1 ? (int)cnt.y : (int)cnt.z);
+            ndec += left;
+            cur = ptr[0];
         }
-        mq_pass(m, cx, mqt, s + (o_cup >> 4), (int)cnt.z);
-        R[np] = m.bp + 3;
-        D[np] = a.dsig[(size_t)b * 32 + p] - dspp;
-        np++;
+        if (s >= nseg) break;
+        // one chunk of up to 16 decisions; the next chunk's load is in flight
+        // behind it, and each context state is read one decision ahead
+        const uint4 nxt = ptr[1];
+        const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+        const int n = min(16, left);
+        uint32_t t = cx[min((w[0] & 0xFFu) >> 1, 18u) * 64];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            if (j < n) {
+                const uint32_t byte = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+                uint32_t nbyte = 0, nt = 0;
+                if (j < 15) {
+                    nbyte = (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu;
+                    nt = cx[min(nbyte >> 1, 18u) * 64];  // may be past the pass end
+                }
+                t = mq_dec(m, cx, mqt, byte, t, nbyte, nt);
+            }
+        }
+        left -= n;
+        ptr++;
+        cur = nxt;
     }
     const int len = mq_flush(m);
-    if (len > m.cap && !(a.variant & 1)) atomicOr(a.err, 1);
-    R[np - 1] = len;
-    for (int i = 0; i < np; i++) {
+    if (len > m.cap) atomicOr(a.err, 1);
+    R[nseg - 1] = len;
+    for (int i = 0; i < nseg; i++) {
         int r = min(R[i], len);
         if (r > 1 && r <= m.cap && m.out[r - 1] == 0xFF) r--;
         R[i] = r;
     }
-    a.npasses[b] = (uint8_t)np;
+    a.npasses[b] = (uint8_t)nseg;
     a.lengths[b] = len;
-    if (a.dbg) {  // debug census: decisions, shader cycles, 100 MHz ticks
-        int64_t ndec = 0;
-        for (int k = 0; k < P; k++) {
-            const uint4 c4 = a.counts[(size_t)b * 32 + k];
-            ndec += c4.x + c4.y + c4.z;
-        }
+    if (a.dbg) {  // debug census: decisions, 100 MHz ticks, lane index
         a.dbg[(size_t)b * 4 + 0] = ndec;
-        a.dbg[(size_t)b * 4 + 1] = (int64_t)(__builtin_amdgcn_s_memtime() - c0);
+        a.dbg[(size_t)b * 4 + 1] = 0;
         a.dbg[(size_t)b * 4 + 2] = (int64_t)(wall_clock64() - w0);
         a.dbg[(size_t)b * 4 + 3] = gi;
     }
 }
 
+// Tier-1 lane order: blocks by decreasing decision count (all passes), so the
+// lanes of a wave carry similar work.  keys = ~count: an ascending radix sort
+// yields the descending order.
+__global__ void __launch_bounds__(256) k_t1_keys(int nblocks, const uint8_t *P, const uint4 *counts,
+                                                 uint32_t *keys, int32_t *vals) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    uint32_t n = 0;
+    for (int k = 0; k < P[b]; k++) {
+        const uint4 c = counts[(size_t)b * 32 + k];
+        n += c.x + c.y + c.z;
+    }
+    keys[b] = ~n;
+    vals[b] = b;
+}
+
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
-    if (a.nitems) hipLaunchKernelGGL(k_t1_cm, dim3((a.nitems + 63) / 64), dim3(64), 0, st, a);
+    if (a.nitems)
+        hipLaunchKernelGGL(k_t1_cm, dim3((a.nitems + kCmWaves - 1) / kCmWaves), dim3(64 * kCmWaves), 0, st, a);
+}
+void launch_t1_keys(int nblocks, const uint8_t *P, const uint4 *counts, uint32_t *keys, int32_t *vals,
+                    hipStream_t st) {
+    if (nblocks) hipLaunchKernelGGL(k_t1_keys, dim3((nblocks + 255) / 256), dim3(256), 0, st, nblocks, P, counts, keys, vals);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
     if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + a.lanes - 1) / a.lanes), dim3(64), 0, st, a);

@@ -15,8 +15,22 @@ a = np.fromfile(os.path.join(d, "mqdbg.bin"), dtype=np.int64).reshape(-1, 4)
 dec, cyc, wall = a[:, 0], a[:, 1], a[:, 2]
 m = dec > 0
 print("t1_mq_ms", st.t1_mq_ms, "blocks", m.sum(), "dec total", dec.sum(), "max", dec.max())
-print("cycles: max", cyc.max(), "wall ticks max", wall.max(), "=> clock GHz", cyc.max() / wall.max() / 10)
-r = cyc[m] / dec[m]
-print("cycles/decision: median", np.median(r), "p10", np.percentile(r, 10), "p90", np.percentile(r, 90))
+
+
+
 o = np.argsort(-cyc)[:8]
 for i in o: print(i, a[i])
+print("decisions per block: mean", dec[m].mean(), "p50", np.median(dec[m]), "p99", np.percentile(dec[m], 99))
+wt = wall[m] / 100.0  # us
+print("per-block wall us: mean", wt.mean(), "p50", np.median(wt), "p99", np.percentile(wt, 99), "max", wt.max())
+print("sum decisions / t1_mq_ms => Gdec/s", dec.sum() / (st.t1_mq_ms * 1e-3) / 1e9)
+print("stages", st.as_dict())
+gi = a[:, 3]
+lanes = int(os.environ.get("JP2HIP_MQ_LANES", "16"))
+wv = gi[m] // lanes
+import collections
+print("ns per decision (per block wall/dec): p10 %.1f p50 %.1f p90 %.1f" % tuple(np.percentile(wall[m] * 10.0 / dec[m], [10, 50, 90])))
+for q in (0, 1, 2, 10, 100, 300, 1000):
+    sel = wv == q
+    if sel.any():
+        print("wave", q, "dec max", dec[m][sel].max(), "min", dec[m][sel].min(), "wall us max", wall[m][sel].max() / 100.0)
