@@ -142,6 +142,74 @@ int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len,
 
 void jp2hip_free(void *p);
 
+/* ------------------------------------------------------------------------
+ * Batch path: one GPU's work queue for a CSV batch.
+ *
+ * Replaces the chain a CSV row takes through the reference
+ *   LoadCsvHandler.java:250-289 -> LargeImageVerticle.java:65-108 ->
+ *   ImageWorkerVerticle.java:54-110 (convert LOSSLESS, reply, then hand the
+ *   JPX to S3BucketVerticle with derivative-image=true) ->
+ *   S3BucketVerticle.java:88-211,286-303 (PUT, delete the JPX after a
+ *   successful upload)
+ * with a native pipeline per GPU: reader threads (TIFF file -> pinned host
+ * buffer, header parse), one encoder thread per context (images in flight on
+ * the GPU, each with its own HIP stream), and uploader threads (atomic JPX
+ * write, upload callback, delete-after-upload), so file I/O and the upload
+ * overlap the encodes.  Images are independent: N GPUs run N of these
+ * (one process per GPU), sharded by the caller; no collective.
+ * ---------------------------------------------------------------------- */
+typedef struct jp2hip_batch jp2hip_batch;
+
+/* Upload hook (S3BucketVerticle stand-in): called on an uploader thread with
+ * the image id (S3 key = file name, ImageWorkerVerticle.java:69) and the
+ * written JPX path.  Return 0 on success.  NULL selects the built-in stub,
+ * which reads every byte of the file and succeeds (FakeS3BucketVerticle). */
+typedef int (*jp2hip_upload_fn)(void *user, const char *image_id_utf8, const char *jpx_path_utf8);
+
+typedef struct jp2hip_batch_config {
+    int32_t device;              /* HIP device ordinal                               */
+    int32_t contexts;            /* images in flight on the GPU (<=0: 3)             */
+    int32_t reader_threads;      /* TIFF readers (<=0: 2)                            */
+    int32_t uploader_threads;    /* JPX writers + uploaders (<=0: 2)                 */
+    int32_t host_threads;        /* tier-2 threads per context (<=0: 16 / contexts)  */
+    int32_t delete_after_upload; /* derivative-image=true: remove the JPX once sent  */
+    int32_t write_output;        /* 0: keep the JPX in memory, skip the file write   */
+    int32_t reserved;
+} jp2hip_batch_config;
+
+#define JP2HIP_BATCH_OK 0
+#define JP2HIP_BATCH_CONVERT_FAILED (-1) /* ImageWorker replies failure (IOException) */
+#define JP2HIP_BATCH_UPLOAD_FAILED (-2)  /* S3 upload failed; callback gets "false"   */
+
+typedef struct jp2hip_batch_result {
+    int64_t job;          /* the caller's job number from jp2hip_batch_submit     */
+    int32_t status;       /* JP2HIP_BATCH_*                                       */
+    int32_t reserved;
+    int64_t in_bytes;     /* TIFF file size                                       */
+    int64_t out_bytes;    /* JPX size                                             */
+    int64_t pixels;       /* width * height                                       */
+    double read_ms;       /* file -> pinned buffer + header parse                 */
+    double encode_ms;     /* H2D + GPU encode + tier-2 (jp2hip_encode_tiff)       */
+    double upload_ms;     /* file write + upload hook + delete                    */
+    char message[240];    /* failure text ("" on success)                         */
+} jp2hip_batch_result;
+
+int jp2hip_batch_create(jp2hip_batch **out, const jp2hip_batch_config *cfg, jp2hip_upload_fn upload,
+                        void *user);
+/* Queue one image: convert `tiff_path` into `jpx_path` (written atomically)
+ * with `conversion` (recipe NULL -> Bucketeer recipe), then upload it under
+ * `image_id`.  Never blocks on the GPU; returns < 0 after close. */
+int jp2hip_batch_submit(jp2hip_batch *b, int64_t job, const char *image_id_utf8, const char *tiff_path_utf8,
+                        const char *jpx_path_utf8, int conversion, const jp2hip_recipe *recipe);
+/* Collect up to `max` finished jobs (uploaded or failed); waits up to
+ * timeout_ms (< 0: until at least one is ready or nothing is pending).
+ * Returns the number written to `results`. */
+int jp2hip_batch_wait(jp2hip_batch *b, jp2hip_batch_result *results, int max, int timeout_ms);
+/* Jobs submitted and not yet returned by jp2hip_batch_wait. */
+int64_t jp2hip_batch_pending(jp2hip_batch *b);
+/* Stop accepting jobs, finish the queued ones, join all threads. */
+void jp2hip_batch_destroy(jp2hip_batch *b);
+
 #ifdef __cplusplus
 }
 #endif

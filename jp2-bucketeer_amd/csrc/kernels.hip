@@ -572,7 +572,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ma.err = (int *)this->err.ptr;
     {
         const char *e = getenv("JP2HIP_MQ_LANES");
-        ma.lanes = std::max(1, std::min(64, e ? atoi(e) : 8));
+        ma.lanes = std::max(1, std::min(64, e ? atoi(e) : 64));
     }
     ma.dbg = nullptr;
     if (dd) {

@@ -128,25 +128,43 @@ __device__ __forceinline__ int flush_stripe(uint8_t *out, int base, const LaneDe
     return total;
 }
 
-#define ROWS6(dst, expr)                                  \
-    _Pragma("unroll") for (int i = 0; i < 6; i++) {       \
-        int r = r0 - 1 + i;                               \
-        dst[i] = (r >= 0 && r < h) ? (expr) : 0ull;       \
-    }
+// The item's bit-plane rows live in VGPRs, one row per lane (lane r holds
+// row r of B[p], S[p], S[p+1], S[p+2], the sign plane and the new-significance
+// masks N); a stripe reads the rows it needs with v_readlane into SGPRs, so
+// the per-stripe mask algebra is scalar and no memory access sits inside the
+// stripe loops.
+struct RowV {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ RowV rowv(uint64_t v) { return RowV{(uint32_t)v, (uint32_t)(v >> 32)}; }
+// row r (wave-uniform) of a lane-distributed mask; 0 outside [0, h)
+__device__ __forceinline__ uint64_t row(const RowV &v, int r, int h) {
+    if (r < 0 || r >= h) return 0ull;
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v.hi, r) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)v.lo, r);
+}
+__device__ __forceinline__ void set_row(RowV &v, int r, uint64_t m, int lane) {
+    v.lo = lane == r ? (uint32_t)m : v.lo;
+    v.hi = lane == r ? (uint32_t)(m >> 32) : v.hi;
+}
+
+#define ROWS6(dst, src)                                            \
+    _Pragma("unroll") for (int i = 0; i < 6; i++) dst[i] = row(src, r0 - 1 + i, h);
 
 // Context modelling: one wavefront per (code-block, bit-plane) item, lane =
 // column.  The stripe's significance state is a handful of 64-bit row masks,
-// identical in every lane (wave-uniform: SALU-friendly); each lane forms the
-// contexts of its own column's <= 4 samples from them, and the stripe's
-// decisions are laid out in scan order (column-major) by a wave prefix sum.
+// wave-uniform (SGPRs, SALU); each lane forms the contexts of its own
+// column's <= 4 samples from them, and the stripe's decisions are laid out in
+// scan order (column-major) by a wave prefix sum.
 //   SPP: membership is the least fixed point of the causal neighbourhood
 //        rule over the stripe's masks (new significance N feeds the samples
 //        visited after it);
 //   MRP: neighbours see the post-SPP state S[p+1] | N;
 //   CUP: visited neighbours see S[p], the others S[p+1] | N (closed form).
+// Signs come from the sign plane; the SPP distortion decrease is summed once
+// per item from N and the sign-magnitude words.
 constexpr int kCmWaves = 4;  // items per workgroup
 __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
-    __shared__ uint64_t Nsh[kCmWaves][64];
     __shared__ uint8_t lzc[4 * 256];
     __shared__ uint8_t lsc[256];
     for (int i = threadIdx.x; i < 1024; i += 64 * kCmWaves) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
@@ -168,15 +186,17 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
     const uint64_t *BP = a.bp + d.bp_off;
     const uint64_t *SP = BP + (size_t)Mb * 64;
     const uint64_t *SGp = BP + (size_t)2 * Mb * 64;
-    const int32_t *SM = a.sm + d.sm_off;
     const uint8_t *zl = lzc + d.band * 256;
-    uint64_t *N = Nsh[wv];
     const int nstripes = (h + 3) >> 2;
-    const uint64_t *Bp = BP + (size_t)p * 64;
-    const uint64_t *S0p = SP + (size_t)p * 64;
     const bool has1 = p + 1 < P, has2 = p + 2 < P;
-    const uint64_t *S1p = SP + (size_t)(p + 1) * 64;
-    const uint64_t *S2p = SP + (size_t)(p + 2) * 64;
+    // one coalesced load per plane row array; lane r keeps row r
+    const bool inr = lane < h;
+    const RowV Bv = rowv(inr ? BP[(size_t)p * 64 + lane] : 0ull);
+    const RowV S0v = rowv(inr ? SP[(size_t)p * 64 + lane] : 0ull);
+    const RowV S1v = rowv(inr && has1 ? SP[(size_t)(p + 1) * 64 + lane] : 0ull);
+    const RowV S2v = rowv(inr && has2 ? SP[(size_t)(p + 2) * 64 + lane] : 0ull);
+    const RowV SGv = rowv(inr ? SGp[lane] : 0ull);
+    RowV Nv = {0u, 0u};
     uint8_t *out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
     int64_t dspp = 0;
     int n_spp = 0, n_mrp = 0, pos = 0;
@@ -187,10 +207,10 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
         for (int s = 0; s < nstripes; s++) {
             const int r0 = s * 4, nr = min(4, h - r0);
             uint64_t s1[6], sg[6], bt[4], n[4] = {0, 0, 0, 0}, mem[4];
-            ROWS6(s1, S1p[r]);
-            ROWS6(sg, SGp[r]);
+            ROWS6(s1, S1v);
+            ROWS6(sg, SGv);
 #pragma unroll
-            for (int q = 0; q < 4; q++) bt[q] = (q < nr) ? Bp[r0 + q] : 0ull;
+            for (int q = 0; q < 4; q++) bt[q] = row(Bv, r0 + q, h);
             const uint64_t bfprev = (r0 > 0) ? (s1[0] | nprev) : 0ull;
             for (;;) {
                 bool changed = false;
@@ -210,7 +230,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
             }
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (q < nr) N[r0 + q] = n[q];
+                if (q < nr) set_row(Nv, r0 + q, n[q], lane);
             nprev = n[3];
             LaneDec e{0, 0, 0};
 #pragma unroll
@@ -225,9 +245,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
                 e.put(zl[pat8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
                 if (bv) {
                     const uint32_t sp = lsc[pats(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
-                    const uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
-                    e.put(sp >> 1, (word >> 31) ^ (sp & 1u));
-                    dspp += dist_gain(word & 0x7FFFFFFFu, p, lossless);
+                    e.put(sp >> 1, bit(sg[q + 1], c) ^ (sp & 1u));
                 }
             }
             pos += flush_stripe(out, pos, e, lane);
@@ -239,14 +257,14 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
         for (int s = 0; s < nstripes; s++) {
             const int r0 = s * 4, nr = min(4, h - r0);
             uint64_t post[6], bt[4], mem[4], fr[4];
-            ROWS6(post, S1p[r] | N[r]);
+#pragma unroll
+            for (int i = 0; i < 6; i++) post[i] = row(S1v, r0 - 1 + i, h) | row(Nv, r0 - 1 + i, h);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                bool in = q < nr;
-                bt[q] = in ? Bp[r0 + q] : 0ull;
-                uint64_t s1q = in ? S1p[r0 + q] : 0ull;
+                bt[q] = row(Bv, r0 + q, h);
+                const uint64_t s1q = row(S1v, r0 + q, h);
                 mem[q] = s1q & V;
-                fr[q] = s1q & ~((in && has2) ? S2p[r0 + q] : 0ull);
+                fr[q] = s1q & ~row(S2v, r0 + q, h);
             }
             LaneDec e{0, 0, 0};
 #pragma unroll
@@ -266,12 +284,13 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
     for (int s = 0; s < nstripes; s++) {
         const int r0 = s * 4, nr = min(4, h - r0);
         uint64_t s1[6], post[6], s0[6], sg[6], bt[4], mem[4];
-        ROWS6(s1, has1 ? S1p[r] : 0ull);
-        ROWS6(post, s1[i] | (spp ? N[r] : 0ull));
-        ROWS6(s0, S0p[r]);
-        ROWS6(sg, SGp[r]);
+        ROWS6(s1, S1v);
 #pragma unroll
-        for (int q = 0; q < 4; q++) bt[q] = (q < nr) ? Bp[r0 + q] : 0ull;
+        for (int i = 0; i < 6; i++) post[i] = s1[i] | row(Nv, r0 - 1 + i, h);
+        ROWS6(s0, S0v);
+        ROWS6(sg, SGv);
+#pragma unroll
+        for (int q = 0; q < 4; q++) bt[q] = row(Bv, r0 + q, h);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (q >= nr) { mem[q] = 0; continue; }
@@ -310,8 +329,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
                 for (int q = 0; q < 4; q++) {
                     if (q != r) continue;
                     const uint32_t sp = lsc[pats(s0[q], s0[q + 1], post[q + 1], post[q + 2], sg[q], sg[q + 1], sg[q + 2], c)];
-                    const uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
-                    e.put(sp >> 1, (word >> 31) ^ (sp & 1u));
+                    e.put(sp >> 1, bit(sg[q + 1], c) ^ (sp & 1u));
                 }
                 qstart = r + 1;
             }
@@ -327,13 +345,26 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
             e.put(zl[pat8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
             if (bv) {
                 const uint32_t sp = lsc[pats(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
-                const uint32_t word = (uint32_t)SM[(r0 + q) * 64 + c];
-                e.put(sp >> 1, (word >> 31) ^ (sp & 1u));
+                e.put(sp >> 1, bit(sg[q + 1], c) ^ (sp & 1u));
             }
         }
         pos += flush_stripe(out, pos, e, lane);
     }
     const int n_cup = pos - cup0;
+    if (spp) {
+        // SPP distortion decrease: lane r sums its row's newly significant
+        // samples (the sign-magnitude words are read only here)
+        const uint64_t nrow = ((uint64_t)Nv.hi << 32) | Nv.lo;
+        if (nrow) {
+            const int32_t *SMr = a.sm + d.sm_off + (size_t)lane * 64;
+            uint64_t m = nrow;
+            while (m) {
+                const int cc = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                dspp += dist_gain((uint32_t)SMr[cc] & 0x7FFFFFFFu, p, lossless);
+            }
+        }
+    }
     dspp = wave_sum64(dspp);
     if (lane == 0) {
         uint4 cnt;  // decisions per pass; pass streams start at 16-byte boundaries
@@ -389,39 +420,82 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
 // Context state = the 32-bit table word of its current index (Qe | NMPS << 16 |
 // NLPS << 22 | SWITCH << 28) with the MPS symbol in bit 31.
 //
-// One decision, straight-line except for the (rare per lane) byte-out: the
-// CODEMPS/CODELPS procedures of Annex C.2 fold into one select -- the
-// interval keeps A-Qe exactly when "MPS" xor "conditional exchange" -- and the
-// context moves to NMPS/NLPS exactly when renormalisation happens.  `t` is the
-// context's state word (read ahead by the caller); returns the new state word.
-__device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint32_t *tab, const uint32_t d) {
+// One decision, straight-line (no branch per decision on a 64-lane wave):
+// the CODEMPS/CODELPS procedures of Annex C.2 fold into one select -- the
+// interval keeps A-Qe exactly when "MPS" xor "conditional exchange" -- the
+// context moves to NMPS/NLPS exactly when renormalisation happens, and every
+// value of RENORME is computed with selects;
+// the (at most one, common) byte-out is applied by select and its byte is
+// written to the lane's 64-byte LDS ring -- to a dummy slot when nothing is
+// emitted -- so the only per-decision branch is the rare second byte-out of
+// one renormalisation.  `valid` = false makes the step a no-op (partial
+// chunks), again by select.
+__device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
+    uint32_t B = m.B;
+    if (B != 0xFF && m.C >= 0x8000000u) {
+        B++;
+        m.C &= 0x7FFFFFFu;
+    }
+    ring[m.bp >= 0 ? (m.bp & 63) : 64] = (uint8_t)B;
+    m.bp++;
+    const bool ff = B == 0xFF;
+    m.B = ff ? (m.C >> 20) : (m.C >> 19);
+    m.C &= ff ? 0xFFFFFu : 0x7FFFFu;
+    m.CT = ff ? 7 : 8;
+}
+
+__device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint32_t *tab, const uint32_t d,
+                                               const bool valid, uint8_t *ring) {
     const uint32_t qe = t & 0xFFFFu;
     const uint32_t mps = t >> 31;
     const uint32_t A1 = m.A - qe;
     const bool isM = d == mps;
     const bool keep = isM != (A1 < qe);
-    const uint32_t An = keep ? A1 : qe;
-    m.C += keep ? qe : 0u;
+    const uint32_t An0 = keep ? A1 : qe;
+    const uint32_t C0 = m.C + (keep ? qe : 0u);
     const bool ren = (!isM) || (A1 < 0x8000u);
     const uint32_t idx = (t >> (isM ? 16 : 22)) & 63u;
     const uint32_t nm = mps ^ ((isM ? 0u : 1u) & (t >> 28));
     const uint32_t tw = tab[idx] | (nm << 31);
-    const int n = __clz(An) - 16;
-    m.A = An << n;
-    if (__builtin_expect(n < m.CT, 1)) {
-        m.C <<= n;
-        m.CT -= n;
-    } else {
-        int r = n;
-        do {
-            m.C <<= m.CT;
-            r -= m.CT;
-            mq_byteout(m);
-        } while (r >= m.CT);
-        m.C <<= r;
-        m.CT -= r;
+    const int n = __clz(An0) - 16;
+    const bool bo = n >= m.CT;
+    const int s1 = bo ? m.CT : n;
+    const uint32_t C1 = C0 << s1;
+    const bool carry = (m.B != 0xFFu) && (C1 >= 0x8000000u);
+    const uint32_t Bc = m.B + (carry ? 1u : 0u);
+    const uint32_t C2 = carry ? (C1 & 0x7FFFFFFu) : C1;
+    const bool ff = Bc == 0xFFu;
+    const bool emit = valid && bo;
+    ring[(emit && m.bp >= 0) ? (m.bp & 63) : 64] = (uint8_t)Bc;
+    uint32_t Cx = bo ? (C2 & (ff ? 0xFFFFFu : 0x7FFFFu)) : C1;
+    int CTx = bo ? (ff ? 7 : 8) : m.CT - n;
+    int rem = n - s1;
+    m.B = emit ? (ff ? (C2 >> 20) : (C2 >> 19)) : m.B;
+    m.bp += emit ? 1 : 0;
+    m.A = valid ? (An0 << n) : m.A;
+    if (emit && rem >= CTx) {  // rare: a second byte-out in this renormalisation
+        m.C = Cx << CTx;
+        rem -= CTx;
+        ring_byteout(m, ring);
+        Cx = m.C;
+        CTx = m.CT;
     }
-    return ren ? tw : t;
+    Cx <<= rem;
+    CTx -= rem;
+    m.C = valid ? Cx : m.C;
+    m.CT = valid ? CTx : m.CT;
+    return (valid && ren) ? tw : t;
+}
+
+// Copy the lane's completed 16-byte ring groups to the code-block output.
+__device__ __forceinline__ void ring_flush(const Mq &m, const uint8_t *ring, int &fl) {
+    while (m.bp - fl >= 16) {
+        const uint32_t *g = (const uint32_t *)(ring + (fl & 63));
+        uint4 v;
+        v.x = g[0]; v.y = g[1]; v.z = g[2]; v.w = g[3];
+        if (fl + 16 <= m.cap) *(uint4 *)(m.out + fl) = v;
+        fl += 16;
+    }
 }
 
 __device__ __forceinline__ int mq_flush(Mq &m) {
@@ -439,16 +513,6 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
     return m.bp;
 }
 
-// Code one decision with context state `t` (read ahead by the caller), store
-// the context's new state, and return the state of the next decision's
-// context: `nt` as read ahead, unless it is the same context.
-__device__ __forceinline__ uint32_t mq_dec(Mq &m, uint32_t *cx, const uint32_t *tab, const uint32_t byte,
-                                           const uint32_t t, const uint32_t nbyte, const uint32_t nt) {
-    const uint32_t tn = mq_step(m, t, tab, byte & 1u);
-    cx[(byte >> 1) * 64] = tn;
-    return ((nbyte >> 1) == (byte >> 1)) ? tn : nt;
-}
-
 // One lane codes one code-block.  The block's passes are segments of the
 // decision streams (each 16-byte aligned, see k_t1_cm); the lane walks them
 // with ONE data-driven loop -- a chunk of up to 16 decisions per iteration;
@@ -463,7 +527,10 @@ __device__ __forceinline__ uint32_t mq_dec(Mq &m, uint32_t *cx, const uint32_t *
 __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     __shared__ uint32_t cxs[19 * 64];
     __shared__ uint32_t mqt[48];
+    __shared__ uint32_t rings[64 * 17];  // 68 bytes per lane: 64-byte ring + dummy slot
     const int lane = threadIdx.x;
+    uint8_t *ring = (uint8_t *)rings + lane * 68;
+    int fl = 0;  // bytes already copied from the ring
     if (lane < 47)
         mqt[lane] = (uint32_t)c_qe[lane] | ((uint32_t)c_nmps[lane] << 16) | ((uint32_t)c_nlps[lane] << 22) |
                     ((uint32_t)(lane == 0 || lane == 6 || lane == 14) << 28);
@@ -534,20 +601,23 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
         uint32_t t = cx[min((w[0] & 0xFFu) >> 1, 18u) * 64];
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            if (j < n) {
-                const uint32_t byte = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
-                uint32_t nbyte = 0, nt = 0;
-                if (j < 15) {
-                    nbyte = (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu;
-                    nt = cx[min(nbyte >> 1, 18u) * 64];  // may be past the pass end
-                }
-                t = mq_dec(m, cx, mqt, byte, t, nbyte, nt);
+            const uint32_t byte = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+            uint32_t nbyte = 0, nt = 0;
+            if (j < 15) {
+                nbyte = (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu;
+                nt = cx[min(nbyte >> 1, 18u) * 64];  // may be past the pass end
             }
+            const uint32_t tn = mq_step(m, t, mqt, byte & 1u, j < n, ring);
+            cx[min(byte >> 1, 18u) * 64] = tn;
+            t = ((nbyte >> 1) == (byte >> 1)) ? tn : nt;
         }
+        ring_flush(m, ring, fl);
         left -= n;
         ptr++;
         cur = nxt;
     }
+    for (int i = fl; i < m.bp; i++)  // bytes still in the ring
+        if (i < m.cap) m.out[i] = ring[i & 63];
     const int len = mq_flush(m);
     if (len > m.cap) atomicOr(a.err, 1);
     R[nseg - 1] = len;

@@ -60,7 +60,10 @@ class Stats(Structure):
 # every symbol include/jp2hip.h declares
 EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_recipe_init",
            "jp2hip_create", "jp2hip_destroy", "jp2hip_encode_file", "jp2hip_encode_tiff",
-           "jp2hip_tiff_layout", "jp2hip_encode_device", "jp2hip_free")
+           "jp2hip_tiff_layout", "jp2hip_encode_device", "jp2hip_free",
+           # batch path (csrc/batch.cpp; bound in jp2hip.batch)
+           "jp2hip_batch_create", "jp2hip_batch_submit", "jp2hip_batch_wait", "jp2hip_batch_pending",
+           "jp2hip_batch_destroy")
 
 _lib = None
 
