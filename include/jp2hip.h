@@ -143,6 +143,53 @@ int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len,
 void jp2hip_free(void *p);
 
 /* ------------------------------------------------------------------------
+ * Tile-split path: one oversized image across GPUs.
+ *
+ * No reference interface exists for this (kdu_compress encodes one image in
+ * one process, KakaduConverter.java:61-71); it is the north_star's "RCCL only
+ * if a single oversized image is split across GPUs".  Rank r of `world`
+ * encodes the contiguous band of tile rows jp2hip_split_rows() names
+ * (ingest, DWT, tier-1 and hulls of its tiles only); the ranks agree on the
+ * PCRD layer thresholds exactly through `allreduce_sum` (a caller-supplied
+ * in-place int64 sum over ranks -- RCCL/torch.distributed on the node), so
+ * the concatenation of every rank's part, in rank order, is byte-identical
+ * to the single-GPU jp2hip_encode_device() output.  The only exchange is a
+ * few hundred all-reduces of <= 64 int64 (threshold bisection, tier-2 sizes);
+ * no pixel or coefficient crosses GPUs.
+ * ---------------------------------------------------------------------- */
+typedef int (*jp2hip_allreduce_fn)(void *user, int64_t *values, int32_t n); /* in-place sum; 0 ok */
+
+typedef struct jp2hip_split {
+    int32_t rank, world;
+    jp2hip_allreduce_fn allreduce_sum; /* may be NULL when world == 1 */
+    void *user;
+} jp2hip_split;
+
+/* Image rows [*row0, *row1) whose tiles rank `rank` encodes. */
+void jp2hip_split_rows(int32_t height, int32_t tile_h, int32_t rank, int32_t world, int32_t *row0,
+                       int32_t *row1);
+
+/* This rank's part of the file: *out (jp2hip_free) goes at byte *file_offset
+ * of a *file_len-byte file.  Rank 0's part starts with the file and main
+ * headers, the last rank's ends with EOC.  d_src/layout describe the whole
+ * TIFF, but only the strips of this rank's rows are read, so d_src may hold
+ * just those (with strip offsets relative to it).  Collective: every rank
+ * must call it with the same image geometry and recipe. */
+int jp2hip_encode_device_split(jp2hip_ctx *ctx, const void *d_src, size_t src_len,
+                               const jp2hip_layout *layout, int conversion,
+                               const jp2hip_recipe *recipe, const jp2hip_split *split,
+                               uint8_t **out, size_t *out_len, uint64_t *file_offset,
+                               uint64_t *file_len, jp2hip_stats *stats);
+
+/* Host-only: global layer thresholds from this rank's hull segments (slope
+ * keys descending, inclusive byte sums) -- the exchange step of the split
+ * encode, exported for tests.  K[l] = min{k : sum over ranks of bytes with
+ * key >= k <= budgets[l]}. */
+int jp2hip_split_thresholds(const uint64_t *keys, const int64_t *cum, int64_t nseg,
+                            const int64_t *budgets, int32_t layers, const jp2hip_split *split,
+                            uint64_t *K);
+
+/* ------------------------------------------------------------------------
  * Batch path: one GPU's work queue for a CSV batch.
  *
  * Replaces the chain a CSV row takes through the reference

@@ -269,6 +269,174 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     return 0;
 }
 
+// Tile-split encode (jp2hip.h, jp2hip_encode_device_split; split.cpp has the
+// exchange rule).  Rank `rank` runs the device pipeline on its band of tile
+// rows only; budgets, thresholds and tier-2 sizes are agreed through
+// sp->allreduce_sum so the parts concatenate to the single-GPU file.
+int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *lay, int conversion,
+                      const jp2hip_recipe *recipe, const jp2hip_split *sp, uint8_t **out, size_t *out_len,
+                      uint64_t *file_offset, uint64_t *file_len, jp2hip_stats *stats, double t_start) {
+    using namespace jp2hip;
+    if (conversion != JP2HIP_LOSSY && conversion != JP2HIP_LOSSLESS)
+        return fail("conversion must be JP2HIP_LOSSY (0) or JP2HIP_LOSSLESS (1)");
+    const int world = sp ? sp->world : 1, rank = sp ? sp->rank : 0;
+    if (world < 1 || rank < 0 || rank >= world) return fail("split: bad rank / world");
+    if (world > 1 && !sp->allreduce_sum) return fail("split: world > 1 needs an allreduce_sum callback");
+    auto allreduce = [&](int64_t *v, int n) {
+        return world <= 1 || sp->allreduce_sum(sp->user, v, (int32_t)n) == 0;
+    };
+    jp2hip_recipe rc;
+    if (recipe) rc = *recipe;
+    else default_recipe(&rc, conversion);
+    if (!lay || !d_src) return fail("null source or layout");
+    Plan full;
+    std::string err;
+    if (!build_plan(full, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
+    int tr0, tr1;
+    split_tile_rows(full.nty, rank, world, tr0, tr1);
+    Plan sub;
+    make_subplan(full, tr0, tr1, sub);
+    const bool have = sub.ntc > 0;
+    const bool prof = ctx->cfg.profile != 0;
+    StageTimes st;
+    std::vector<uint64_t> keys;
+    std::vector<int64_t> cum;
+    bool ok = !have || (ctx->gpu.run_front(d_src, *lay, sub, prof, st, err) && ctx->gpu.segments(keys, cum, err));
+    {
+        int64_t flag = ok ? 0 : 1;
+        if (!allreduce(&flag, 1)) return fail("split: all-reduce failed");
+        if (!ok) return fail(err);
+        if (flag) return fail("split: another rank failed");
+    }
+    const int L = rc.layers;
+    const size_t nbf = full.blocks.size(), nbl = sub.blocks.size(), b0 = (size_t)sub.block0;
+    std::vector<uint8_t> P_full(nbf, 0), nl_full(nbf * L, 0), h_nl;
+    std::vector<int32_t> lrate_full(nbf * L, 0), h_lrate;
+    if (have) std::copy(ctx->gpu.block_planes().begin(), ctx->gpu.block_planes().begin() + nbl, P_full.begin() + b0);
+    T2Input in;
+    in.plan = &full;
+    in.P = P_full.data();
+    in.nl = nl_full.data();
+    in.lrate = lrate_full.data();
+    in.data = nullptr;
+    in.data_off = nullptr;
+    in.threads = ctx->threads;
+    in.tile0 = sub.tile0;
+    in.tile1 = sub.tile0 + full.ntx * (tr1 - tr0);
+    T2State &t2 = ctx->t2;
+    std::vector<int64_t> budgets((size_t)L, 0);
+    std::vector<uint64_t> K((size_t)L);
+    double t2ms = 0;
+    int iters = 0;
+    int64_t cs_bytes = 0;
+    // one selection + header pass for `budgets`; returns false on failure
+    auto round = [&]() -> bool {
+        if (jp2hip_split_thresholds(keys.data(), cum.data(), (int64_t)keys.size(), budgets.data(), L, sp,
+                                    K.data()) != 0) {
+            err = "split: threshold exchange failed";
+            return false;
+        }
+        bool rok = true;
+        if (have) {
+            rok = ctx->gpu.select_keys(sub, K, h_nl, h_lrate, prof, st, err);
+            if (rok) {
+                std::copy(h_nl.begin(), h_nl.end(), nl_full.begin() + b0 * L);
+                std::copy(h_lrate.begin(), h_lrate.end(), lrate_full.begin() + b0 * L);
+            }
+        }
+        const double t0 = now_ms();
+        int64_t v[2] = {0, rok ? 0 : 1};
+        if (rok) v[0] = t2_headers(in, t2) - (int64_t)t2.main.size() - 2;
+        t2ms += now_ms() - t0;
+        if (!allreduce(v, 2)) { err = "split: all-reduce failed"; return false; }
+        if (v[1]) { if (rok) err = "split: another rank failed"; return false; }
+        cs_bytes = (int64_t)t2.main.size() + 2 + v[0];
+        iters++;
+        return true;
+    };
+    if (rc.rate_bpp <= 0.0) {
+        int64_t total = 0;
+        if (have)
+            for (size_t b = 0; b < nbl; b++) total += ctx->gpu.block_lengths()[b];
+        if (!allreduce(&total, 1)) return fail("split: all-reduce failed");
+        for (int l = 0; l < L; l++) budgets[l] = total >> (L - 1 - l);
+        if (!round()) return fail(err);
+    } else {
+        const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)full.w * (double)full.h / 8.0);
+        int64_t budget = target - 12 * full.npackets - 16 * full.ntileparts - 256;
+        for (int it = 0; it < 8; it++) {
+            if (budget < 0) budget = 0;
+            for (int l = 0; l < L; l++) budgets[l] = budget >> (L - 1 - l);
+            if (!round()) return fail(err);
+            if (cs_bytes <= target) break;
+            budget -= (cs_bytes - target) << it;  // as encode_core / the oracle
+        }
+    }
+    // this rank's included bytes
+    std::vector<int32_t> final_len(nbl);
+    std::vector<uint64_t> offs(nbl), offs_full(nbf, 0);
+    uint64_t total = 0;
+    for (size_t b = 0; b < nbl; b++) {
+        final_len[b] = h_lrate[b * L + (L - 1)];
+        offs[b] = total;
+        offs_full[b0 + b] = total;
+        total += (uint64_t)final_len[b];
+    }
+    const uint8_t *data = nullptr;
+    const double tg = now_ms();
+    ok = !have || ctx->gpu.gather(sub, final_len, offs, total, &data, prof, st, err);
+    const double gather_ms = now_ms() - tg;
+    const bool with_main = rank == 0, with_eoc = rank == world - 1;
+    const size_t fh = with_main ? file_header_bytes(full) : 0;
+    const uint64_t part = ok ? fh + t2_part_bytes(in, t2, with_main, with_eoc) : 0;
+    std::vector<int64_t> sizes((size_t)world + 1, 0);
+    sizes[rank] = (int64_t)part;
+    sizes[world] = ok ? 0 : 1;
+    if (!allreduce(sizes.data(), world + 1)) return fail("split: all-reduce failed");
+    if (!ok) return fail(err);
+    if (sizes[world]) return fail("split: another rank failed");
+    uint64_t off = 0, flen = 0;
+    for (int r = 0; r < world; r++) {
+        if (r < rank) off += (uint64_t)sizes[r];
+        flen += (uint64_t)sizes[r];
+    }
+    in.data = data;
+    in.data_off = offs_full.data();
+    const double t0 = now_ms();
+    uint8_t *buf = (uint8_t *)std::malloc(part ? part : 1);
+    if (!buf) return fail("out of memory");
+    if (with_main) write_file_header(full, (uint64_t)cs_bytes, buf);
+    t2_emit_part(in, t2, buf + fh, with_main, with_eoc);
+    t2ms += now_ms() - t0;
+    *out = buf;
+    *out_len = part;
+    if (file_offset) *file_offset = off;
+    if (file_len) *file_len = flen;
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        stats->total_ms = now_ms() - t_start;
+        stats->ingest_ms = st.ingest;
+        stats->dwt_ms = st.dwt;
+        stats->quant_ms = st.quant;
+        stats->t1_ms = st.t1_cm + st.t1_mq;
+        stats->t1_cm_ms = st.t1_cm;
+        stats->t1_mq_ms = st.t1_mq;
+        stats->pcrd_ms = st.pcrd;
+        stats->d2h_ms = prof ? st.d2h : gather_ms;
+        stats->t2_ms = t2ms;
+        stats->codeblocks = (int64_t)nbl;
+        if (have) {
+            int64_t tb = 0, tp = 0;
+            ctx->gpu.t1_total_bytes(tb, tp);
+            stats->t1_bytes = tb;
+            stats->coded_passes = tp;
+        }
+        stats->out_bytes = (int64_t)flen;
+        stats->rate_iterations = iters;
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -397,6 +565,20 @@ int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path, const char *out_p
         return fail(std::string("cannot write output: ") + out_path);
     }
     return 0;
+}
+
+int jp2hip_encode_device_split(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *layout,
+                               int conversion, const jp2hip_recipe *recipe, const jp2hip_split *split,
+                               uint8_t **out, size_t *out_len, uint64_t *file_offset, uint64_t *file_len,
+                               jp2hip_stats *stats) {
+    if (!ctx || !out || !out_len) return fail("null argument");
+    *out = nullptr;
+    *out_len = 0;
+    (void)src_len;
+    double t0 = now_ms();
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return encode_split_core(ctx, d_src, layout, conversion, recipe, split, out, out_len, file_offset, file_len,
+                             stats, t0);
 }
 
 void jp2hip_free(void *p) { std::free(p); }

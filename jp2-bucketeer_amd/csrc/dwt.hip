@@ -115,7 +115,7 @@ struct DwtBandArgs {
     const uint8_t *tif;
     const uint64_t *strip_off;
     int rps, img_w, nc, bits, planar, big_endian, mct, spp_strips;
-    int ntx, tile_w, tile_h;
+    int ntx, tile_w, tile_h, row0;  // row0: image row of tile row 0 (tile-split bands)
     // non-INGEST source: LL of the previous level (compact scratch planes)
     const void *src;
     int src_stride;
@@ -147,7 +147,7 @@ __device__ __forceinline__ int32_t band_load(const DwtBandArgs &a, int tc, int y
         return s[(size_t)y * a.src_stride + x];
     }
     const int c = tc % a.nc, t = tc / a.nc;
-    const int gx = (t % a.ntx) * a.tile_w + x, gy = (t / a.ntx) * a.tile_h + y;
+    const int gx = (t % a.ntx) * a.tile_w + x, gy = a.row0 + (t / a.ntx) * a.tile_h + y;
     const int32_t off = 1 << (a.bits - 1);
     const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : a.nc) * (a.bits >> 3);
     const int strip = gy / a.rps;
@@ -384,7 +384,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
     a.strip_off = p.strip_off;
     a.rps = p.rps; a.img_w = p.img_w; a.nc = p.nc; a.bits = p.bits; a.planar = p.planar;
     a.big_endian = p.big_endian; a.mct = p.mct; a.spp_strips = p.spp_strips;
-    a.ntx = p.ntx; a.tile_w = p.tile_w; a.tile_h = p.tile_h;
+    a.ntx = p.ntx; a.tile_w = p.tile_w; a.tile_h = p.tile_h; a.row0 = p.row0;
     a.dst = p.coef;
     a.plane_w = p.plane_w;
     a.plane = (size_t)p.plane_w * p.plane_h;

@@ -56,7 +56,7 @@ struct DwtLaunch {
     const void *tif;
     const uint64_t *strip_off;
     int rps, img_w, nc, bits, planar, big_endian, mct, spp_strips;
-    int ntx, tile_w, tile_h, plane_w, plane_h, ntc, levels, reversible;
+    int ntx, tile_w, tile_h, row0, plane_w, plane_h, ntc, levels, reversible;
     const int32_t *tc_w, *tc_h;
     void *coef, *scratch0, *scratch1;  // scratch: ntc * ceil(plane_w/2) * ceil(plane_h/2) words each
 };
@@ -85,6 +85,12 @@ class GpuEncoder {
     // layer thresholds for the given data budgets -> per-block layer tables
     bool select(const Plan &plan, const std::vector<int64_t> &budgets, std::vector<uint8_t> &h_nl,
                 std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err);
+    // per-block layer tables for explicit slope thresholds K[layer]
+    // (tile-split: thresholds agreed across ranks)
+    bool select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::vector<uint8_t> &h_nl,
+                     std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err);
+    // this encode's hull segments: slope keys (descending) and inclusive byte sums
+    bool segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err);
     // compact the included bytes of every block and download them
     bool gather(const Plan &plan, const std::vector<int32_t> &final_len,
                 const std::vector<uint64_t> &offsets, uint64_t total, const uint8_t **host_data,
@@ -99,6 +105,8 @@ class GpuEncoder {
   private:
     // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
+    bool apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate,
+                          bool profile, StageTimes &st, std::string &err);
     static constexpr int kNumEvents = 12;
     int device = 0;
     hipStream_t stream = nullptr;

@@ -76,12 +76,22 @@ struct Plan {
     uint64_t bp_words = 0, sm_words = 0, out_bytes = 0;
     int64_t npackets = 0, ntileparts = 0;
     double compw[4] = {1, 1, 1, 1};
+    // tile-split band (make_subplan): the device part covers tiles
+    // [tile0, tile0 + ntc/nc) = image rows [row0, row0 + band_h); its blocks
+    // are the full plan's blocks [block0, block0 + blocks.size())
+    int row0 = 0, band_h = 0, tile0 = 0, block0 = 0;
 };
 
 bool build_plan(Plan &plan, const jp2hip_recipe &rc, int w, int h, int nc, int bits,
                 std::string &err);
 
 int prec_log2(const jp2hip_recipe &rc, int r, bool vertical);
+
+// Tile rows [tr0, tr1) of rank `rank` out of `world` (contiguous bands).
+void split_tile_rows(int nty, int rank, int world, int &tr0, int &tr1);
+// The device part of `full` for tile rows [tr0, tr1): same blocks, offsets
+// rebased to the band (tier-2 keeps using `full` and global block indices).
+void make_subplan(const Plan &full, int tr0, int tr1, Plan &sub);
 
 // Tier-2 inputs: the layer table chosen by PCRD.  `data` holds the included
 // bytes of every block back to back at `data_off[b]` (needed by t2_emit only).
@@ -93,6 +103,7 @@ struct T2Input {
     const uint8_t *data;
     const uint64_t *data_off;
     int threads;
+    int tile0 = 0, tile1 = -1;  // tiles to code ([tile0, tile1); -1: all)
 };
 
 struct TagNode {
@@ -125,11 +136,17 @@ struct T2State {
     int64_t total = 0;               // code-stream bytes, SOC .. EOC
 };
 
-// Header pass: codes every packet header, returns the code-stream size.
+// Header pass: codes every packet header of tiles [in.tile0, in.tile1),
+// returns main header + those tiles + EOC (the code-stream size when the
+// range is every tile).
 int64_t t2_headers(const T2Input &in, T2State &st);
 // Writes the code-stream described by the last t2_headers() into dst
 // (st.total bytes); in.data / in.data_off must be set.
 void t2_emit(const T2Input &in, const T2State &st, uint8_t *dst);
+// Tile-split: bytes of tiles [in.tile0, in.tile1) (+ main header / EOC when
+// asked) as written by t2_emit_part.
+uint64_t t2_part_bytes(const T2Input &in, const T2State &st, bool with_main, bool with_eoc);
+void t2_emit_part(const T2Input &in, const T2State &st, uint8_t *dst, bool with_main, bool with_eoc);
 
 // JP2 / JPX boxes in front of the code-stream (0 bytes for raw J2K).
 size_t file_header_bytes(const Plan &plan);

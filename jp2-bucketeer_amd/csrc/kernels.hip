@@ -46,6 +46,7 @@ struct IngestArgs {
     const uint64_t *strip_off;
     int rps, w, h, nc, bits, planar, big_endian, mct, reversible;
     int ntx, tile_w, tile_h, plane_w, plane_h, spp_strips;  // strips per plane
+    int row0;  // image row of local row 0 (tile-split bands)
     void *coef;
 };
 
@@ -70,7 +71,7 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
     int32_t off = 1 << (a.bits - 1);
     int32_t s[4];
 #pragma unroll
-    for (int c = 0; c < 4; c++) s[c] = (c < a.nc) ? read_sample(a, x, y, c) - off : 0;
+    for (int c = 0; c < 4; c++) s[c] = (c < a.nc) ? read_sample(a, x, a.row0 + y, c) - off : 0;
     int tx = x / a.tile_w, ty = y / a.tile_h;
     size_t plane = (size_t)a.plane_w * a.plane_h;
     size_t base = ((size_t)(ty * a.ntx + tx) * a.nc) * plane + (size_t)(y - ty * a.tile_h) * a.plane_w +
@@ -450,14 +451,15 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         ia.src = (const uint8_t *)d_src;
         ia.strip_off = (const uint64_t *)strips.ptr;
         ia.rps = lay.rows_per_strip;
-        ia.w = plan.w; ia.h = plan.h; ia.nc = plan.nc; ia.bits = plan.bits;
+        ia.w = plan.w; ia.h = plan.band_h; ia.nc = plan.nc; ia.bits = plan.bits;
+        ia.row0 = plan.row0;
         ia.planar = lay.planar; ia.big_endian = lay.big_endian;
         ia.mct = plan.rc.mct; ia.reversible = plan.rc.reversible;
         ia.ntx = plan.ntx; ia.tile_w = plan.rc.tile_w; ia.tile_h = plan.rc.tile_h;
         ia.plane_w = plan.plane_w; ia.plane_h = plan.plane_h;
         ia.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
         ia.coef = coef.ptr;
-        dim3 gi((plan.w + 63) / 64, (plan.h + 3) / 4);
+        dim3 gi((plan.w + 63) / 64, (plan.band_h + 3) / 4);
         hipLaunchKernelGGL(k_ingest, gi, dim3(256), 0, stream, ia);
         HIPCHECK(hipGetLastError());
     } else {
@@ -471,7 +473,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.img_w = plan.w; dl.nc = plan.nc; dl.bits = plan.bits;
         dl.planar = lay.planar; dl.big_endian = lay.big_endian; dl.mct = plan.rc.mct;
         dl.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
-        dl.ntx = plan.ntx; dl.tile_w = plan.rc.tile_w; dl.tile_h = plan.rc.tile_h;
+        dl.ntx = plan.ntx; dl.tile_w = plan.rc.tile_w; dl.tile_h = plan.rc.tile_h; dl.row0 = plan.row0;
         dl.plane_w = plan.plane_w; dl.plane_h = plan.plane_h; dl.ntc = plan.ntc;
         dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
@@ -676,13 +678,28 @@ bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets,
                         std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate, bool profile,
                         StageTimes &st, std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    const int nb = (int)plan.blocks.size();
     const int L = plan.rc.layers;
     HIPCHECK(hipMemcpyAsync(budget.ptr, budgets.data(), sizeof(int64_t) * L, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipEventRecord(ev[6], stream));
     hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
                        (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr);
     HIPCHECK(hipGetLastError());
+    return apply_thresholds(plan, h_nl, h_lrate, profile, st, err);
+}
+
+bool GpuEncoder::select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::vector<uint8_t> &h_nl,
+                             std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(hipMemcpyAsync(thr.ptr, K.data(), sizeof(uint64_t) * plan.rc.layers, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipEventRecord(ev[6], stream));
+    return apply_thresholds(plan, h_nl, h_lrate, profile, st, err);
+}
+
+// per-block layer tables for the thresholds in `thr` (ev[6] already recorded)
+bool GpuEncoder::apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate,
+                                  bool profile, StageTimes &st, std::string &err) {
+    const int nb = (int)plan.blocks.size();
+    const int L = plan.rc.layers;
     ApplyArgs aa;
     aa.nblocks = nb;
     aa.layers = L;
@@ -700,14 +717,29 @@ bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets,
     HIPCHECK(hipEventRecord(ev[7], stream));
     h_nl.resize((size_t)nb * L);
     h_lrate.resize((size_t)nb * L);
-    HIPCHECK(hipMemcpyAsync(h_nl.data(), nl.ptr, h_nl.size(), hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(h_lrate.data(), lrate.ptr, sizeof(int32_t) * h_lrate.size(), hipMemcpyDeviceToHost, stream));
+    if (nb) {
+        HIPCHECK(hipMemcpyAsync(h_nl.data(), nl.ptr, h_nl.size(), hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(h_lrate.data(), lrate.ptr, sizeof(int32_t) * h_lrate.size(), hipMemcpyDeviceToHost,
+                                stream));
+    }
     HIPCHECK(hipStreamSynchronize(stream));
     if (profile) {
         float t;
         HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[7]));
         st.pcrd += t;
     }
+    return true;
+}
+
+bool GpuEncoder::segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    keys.resize((size_t)nseg);
+    cum.resize((size_t)nseg);
+    if (nseg > 0) {
+        HIPCHECK(hipMemcpyAsync(keys.data(), segkey2.ptr, sizeof(uint64_t) * nseg, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(cum.data(), segcum.ptr, sizeof(int64_t) * nseg, hipMemcpyDeviceToHost, stream));
+    }
+    HIPCHECK(hipStreamSynchronize(stream));
     return true;
 }
 

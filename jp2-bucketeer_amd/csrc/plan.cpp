@@ -87,6 +87,18 @@ static double bibo53(int d, bool hi) {
     return s;
 }
 
+// tier-1 lanes: similar blocks side by side in a wavefront, biggest first
+static void t1_lane_order(Plan &P) {
+    P.t1_order.resize(P.blocks.size());
+    std::iota(P.t1_order.begin(), P.t1_order.end(), 0);
+    std::stable_sort(P.t1_order.begin(), P.t1_order.end(), [&](int a, int b) {
+        const BlockDesc &A = P.blocks[a], &B = P.blocks[b];
+        int wa = A.w * A.h, wb = B.w * B.h;
+        if (wa != wb) return wa > wb;
+        return A.Mb > B.Mb;
+    });
+}
+
 BandQuant band_quant(const jp2hip_recipe &rc, int bits, int d, int band) {
     BandQuant q;
     bool hx = (band == 1 || band == 3), hy = (band == 2 || band == 3);
@@ -146,6 +158,7 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
     P.ntc = P.ntx * P.nty * nc;
     P.plane_w = rc.tile_w;
     P.plane_h = rc.tile_h;
+    P.band_h = h;
     if (rc.mct && nc >= 3) {
         if (rc.reversible) { P.compw[0] = 3.0; P.compw[1] = 0.6875; P.compw[2] = 0.6875; }
         else {
@@ -264,16 +277,55 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
     P.bp_words = bpw;
     P.sm_words = smw;
     P.out_bytes = ob;
-    // tier-1 lanes: similar blocks side by side in a wavefront, biggest first
-    P.t1_order.resize(P.blocks.size());
-    std::iota(P.t1_order.begin(), P.t1_order.end(), 0);
-    std::stable_sort(P.t1_order.begin(), P.t1_order.end(), [&](int a, int b) {
-        const BlockDesc &A = P.blocks[a], &B = P.blocks[b];
-        int wa = A.w * A.h, wb = B.w * B.h;
-        if (wa != wb) return wa > wb;
-        return A.Mb > B.Mb;
-    });
+    t1_lane_order(P);
     return true;
+}
+
+void split_tile_rows(int nty, int rank, int world, int &tr0, int &tr1) {
+    tr0 = (int)((int64_t)nty * rank / world);
+    tr1 = (int)((int64_t)nty * (rank + 1) / world);
+}
+
+void make_subplan(const Plan &full, int tr0, int tr1, Plan &S) {
+    S = Plan();
+    S.rc = full.rc;
+    S.w = full.w; S.h = full.h; S.nc = full.nc; S.bits = full.bits;
+    S.ntx = full.ntx;
+    S.nty = tr1 - tr0;
+    S.ntc = S.ntx * S.nty * S.nc;
+    S.plane_w = full.plane_w;
+    S.plane_h = full.plane_h;
+    std::memcpy(S.compw, full.compw, sizeof S.compw);
+    S.tile0 = tr0 * full.ntx;
+    const int tile1 = tr1 * full.ntx;
+    S.row0 = std::min(full.h, tr0 * full.rc.tile_h);
+    S.band_h = std::min(full.h, tr1 * full.rc.tile_h) - S.row0;
+    const int tc0 = S.tile0 * full.nc, tc1 = tile1 * full.nc;
+    S.tc_w.assign(full.tc_w.begin() + tc0, full.tc_w.begin() + tc1);
+    S.tc_h.assign(full.tc_h.begin() + tc0, full.tc_h.begin() + tc1);
+    // blocks are emitted tile by tile, so the band's blocks are contiguous
+    const int nb = (int)full.blocks.size();
+    int b0 = 0;
+    while (b0 < nb && full.blocks[b0].tc < tc0) b0++;
+    int b1 = b0;
+    while (b1 < nb && full.blocks[b1].tc < tc1) b1++;
+    S.block0 = b0;
+    S.blocks.assign(full.blocks.begin() + b0, full.blocks.begin() + b1);
+    S.weight.assign(full.weight.begin() + b0, full.weight.begin() + b1);
+    if (!S.blocks.empty()) {
+        const BlockDesc f = S.blocks.front();
+        for (BlockDesc &b : S.blocks) {
+            b.tc -= tc0;
+            b.bp_off -= f.bp_off;
+            b.sm_off -= f.sm_off;
+            b.out_off -= f.out_off;
+        }
+        const BlockDesc &l = S.blocks.back();
+        S.bp_words = l.bp_off + (uint64_t)(2 * l.Mb + 1) * 64;
+        S.sm_words = l.sm_off + (uint64_t)64 * l.h;
+        S.out_bytes = l.out_off + l.out_cap;
+    }
+    t1_lane_order(S);
 }
 
 }  // namespace jp2hip

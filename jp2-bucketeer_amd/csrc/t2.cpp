@@ -399,10 +399,19 @@ void parallel_tiles(int ntiles, int threads, F &&f) {
 
 }  // namespace
 
+static void tile_range(const T2Input &in, int &t0, int &t1) {
+    const int ntiles = in.plan->ntx * in.plan->nty;
+    t0 = std::max(0, in.tile0);
+    t1 = in.tile1 < 0 ? ntiles : std::min(ntiles, in.tile1);
+    if (t1 < t0) t1 = t0;
+}
+
 int64_t t2_headers(const T2Input &in, T2State &st) {
     const Plan &P = *in.plan;
     const int ntiles = P.ntx * P.nty;
-    const int nth = std::max(1, std::min(in.threads, ntiles));
+    int t0, t1;
+    tile_range(in, t0, t1);
+    const int nth = std::max(1, std::min(in.threads, std::max(1, t1 - t0)));
     st.tiles.resize((size_t)ntiles);
     if ((int)st.workers.size() < nth) st.workers.resize((size_t)nth);
     for (auto &w : st.workers)
@@ -411,27 +420,42 @@ int64_t t2_headers(const T2Input &in, T2State &st) {
             w.incl.resize(P.blocks.size());
         }
     main_header(P, st.main);
-    parallel_tiles(ntiles, nth, [&](int wid, int t) { tile_headers(in, t, st.tiles[t], st.workers[wid]); });
+    parallel_tiles(t1 - t0, nth, [&](int wid, int i) { tile_headers(in, t0 + i, st.tiles[t0 + i], st.workers[wid]); });
     int64_t total = (int64_t)st.main.size() + 2;
-    for (int t = 0; t < ntiles; t++) total += (int64_t)st.tiles[t].bytes;
+    for (int t = t0; t < t1; t++) total += (int64_t)st.tiles[t].bytes;
     st.total = total;
     return total;
 }
 
-void t2_emit(const T2Input &in, const T2State &st, uint8_t *dst) {
-    const Plan &P = *in.plan;
-    const int ntiles = P.ntx * P.nty;
-    std::memcpy(dst, st.main.data(), st.main.size());
-    std::vector<uint64_t> toff((size_t)ntiles);
-    uint64_t o = st.main.size();
-    for (int t = 0; t < ntiles; t++) {
-        toff[t] = o;
+uint64_t t2_part_bytes(const T2Input &in, const T2State &st, bool with_main, bool with_eoc) {
+    int t0, t1;
+    tile_range(in, t0, t1);
+    uint64_t n = (with_main ? st.main.size() : 0) + (with_eoc ? 2 : 0);
+    for (int t = t0; t < t1; t++) n += st.tiles[t].bytes;
+    return n;
+}
+
+void t2_emit_part(const T2Input &in, const T2State &st, uint8_t *dst, bool with_main, bool with_eoc) {
+    int t0, t1;
+    tile_range(in, t0, t1);
+    uint64_t o = 0;
+    if (with_main) {
+        std::memcpy(dst, st.main.data(), st.main.size());
+        o = st.main.size();
+    }
+    std::vector<uint64_t> toff((size_t)(t1 - t0));
+    for (int t = t0; t < t1; t++) {
+        toff[t - t0] = o;
         o += st.tiles[t].bytes;
     }
-    dst[o] = 0xFF;  // EOC
-    dst[o + 1] = 0xD9;
-    parallel_tiles(ntiles, in.threads, [&](int, int t) { tile_emit(in, t, st.tiles[t], dst + toff[t]); });
+    if (with_eoc) {
+        dst[o] = 0xFF;
+        dst[o + 1] = 0xD9;
+    }
+    parallel_tiles(t1 - t0, in.threads, [&](int, int i) { tile_emit(in, t0 + i, st.tiles[t0 + i], dst + toff[i]); });
 }
+
+void t2_emit(const T2Input &in, const T2State &st, uint8_t *dst) { t2_emit_part(in, st, dst, true, true); }
 
 size_t file_header_bytes(const Plan &P) {
     if (P.rc.format == JP2HIP_FORMAT_J2K) return 0;
@@ -483,7 +507,8 @@ void write_file_header(const Plan &P, uint64_t cs_bytes, uint8_t *dst) {
             u16(c); u16(alpha ? 1 : 0); u16(alpha ? 0 : c + 1);
         }
     }
-    box((uint32_t)(8 + cs_bytes), "jp2c");
+    // a code-stream past 4 GiB: length 0 = "to the end of the file" (last box)
+    box(8 + cs_bytes > 0xFFFFFFFFull ? 0u : (uint32_t)(8 + cs_bytes), "jp2c");
 }
 
 }  // namespace jp2hip

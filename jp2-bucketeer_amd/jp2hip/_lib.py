@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, Structure, byref, c_char_p, c_double, c_int, c_int32,
+from ctypes import (CFUNCTYPE, POINTER, Structure, byref, c_char_p, c_double, c_int, c_int32,
                     c_int64, c_size_t, c_uint8, c_uint64, c_void_p)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -63,7 +63,18 @@ EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_recipe
            "jp2hip_tiff_layout", "jp2hip_encode_device", "jp2hip_free",
            # batch path (csrc/batch.cpp; bound in jp2hip.batch)
            "jp2hip_batch_create", "jp2hip_batch_submit", "jp2hip_batch_wait", "jp2hip_batch_pending",
-           "jp2hip_batch_destroy")
+           "jp2hip_batch_destroy",
+           # tile-split path (csrc/split.cpp + api.cpp; bound in jp2hip.split)
+           "jp2hip_split_rows", "jp2hip_encode_device_split", "jp2hip_split_thresholds")
+
+
+# int (*)(void *user, int64_t *values, int32_t n): in-place sum over ranks, 0 ok
+ALLREDUCE_FN = CFUNCTYPE(c_int, c_void_p, POINTER(c_int64), c_int32)
+
+
+class Split(Structure):
+    _fields_ = [("rank", c_int32), ("world", c_int32), ("allreduce_sum", ALLREDUCE_FN),
+                ("user", c_void_p)]
 
 _lib = None
 
@@ -92,6 +103,16 @@ def lib():
                                        POINTER(Recipe), POINTER(POINTER(c_uint8)),
                                        POINTER(c_size_t), POINTER(Stats)]
     L.jp2hip_free.argtypes = [c_void_p]
+    L.jp2hip_split_rows.argtypes = [c_int32, c_int32, c_int32, c_int32, POINTER(c_int32),
+                                    POINTER(c_int32)]
+    L.jp2hip_split_rows.restype = None
+    L.jp2hip_encode_device_split.argtypes = [c_void_p, c_void_p, c_size_t, POINTER(Layout), c_int,
+                                             POINTER(Recipe), POINTER(Split),
+                                             POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                             POINTER(c_uint64), POINTER(c_uint64), POINTER(Stats)]
+    L.jp2hip_split_thresholds.argtypes = [POINTER(c_uint64), POINTER(c_int64), c_int64,
+                                          POINTER(c_int64), c_int32, POINTER(Split),
+                                          POINTER(c_uint64)]
     _lib = L
     return L
 
@@ -185,6 +206,22 @@ class Encoder:
         if rc != 0:
             raise Jp2hipError(last_error())
         return self._take(out, n), st
+
+    def encode_device_split(self, d_ptr: int, nbytes: int, layout: Layout, conversion: int,
+                            split: Split, rcp: Recipe | None = None):
+        """This rank's part of a tile-split encode: (bytes, file_offset, file_len, Stats)."""
+        out = POINTER(c_uint8)()
+        n = c_size_t()
+        off = c_uint64()
+        flen = c_uint64()
+        st = Stats()
+        rc = lib().jp2hip_encode_device_split(self._h, c_void_p(d_ptr), nbytes, byref(layout),
+                                              conversion, byref(rcp) if rcp is not None else None,
+                                              byref(split), byref(out), byref(n), byref(off),
+                                              byref(flen), byref(st))
+        if rc != 0:
+            raise Jp2hipError(last_error())
+        return self._take(out, n), off.value, flen.value, st
 
     def encode_file(self, tiff_path: str, out_path: str, conversion: int,
                     rcp: Recipe | None = None):
