@@ -53,6 +53,29 @@ def synth_u16(h, w, comps=3, seed=2):
     return out if comps > 1 else out[..., 0]
 
 
+def synth_gray16_rows(row0, row1, w, seed=5, band=512):
+    """C5 content (40000x30000 Gray16) for image rows
+    [row0, row1) only: synth_u16's sinusoids in global coordinates, noise
+    seeded per `band` rows (seed, row // band), so any split of the image
+    into bands of whole `band`-row groups yields the same pixels."""
+    out = np.empty((row1 - row0, w), np.uint16)
+    x = np.arange(w, dtype=np.float32)
+    sx = (32768 + 12000 * np.sin(x / 53.0)).astype(np.float32)
+    g = row0
+    while g < row1:
+        e = min(row1, (g // band + 1) * band)
+        rng = np.random.default_rng([seed, g // band])
+        skip = g - (g // band) * band  # noise rows of this group before g
+        if skip:
+            rng.standard_normal((skip, w), dtype=np.float32)
+        y = np.arange(g, e, dtype=np.float32)[:, None]
+        v = sx[None, :] + 9000 * np.cos(y / 31.0) + 6000 * np.sin((x[None, :] - y) / 17.0)
+        v += 400 * rng.standard_normal((e - g, w), dtype=np.float32)
+        out[g - row0:e - row0] = np.clip(v, 0, 65535).astype(np.uint16)
+        g = e
+    return out
+
+
 def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=False,
                alpha=None) -> bytes:
     """Uncompressed baseline TIFF (strips), 8/16-bit, 1-4 samples."""
