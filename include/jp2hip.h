@@ -72,6 +72,10 @@ typedef struct jp2hip_recipe {
     double rate_bpp;         /* "-rate 3"; <= 0 means "-rate -" (all passes)   */
     int32_t format;          /* JP2HIP_FORMAT_*                                */
     int32_t comment;         /* emit a COM marker                              */
+    int32_t slope_skip;      /* rate-driven (rate_bpp > 0) only: do not code   */
+                             /* bit-planes whose predicted slope lies far      */
+                             /* below the rate target's, as kdu_compress's     */
+                             /* block coder does under "-rate"; 0 = code all   */
 } jp2hip_recipe;
 
 /* Where the samples live inside a source buffer (a baseline TIFF's strips). */

@@ -154,6 +154,25 @@ void default_recipe(jp2hip_recipe *r, int conversion) {
     r->rate_bpp = lossless ? 0.0 : 3.0;
     r->format = JP2HIP_FORMAT_JPX;
     r->comment = 1;
+    r->slope_skip = 1;
+}
+
+// Slope prediction's rate target (bytes; 0 = prediction off) -- the same
+// floor(rate * W * H / 8) the oracle's predict_and_code uses.
+int64_t skip_target_of(const jp2hip_recipe &rc, int w, int h) {
+    if (!rc.slope_skip || rc.rate_bpp <= 0.0) return 0;
+    return (int64_t)std::floor(rc.rate_bpp * (double)w * (double)h / 8.0);
+}
+
+// Safety net of the prediction (oracle predict_and_code): planes were
+// skipped, yet all coded bytes together stay below the target.
+void undershoot_terms(const jp2hip::GpuEncoder &g, int64_t &coded, int64_t &skipped) {
+    coded = 0;
+    skipped = 0;
+    const std::vector<int32_t> &len = g.block_lengths();
+    const std::vector<uint8_t> &pm = g.block_pmin();
+    for (size_t b = 0; b < len.size(); b++) coded += len[b];
+    for (size_t b = 0; b < pm.size(); b++) skipped |= pm[b] > 0;
 }
 
 // The whole encode with the source already in device memory.  On success
@@ -174,7 +193,14 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     if (!build_plan(plan, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     const bool prof = ctx->cfg.profile != 0;
     StageTimes st;
-    if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err)) return fail(err);
+    const int64_t skip_target = skip_target_of(rc, plan.w, plan.h);
+    if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, skip_target)) return fail(err);
+    if (skip_target > 0) {
+        int64_t coded, skipped;
+        undershoot_terms(ctx->gpu, coded, skipped);
+        if (skipped && coded < skip_target && !ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, 0))
+            return fail(err);
+    }
     const int nb = (int)plan.blocks.size();
     const int L = rc.layers;
     const std::vector<int32_t> &len = ctx->gpu.block_lengths();
@@ -301,7 +327,35 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
     StageTimes st;
     std::vector<uint64_t> keys;
     std::vector<int64_t> cum;
-    bool ok = !have || (ctx->gpu.run_front(d_src, *lay, sub, prof, st, err) && ctx->gpu.segments(keys, cum, err));
+    // slope prediction over the whole image: the plane histogram is summed
+    // over ranks (one all-reduce of kSlopeBins + 1 int64, the last entry a
+    // failure flag, so a rank that failed earlier still joins the exchange)
+    const int64_t skip_target = skip_target_of(rc, full.w, full.h);
+    bool hist_done = false;
+    GpuEncoder::HistReduce reduce = [&](std::vector<int64_t> &h) {
+        hist_done = true;
+        std::vector<int64_t> v(h.size() + 1, 0);
+        std::copy(h.begin(), h.end(), v.begin());
+        if (!allreduce(v.data(), (int)v.size()) || v.back() != 0) return false;
+        std::copy(v.begin(), v.end() - 1, h.begin());
+        return true;
+    };
+    bool ok = !have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, skip_target, &reduce);
+    if (skip_target > 0 && !hist_done) {  // no blocks here, or failed before the exchange
+        std::vector<int64_t> v((size_t)kSlopeBins + 1, 0);
+        v.back() = ok ? 0 : 1;
+        if (!allreduce(v.data(), (int)v.size())) return fail("split: all-reduce failed");
+        if (ok && v.back()) { ok = false; err = "split: another rank failed"; }
+    }
+    if (skip_target > 0) {  // the prediction's safety net, decided globally
+        int64_t v[3] = {0, 0, ok ? 0 : 1};
+        if (ok && have) undershoot_terms(ctx->gpu, v[0], v[1]);
+        if (!allreduce(v, 3)) return fail("split: all-reduce failed");
+        if (ok && v[2]) { ok = false; err = "split: another rank failed"; }
+        if (ok && v[1] && v[0] < skip_target && have)
+            ok = ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, 0);
+    }
+    ok = ok && (!have || ctx->gpu.segments(keys, cum, err));
     {
         int64_t flag = ok ? 0 : 1;
         if (!allreduce(&flag, 1)) return fail("split: all-reduce failed");

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -38,6 +39,7 @@ struct T1MqArgs {
     const int32_t *order;
     int nblocks;
     const uint8_t *P;
+    const uint8_t *pmin;  // lowest coded plane (slope prediction; 0 = all)
     const uint8_t *stream;
     const uint64_t *slot_off;
     const uint4 *counts;
@@ -63,8 +65,8 @@ struct DwtLaunch {
 bool launch_dwt(const DwtLaunch &p, hipStream_t st);
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st);
-void launch_t1_keys(int nblocks, const uint8_t *P, const uint4 *counts, uint32_t *keys, int32_t *vals,
-                    hipStream_t st);
+void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
+                    int32_t *vals, hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
 uint32_t t1_plane_stream_cap(int w, int h);
 
@@ -79,9 +81,16 @@ class GpuEncoder {
     bool upload_source(const void *host, size_t len, std::string &err);
     const void *source() const { return src.ptr; }
 
-    // ingest, DWT, quantiser, tier-1, hulls; downloads per-block totals
+    // Sums a slope-prediction histogram over the ranks of a tile-split
+    // encode, in place; false = exchange failed (or another rank failed).
+    using HistReduce = std::function<bool(std::vector<int64_t> &)>;
+    // ingest, DWT, quantiser, tier-1, hulls; downloads per-block totals.
+    // skip_target > 0: rate-driven encode of skip_target bytes with slope
+    // prediction (bit-planes far below the predicted threshold not coded);
+    // reduce (tile-split only) makes the prediction global.
     bool run_front(const void *d_src, const jp2hip_layout &lay, const Plan &plan, bool profile,
-                   StageTimes &st, std::string &err);
+                   StageTimes &st, std::string &err, int64_t skip_target = 0,
+                   const HistReduce *reduce = nullptr);
     // layer thresholds for the given data budgets -> per-block layer tables
     bool select(const Plan &plan, const std::vector<int64_t> &budgets, std::vector<uint8_t> &h_nl,
                 std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err);
@@ -100,6 +109,7 @@ class GpuEncoder {
     const std::vector<int32_t> &block_lengths() const { return h_lengths; }
     const std::vector<uint8_t> &block_passes() const { return h_npasses; }
     const std::vector<uint8_t> &block_planes() const { return h_P; }
+    const std::vector<uint8_t> &block_pmin() const { return h_pmin; }
     hipStream_t get_stream() const { return stream; }
 
   private:
@@ -113,13 +123,14 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        est, hist, kcut, pmin, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
         dbgbuf;
     int nseg = 0;
     uint8_t *h_packed = nullptr;
     size_t h_packed_cap = 0;
     std::vector<int32_t> h_lengths;
-    std::vector<uint8_t> h_npasses, h_P;
+    std::vector<uint8_t> h_npasses, h_P, h_pmin;
+    std::vector<int64_t> h_hist;
     std::vector<int2> h_items;
     std::vector<uint64_t> h_slot;
 };

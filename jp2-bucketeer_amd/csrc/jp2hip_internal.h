@@ -12,6 +12,12 @@
 namespace jp2hip {
 
 constexpr int kMaxPasses = 96;    // 3*32-2 rounded up; per-block pass table stride
+// slope prediction (kernels.hip k_plane_*, oracle predict_and_code): 1/8-octave
+// bins of the double slope's bit pattern covering 2^-64 .. 2^64, and the
+// margin (bins) kept below the predicted rate-target bin
+constexpr int kSlopeBins = 1024;
+constexpr int kSlopeBinBase = (1023 - 64) << 3;
+constexpr int kSkipMargin = 12;
 constexpr int kMaxLayers = 32;
 constexpr int kMaxLevels = 12;
 

@@ -117,6 +117,7 @@ struct QuantArgs {
     int32_t *sm;
     uint8_t *P;
     int64_t *dref, *dsig;  // [block][32]
+    uint32_t *est;         // [block][32] predicted coded size of plane p, 1/16 bit
 };
 
 __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
@@ -154,6 +155,13 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     uint64_t *B = a.bp + d.bp_off;
     uint64_t *S = B + (size_t)d.Mb * 64;
     uint64_t *SG = B + (size_t)2 * d.Mb * 64;
+    // lane p also gathers plane p's slope-prediction counts (oracle
+    // plane_stats): significant samples, and insignificant samples with a
+    // significant 8-neighbour (row y-1 is finalised once row y is known)
+    const uint64_t wmask = d.w >= 64 ? ~0ull : ((1ull << d.w) - 1ull);
+    auto dil = [](uint64_t m) { return m | (m << 1) | (m >> 1); };
+    uint64_t up = 0, mid = 0;
+    uint32_t cntS = 0, nnb = 0;
     for (int y = 0; y < d.h; y++) {
         uint32_t word = act ? (uint32_t)sm[y * 64 + lane] : 0u;
         uint32_t v = word & 0x7FFFFFFFu;
@@ -169,6 +177,16 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             S[(size_t)lane * 64 + y] = myS;
         }
         if (lane == 63) SG[y] = sg;
+        cntS += __popcll(myS);
+        if (y > 0) nnb += __popcll((dil(up) | dil(mid) | dil(myS)) & ~mid & wmask);
+        up = mid;
+        mid = myS;
+    }
+    nnb += __popcll((dil(up) | dil(mid)) & ~mid & wmask);
+    {
+        const uint32_t nref = (uint32_t)__shfl_down((int)cntS, 1, 64);  // |S[p+1]|
+        const uint32_t nnew = cntS - (lane < 63 ? nref : 0u);
+        if (lane < P) a.est[(size_t)b * 32 + lane] = 16u * (lane < 63 ? nref : 0u) + 56u * nnew + 5u * nnb;
     }
     bool lossless = a.reversible != 0;
     for (int p = 0; p < P; p++) {
@@ -190,6 +208,93 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             a.dsig[(size_t)b * 32 + p] = sig;
         }
     }
+}
+
+// --------------------------------------------------------------------------
+// S4b: slope prediction (rate-driven encodes; oracle/jp2_oracle.c
+// predict_and_code).  kdu_compress "-rate" (KakaduConverter.java:44) stops
+// its block coder at a predicted slope threshold instead of coding passes
+// PCRD-opt will discard.  Plane p of a block has predicted slope
+// pd * weight / est; est is histogrammed over 1/8-octave slope bins, the bin
+// where the predicted size reaches the target fixes the cut, and planes more
+// than kSkipMargin bins below it are not coded (pmin = lowest coded plane).
+// All integer after the one IEEE division, so the oracle agrees bit for bit.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ int slope_bin(double s) {
+    if (!(s > 0.0)) return -1;
+    const uint64_t k = (uint64_t)__double_as_longlong(s);
+    const int b = (int)(k >> 49) - kSlopeBinBase;
+    return b < 0 ? 0 : (b >= kSlopeBins ? kSlopeBins - 1 : b);
+}
+__device__ __forceinline__ int plane_bin(int64_t pd, double wgt, uint32_t est) {
+    if (est == 0) return pd > 0 ? kSlopeBins - 1 : -1;
+    return slope_bin((double)pd * wgt / (double)est);
+}
+
+struct PredictArgs {
+    int nblocks;
+    const uint8_t *P;
+    const int64_t *dref, *dsig;
+    const uint32_t *est;
+    const double *weight;
+    unsigned long long *hist;  // [kSlopeBins]
+    int *kcut;
+    uint8_t *pmin;
+};
+
+__global__ void __launch_bounds__(256) k_plane_hist(PredictArgs a) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nblocks) return;
+    const int P = a.P[b];
+    const double wgt = a.weight[b];
+    for (int p = 0; p < P; p++) {
+        const size_t i = (size_t)b * 32 + p;
+        const int k = plane_bin(a.dref[i] + a.dsig[i], wgt, a.est[i]);
+        if (k >= 0) atomicAdd(&a.hist[k], (unsigned long long)a.est[i]);
+    }
+}
+
+// kstar = #{k in [1, kSlopeBins) : sum_{j >= k} hist[j] >= goal} (the
+// oracle's downward scan), kcut = kstar - kSkipMargin.  One wave; lane l owns
+// bins [16 l, 16 l + 16).
+__global__ void __launch_bounds__(64) k_plane_cut(const unsigned long long *hist, int64_t goal, int *kcut) {
+    const int lane = threadIdx.x;
+    constexpr int kPer = kSlopeBins / 64;
+    unsigned long long h[kPer], part = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) { h[i] = hist[lane * kPer + i]; part += h[i]; }
+    // exclusive suffix sum over lanes: bins above this lane's range
+    unsigned long long above = 0;
+    for (int o = 1; o < 64; o++) {
+        const int src = lane + o;
+        const unsigned long long v = (unsigned long long)__shfl((long long)part, src < 64 ? src : 63, 64);
+        above += src < 64 ? v : 0ull;
+    }
+    int cnt = 0;
+    unsigned long long acc = above;
+#pragma unroll
+    for (int i = kPer - 1; i >= 0; i--) {
+        acc += h[i];
+        const int k = lane * kPer + i;
+        cnt += (k >= 1 && acc >= (unsigned long long)goal) ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (lane == 0) *kcut = cnt - kSkipMargin;
+}
+
+__global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nblocks) return;
+    const int P = a.P[b];
+    const int kc = *a.kcut;
+    const double wgt = a.weight[b];
+    int pmin = P > 0 ? P - 1 : 0;
+    for (int p = 0; p < P; p++) {
+        const size_t i = (size_t)b * 32 + p;
+        if (plane_bin(a.dref[i] + a.dsig[i], wgt, a.est[i]) >= kc) { pmin = p; break; }
+    }
+    a.pmin[b] = (uint8_t)pmin;
 }
 
 // --------------------------------------------------------------------------
@@ -406,7 +511,8 @@ bool GpuEncoder::dump(const char *dir, const char *name, const DevBuf &b, size_t
 }
 
 bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Plan &plan,
-                           bool profile, StageTimes &st, std::string &err) {
+                           bool profile, StageTimes &st, std::string &err, int64_t skip_target,
+                           const HistReduce *reduce) {
     HIPCHECK(hipSetDevice(device));
     const int nb = (int)plan.blocks.size();
     size_t plane = (size_t)plan.plane_w * plan.plane_h;
@@ -418,6 +524,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<uint8_t>(P, nb, err)) return false;
     if (!ensure<int64_t>(dref, (size_t)nb * 32, err)) return false;
     if (!ensure<int64_t>(dsig, (size_t)nb * 32, err)) return false;
+    if (!ensure<uint32_t>(est, (size_t)nb * 32, err)) return false;
+    if (!ensure<uint8_t>(pmin, nb, err)) return false;
+    if (!ensure<unsigned long long>(hist, kSlopeBins, err)) return false;
+    if (!ensure<int>(kcut, 1, err)) return false;
     if (!ensure<uint8_t>(t1out, plan.out_bytes, err)) return false;
     if (!ensure<int32_t>(rates, (size_t)nb * kMaxPasses, err)) return false;
     if (!ensure<int64_t>(dists, (size_t)nb * kMaxPasses, err)) return false;
@@ -496,27 +606,65 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.P = (uint8_t *)P.ptr;
     qa.dref = (int64_t *)dref.ptr;
     qa.dsig = (int64_t *)dsig.ptr;
+    qa.est = (uint32_t *)est.ptr;
     if (nb) hipLaunchKernelGGL(k_quant, dim3(nb), dim3(64), 0, stream, qa);
     HIPCHECK(hipGetLastError());
+    // S4b: slope prediction -> lowest coded plane per block
+    if (skip_target > 0 && nb) {
+        PredictArgs pa;
+        pa.nblocks = nb;
+        pa.P = (const uint8_t *)P.ptr;
+        pa.dref = (const int64_t *)dref.ptr;
+        pa.dsig = (const int64_t *)dsig.ptr;
+        pa.est = (const uint32_t *)est.ptr;
+        pa.weight = (const double *)weight.ptr;
+        pa.hist = (unsigned long long *)hist.ptr;
+        pa.kcut = (int *)kcut.ptr;
+        pa.pmin = (uint8_t *)pmin.ptr;
+        HIPCHECK(hipMemsetAsync(hist.ptr, 0, sizeof(unsigned long long) * kSlopeBins, stream));
+        hipLaunchKernelGGL(k_plane_hist, dim3((nb + 255) / 256), dim3(256), 0, stream, pa);
+        HIPCHECK(hipGetLastError());
+        if (reduce) {
+            h_hist.resize(kSlopeBins);
+            HIPCHECK(hipMemcpyAsync(h_hist.data(), hist.ptr, sizeof(int64_t) * kSlopeBins, hipMemcpyDeviceToHost,
+                                    stream));
+            HIPCHECK(hipStreamSynchronize(stream));
+            if (!(*reduce)(h_hist)) {
+                err = "split: slope-prediction exchange failed";
+                return false;
+            }
+            HIPCHECK(hipMemcpyAsync(hist.ptr, h_hist.data(), sizeof(int64_t) * kSlopeBins, hipMemcpyHostToDevice,
+                                    stream));
+        }
+        hipLaunchKernelGGL(k_plane_cut, dim3(1), dim3(64), 0, stream, (const unsigned long long *)hist.ptr,
+                           skip_target * 128, (int *)kcut.ptr);
+        hipLaunchKernelGGL(k_plane_pmin, dim3((nb + 255) / 256), dim3(256), 0, stream, pa);
+        HIPCHECK(hipGetLastError());
+    } else if (nb) {
+        HIPCHECK(hipMemsetAsync(pmin.ptr, 0, nb, stream));
+    }
     HIPCHECK(hipEventRecord(ev[3], stream));
     // S5: tier-1.  Items (block, plane) ordered by plane depth from the top,
     // then by block shape, so a wavefront's lanes do similar work.
     h_P.resize(nb);
+    h_pmin.resize(nb);
     HIPCHECK(hipMemcpyAsync(h_P.data(), P.ptr, nb, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(h_pmin.data(), pmin.ptr, nb, hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipStreamSynchronize(stream));
     h_slot.resize(nb);
     uint64_t stream_bytes = 0;
     int maxP = 0;
     for (int i = 0; i < nb; i++) {
+        const int pc = h_P[i] - h_pmin[i];  // coded planes, from the top
         h_slot[i] = stream_bytes;
-        stream_bytes += (uint64_t)h_P[i] * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
-        maxP = std::max(maxP, (int)h_P[i]);
+        stream_bytes += (uint64_t)pc * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
+        maxP = std::max(maxP, pc);
     }
     h_items.clear();
     for (int k = 0; k < maxP; k++)
         for (int i = 0; i < nb; i++) {
             int bb = plan.t1_order[i];
-            if (h_P[bb] > k) h_items.push_back(make_int2(bb, h_P[bb] - 1 - k));
+            if (h_P[bb] - h_pmin[bb] > k) h_items.push_back(make_int2(bb, h_P[bb] - 1 - k));
         }
     const int nitems = (int)h_items.size();
     if (!ensure<int2>(items, std::max(nitems, 1), err) || !ensure<uint64_t>(slotoff, nb, err) ||
@@ -543,8 +691,8 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     // MQ lane order: blocks by decreasing decision count
     if (!ensure<uint32_t>(ordkey, nb, err) || !ensure<uint32_t>(ordkey2, nb, err) || !ensure<int32_t>(ordval, nb, err))
         return false;
-    launch_t1_keys(nb, (const uint8_t *)P.ptr, (const uint4 *)counts.ptr, (uint32_t *)ordkey.ptr,
-                   (int32_t *)ordval.ptr, stream);
+    launch_t1_keys(nb, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr, (const uint4 *)counts.ptr,
+                   (uint32_t *)ordkey.ptr, (int32_t *)ordval.ptr, stream);
     HIPCHECK(hipGetLastError());
     if (nb) {
         size_t tb = 0;
@@ -560,6 +708,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ma.order = (const int32_t *)order.ptr;
     ma.nblocks = nb;
     ma.P = (const uint8_t *)P.ptr;
+    ma.pmin = (const uint8_t *)pmin.ptr;
     ma.stream = (const uint8_t *)stream_buf.ptr;
     ma.slot_off = (const uint64_t *)slotoff.ptr;
     ma.counts = (const uint4 *)counts.ptr;

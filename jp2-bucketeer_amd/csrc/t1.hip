@@ -542,12 +542,13 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     const uint64_t w0 = wall_clock64();
     const int b = a.order[gi];
     const BlockDesc d = a.blocks[b];
-    const int P = a.P[b];
-    if (P == 0) {
+    const int Pt = a.P[b];
+    if (Pt == 0) {
         a.npasses[b] = 0;
         a.lengths[b] = 0;
         return;
     }
+    const int P = Pt - a.pmin[b];  // coded planes Pt-1 .. pmin (slope prediction)
     uint32_t *cx = cxs + lane;
 #pragma unroll
     for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];
@@ -576,7 +577,7 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     for (;;) {
         // close finished segments (empty passes close at once)
         while (left <= 0 && s < nseg) {
-            const int p = P - 1 - k;
+            const int p = Pt - 1 - k;
             R[s] = m.bp + 3;
             D[s] = pass == 0 ? dspp[k] : (pass == 1 ? dref[p] : dsig[p] - dspp[k]);
             if (++s >= nseg) break;
@@ -639,12 +640,13 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
 // Tier-1 lane order: blocks by decreasing decision count (all passes), so the
 // lanes of a wave carry similar work.  keys = ~count: an ascending radix sort
 // yields the descending order.
-__global__ void __launch_bounds__(256) k_t1_keys(int nblocks, const uint8_t *P, const uint4 *counts,
-                                                 uint32_t *keys, int32_t *vals) {
+__global__ void __launch_bounds__(256) k_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin,
+                                                 const uint4 *counts, uint32_t *keys, int32_t *vals) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblocks) return;
     uint32_t n = 0;
-    for (int k = 0; k < P[b]; k++) {
+    const int pc = P[b] ? P[b] - pmin[b] : 0;
+    for (int k = 0; k < pc; k++) {
         const uint4 c = counts[(size_t)b * 32 + k];
         n += c.x + c.y + c.z;
     }
@@ -656,9 +658,11 @@ void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (a.nitems)
         hipLaunchKernelGGL(k_t1_cm, dim3((a.nitems + kCmWaves - 1) / kCmWaves), dim3(64 * kCmWaves), 0, st, a);
 }
-void launch_t1_keys(int nblocks, const uint8_t *P, const uint4 *counts, uint32_t *keys, int32_t *vals,
-                    hipStream_t st) {
-    if (nblocks) hipLaunchKernelGGL(k_t1_keys, dim3((nblocks + 255) / 256), dim3(256), 0, st, nblocks, P, counts, keys, vals);
+void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
+                    int32_t *vals, hipStream_t st) {
+    if (nblocks)
+        hipLaunchKernelGGL(k_t1_keys, dim3((nblocks + 255) / 256), dim3(256), 0, st, nblocks, P, pmin, counts, keys,
+                           vals);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
     if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + a.lanes - 1) / a.lanes), dim3(64), 0, st, a);

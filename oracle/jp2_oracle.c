@@ -79,6 +79,7 @@ void oracle_recipe_init(oracle_recipe *r, int lossless) {
     r->rate_bpp = lossless ? 0.0 : 3.0;
     r->format = 2;
     r->comment = 1;
+    r->slope_skip = 1;
 }
 
 /* precinct exponent for resolution r (0 = lowest) given Kakadu ordering */
@@ -599,6 +600,15 @@ static void code_sign(t1ctx *t, int x, int y) {
 int oracle_t1_encode(const int32_t *sm, int w, int h, int band, int lossless,
                      uint8_t *out, int cap, int *out_len, int32_t *rates, int64_t *dists,
                      int *nplanes) {
+    return oracle_t1_encode_planes(sm, w, h, band, lossless, 0, out, cap, out_len, rates, dists, nplanes);
+}
+
+/* Planes P-1 .. pmin only: the codeword is flushed after the last coded
+ * pass, so the truncation lengths of the coded passes are those of a block
+ * whose lower planes do not exist. */
+int oracle_t1_encode_planes(const int32_t *sm, int w, int h, int band, int lossless, int pmin,
+                            uint8_t *out, int cap, int *out_len, int32_t *rates, int64_t *dists,
+                            int *nplanes) {
     uint32_t maxv = 0;
     for (int i = 0; i < w * h; i++) {
         uint32_t v = (uint32_t)sm[i] & 0x7FFFFFFFu;
@@ -616,7 +626,9 @@ int oracle_t1_encode(const int32_t *sm, int w, int h, int band, int lossless,
     mq_init(&mq, buf + 1);
     t1ctx t = {w, h, sm, flags, flags + fs, flags + 2 * fs, band, lossless, &mq};
     int np = 0;
-    for (int p = P - 1; p >= 0; p--) {
+    if (pmin < 0) pmin = 0;
+    if (pmin > P - 1) pmin = P - 1;
+    for (int p = P - 1; p >= pmin; p--) {
         for (int pass = (p == P - 1 ? 2 : 0); pass < 3; pass++) {
             int64_t dd = 0;
             for (int y0 = 0; y0 < h; y0 += 4) {
@@ -820,6 +832,10 @@ typedef struct {
     double hslope[101];
     int nl[32];          /* cumulative passes after layer l */
     int lblock, incl;
+    int32_t *sm;         /* quantised samples, kept until slope prediction ran */
+    int pmin;            /* lowest coded bit-plane */
+    uint32_t est[32];    /* predicted coded size of plane p, 1/16 bit */
+    int64_t pd[32];      /* exact distortion decrease of plane p */
 } cblk;
 
 typedef struct {
@@ -851,6 +867,7 @@ typedef struct {
     cblk **all;
     int nall, capall;
     double compw[4];
+    int skip;            /* slope prediction active (rate-driven + slope_skip) */
 } encoder;
 
 static void add_block(encoder *E, cblk *b) {
@@ -898,6 +915,128 @@ static void tile_samples(const encoder *E, const void *pix, int tx0, int ty0, in
             }
         }
     }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Slope prediction (rate-driven encodes only)                               */
+/* ------------------------------------------------------------------------ */
+/* kdu_compress with "-rate" (KakaduConverter.java:44) does not code the
+ * passes PCRD-opt will certainly discard: its block coder stops at a slope
+ * threshold predicted from the rate target.  Restated here exactly and
+ * deterministically: each bit-plane p of a block gets a predicted coded size
+ *     est = 16*refine + 56*new + 5*insignificant-next-to-significant
+ * (1/16 bit: ~1 bit per refinement, ~3.5 bits per newly significant sample
+ * with its sign, ~0.3 bit per zero decision next to significance) and its
+ * exact distortion decrease pd; slope = pd * weight / est.  A histogram of
+ * est over slope bins (1/8 octave) locates the bin where the predicted size
+ * reaches the rate target; planes more than kSkipMargin bins (1.5 octaves)
+ * below it are not coded.  PCRD-opt then runs on the coded passes as usual. */
+enum { kSlopeBins = 1024, kSlopeBinBase = (1023 - 64) << 3, kSkipMargin = 12 };
+
+static int slope_bin(double s) {
+    if (!(s > 0.0)) return -1;
+    uint64_t k;
+    memcpy(&k, &s, 8);
+    int b = (int)(k >> 49) - kSlopeBinBase;
+    return b < 0 ? 0 : (b >= kSlopeBins ? kSlopeBins - 1 : b);
+}
+
+static int plane_bin(const cblk *b, int p) {
+    if (b->est[p] == 0) return b->pd[p] > 0 ? kSlopeBins - 1 : -1;
+    return slope_bin((double)b->pd[p] * b->weight / (double)b->est[p]);
+}
+
+static void plane_stats(cblk *b, const int32_t *sm, int lossless) {
+    uint32_t maxv = 0;
+    int w = b->w, h = b->h;
+    for (int i = 0; i < w * h; i++) {
+        uint32_t v = (uint32_t)sm[i] & 0x7FFFFFFFu;
+        if (v > maxv) maxv = v;
+    }
+    int P = 0;
+    while (P < 31 && (maxv >> P)) P++;
+    b->P = P;
+    for (int p = 0; p < P; p++) {
+        int64_t nref = 0, nnew = 0, nnb = 0, pd = 0;
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                uint32_t v = (uint32_t)sm[y * w + x] & 0x7FFFFFFFu;
+                if (v >> p) {
+                    pd += dist_at(v, p + 1, lossless) - dist_at(v, p, lossless);
+                    if (v >> (p + 1)) nref++;
+                    else nnew++;
+                    continue;
+                }
+                int nb = 0;
+                for (int dy = -1; dy <= 1 && !nb; dy++)
+                    for (int dx = -1; dx <= 1 && !nb; dx++) {
+                        int xx = x + dx, yy = y + dy;
+                        if ((dx || dy) && xx >= 0 && xx < w && yy >= 0 && yy < h &&
+                            (((uint32_t)sm[yy * w + xx] & 0x7FFFFFFFu) >> p))
+                            nb = 1;
+                    }
+                nnb += nb;
+            }
+        b->est[p] = (uint32_t)(16 * nref + 56 * nnew + 5 * nnb);
+        b->pd[p] = pd;
+    }
+}
+
+/* lowest plane to code: the lowest whose bin reaches kcut (at least the top) */
+static int plane_cut(const cblk *b, int kcut) {
+    int pmin = b->P > 0 ? b->P - 1 : 0;
+    for (int p = 0; p < b->P; p++)
+        if (plane_bin(b, p) >= kcut) { pmin = p; break; }
+    return pmin;
+}
+
+/* bin threshold for a target of `target` bytes from the summed histogram */
+static int predict_cut(const int64_t *hist, int64_t target) {
+    int64_t acc = 0, goal = target * 128;  /* est is in 1/16 bit */
+    int k = kSlopeBins - 1;
+    for (; k > 0; k--) {
+        acc += hist[k];
+        if (acc >= goal) break;
+    }
+    return k - kSkipMargin;
+}
+
+/* T1-code every block with its predicted plane range (skip mode) */
+static int predict_and_code(encoder *E, int64_t target) {
+    int64_t *hist = (int64_t *)calloc(kSlopeBins, sizeof(int64_t));
+    for (int i = 0; i < E->nall; i++) {
+        cblk *b = E->all[i];
+        for (int p = 0; p < b->P; p++) {
+            int k = plane_bin(b, p);
+            if (k >= 0) hist[k] += b->est[p];
+        }
+    }
+    int kcut = predict_cut(hist, target);
+    if (getenv("ORACLE_SKIP_DEBUG")) { int64_t tot = 0; int lo = -1, hi = -1; for (int k = 0; k < kSlopeBins; k++) { tot += hist[k]; if (hist[k] && lo < 0) lo = k; if (hist[k]) hi = k; } fprintf(stderr, "skip: target %lld est_total_bytes %lld bins %d..%d kcut %d\n", (long long)target, (long long)(tot / 128), lo, hi, kcut); }
+    free(hist);
+    int lossless = E->rc->reversible;
+    /* pass 0: predicted plane ranges.  Safety net: if every coded byte
+     * together stays below the target while planes were skipped, the
+     * prediction undershot -- code everything (pass 1). */
+    for (int pass = 0; pass < 2; pass++) {
+        int64_t total = 0;
+        int skipped = 0;
+        for (int i = 0; i < E->nall; i++) {
+            cblk *b = E->all[i];
+            b->pmin = pass == 0 ? plane_cut(b, kcut) : 0;
+            skipped |= b->pmin > 0;
+            int cap = b->w * b->h * 8 + 256;
+            if (!b->data) b->data = (uint8_t *)malloc((size_t)cap);
+            int np = oracle_t1_encode_planes(b->sm, b->w, b->h, b->band, lossless, b->pmin, b->data, cap,
+                                             &b->len, b->rates, b->dd, &b->P);
+            if (np < 0) return -1;
+            b->npasses = np;
+            total += b->len;
+        }
+        if (pass == 0 && !(skipped && total < target)) break;
+    }
+    for (int i = 0; i < E->nall; i++) { free(E->all[i]->sm); E->all[i]->sm = NULL; }
+    return 0;
 }
 
 /* encode all code-blocks of one tile-component; builds the precinct model */
@@ -985,6 +1124,15 @@ static int code_tilecomp(encoder *E, tileinfo *T, int c, void *buf, int tw, int 
                                     if (v > vmax) v = vmax;
                                     sm[yy * b->w + xx] = (int32_t)((s << 31) | v);
                                 }
+                            }
+                            if (E->skip) {
+                                /* slope prediction first needs every block's
+                                 * plane statistics: code later */
+                                plane_stats(b, sm, rc->reversible);
+                                b->sm = sm;
+                                pb->blk[(cy - cy0) * pb->ncw + (cx - cx0)] = b;
+                                add_block(E, b);
+                                continue;
                             }
                             int cap = b->w * b->h * 8 + 256;
                             b->data = (uint8_t *)malloc((size_t)cap);
@@ -1363,7 +1511,7 @@ static void free_encoder(encoder *E) {
         }
         free(E->tiles);
     }
-    for (int i = 0; i < E->nall; i++) { free(E->all[i]->data); free(E->all[i]); }
+    for (int i = 0; i < E->nall; i++) { free(E->all[i]->data); free(E->all[i]->sm); free(E->all[i]); }
     free(E->all);
 }
 
@@ -1382,6 +1530,7 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
     encoder E;
     memset(&E, 0, sizeof E);
     E.rc = rc; E.w = w; E.h = h; E.nc = nc; E.bits = bits;
+    E.skip = rc->slope_skip && rc->rate_bpp > 0.0;
     E.ntx = ceil_div(w, rc->tile_w);
     E.nty = ceil_div(h, rc->tile_h);
     /* component MSE weights: energy of the inverse colour transform columns */
@@ -1415,6 +1564,11 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
             }
             for (int c = 0; c < nc; c++) free(planes[c]);
         }
+    }
+    if (E.skip &&
+        predict_and_code(&E, (int64_t)floor(rc->rate_bpp * (double)w * (double)h / 8.0))) {
+        free_encoder(&E);
+        return -1;
     }
     /* PCRD */
     int ns = 0;

@@ -45,6 +45,9 @@ typedef struct oracle_recipe {
     double rate_bpp;           /* -rate 3 ; <= 0 => "-rate -" (all passes)   */
     int32_t format;            /* 0 raw J2K codestream, 1 JP2, 2 JPX         */
     int32_t comment;           /* write a COM marker                         */
+    int32_t slope_skip;        /* rate-driven only: skip bit-planes whose    */
+                               /* predicted slope is far below the target's  */
+                               /* (Kakadu-style slope prediction); 0 = off   */
 } oracle_recipe;
 
 /* Fill the Bucketeer recipe: lossless != 0 -> LOSSLESS_OPTIONS, else LOSSY. */
@@ -74,6 +77,10 @@ void oracle_fdwt(void *data, int w, int h, int levels, int reversible);
 int oracle_t1_encode(const int32_t *sm, int w, int h, int band, int lossless,
                      uint8_t *out_bytes, int cap, int *out_len,
                      int32_t *rates, int64_t *dists, int *nplanes);
+/* Same, coding only bit-planes >= pmin (the planes slope prediction keeps). */
+int oracle_t1_encode_planes(const int32_t *sm, int w, int h, int band, int lossless, int pmin,
+                            uint8_t *out_bytes, int cap, int *out_len,
+                            int32_t *rates, int64_t *dists, int *nplanes);
 
 /* Debug: MQ decisions coded since the previous call (workload analysis). */
 int64_t oracle_debug_decisions(void);

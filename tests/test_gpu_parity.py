@@ -95,6 +95,23 @@ def test_golden_lossy_cases(encoder, golden, case):
     assert ps >= c["opj_psnr"] - 0.1
 
 
+@pytest.mark.parametrize("rate", [3.0, 1.0])
+def test_slope_prediction_on_off_both_identical_to_oracle(encoder, rate):
+    """Slope prediction (recipe.slope_skip, default on for rate-driven
+    encodes) codes fewer bit-planes; with it on or off the GPU output equals
+    the oracle's, and the rate is met either way."""
+    img = _img(517, 1030, 3, 8, seed=41)
+    tif = im.tiff_bytes(img)
+    mq = {}
+    for skip in (0, 1):
+        rc = jp2hip.recipe(jp2hip.LOSSY, rate_bpp=rate, slope_skip=skip)
+        got, st = encoder.encode_tiff(tif, jp2hip.LOSSY, rc)
+        assert got == ol.encode(img, ol.copy_recipe(rc)), skip
+        assert len(im.codestream(got)) <= rate * 517 * 1030 / 8
+        mq[skip] = st.t1_bytes
+    assert mq[1] < 0.8 * mq[0]
+
+
 def test_c2_full_size_identical_and_on_rate(encoder):
     """C2 at full size: 6000x4000 RGB8 lossy 3 bpp."""
     img = im.synth_rgb8(4000, 6000, seed=1234)

@@ -127,3 +127,26 @@ def test_oracle_t1_empty_and_single_sample():
     one[5, 7] = 1 | (1 << 31)
     b, r, d, P = ol.t1_encode(one.view(np.int32), 3, True)
     assert P == 1 and len(r) == 1 and d[0] > 0 and r[-1] == len(b)
+
+
+def test_oracle_slope_prediction_skips_planes_not_quality():
+    """Slope prediction (rate-driven only): fewer MQ decisions, same rate, no
+    PSNR loss against coding every pass (oracle predict_and_code)."""
+    img = im.synth_rgb8(512, 1024, seed=11)
+    L = ol.lib()
+    res = {}
+    for skip in (0, 1):
+        L.oracle_debug_decisions()
+        cs = ol.encode(img, ol.recipe(False, format=0, slope_skip=skip))
+        res[skip] = (L.oracle_debug_decisions(), len(cs), im.psnr(img, im.decode_pillow(cs)))
+    assert res[1][0] < 0.8 * res[0][0]
+    target = int(3.0 * 512 * 1024 / 8)
+    assert target * 0.97 <= res[1][1] <= target
+    assert res[1][2] >= res[0][2] - 0.02
+
+
+def test_oracle_slope_prediction_inactive_for_lossless():
+    img = im.synth_rgb8(200, 300, seed=3)
+    a = ol.encode(img, ol.recipe(True, format=0, slope_skip=1))
+    b = ol.encode(img, ol.recipe(True, format=0, slope_skip=0))
+    assert a == b

@@ -258,6 +258,24 @@ def test_split_parts_concatenate_to_single_gpu_file(encoder, case):
 
 
 @pytest.mark.gpu
+def test_split_slope_prediction_is_global(encoder):
+    """Gray16 at 1 bpp: slope prediction skips planes, and its histogram is
+    summed over ranks, so every world size reproduces the single-GPU file."""
+    import oracle_lib as ol
+    img = im.synth_u16(1100, 900, comps=1, seed=12)
+    rc = jp2hip.recipe(jp2hip.LOSSY, levels=7, tile_w=256, tile_h=256, rate_bpp=1.0)
+    tif = im.tiff_bytes(img)
+    single, st = encoder.encode_tiff(tif, jp2hip.LOSSY, rc)
+    assert single == ol.encode(img, ol.copy_recipe(rc))
+    _, st0 = encoder.encode_tiff(tif, jp2hip.LOSSY, jp2hip.recipe(jp2hip.LOSSY, levels=7, tile_w=256, tile_h=256,
+                                                                  rate_bpp=1.0, slope_skip=0))
+    assert st.t1_bytes < st0.t1_bytes
+    for world in (2, 3):
+        got, _ = _encode_world(tif, jp2hip.LOSSY, rc, world)
+        assert got == single, world
+
+
+@pytest.mark.gpu
 def test_split_band_only_upload(encoder):
     img = im.synth_u16(1500, 800, comps=1, seed=8)
     rc = jp2hip.recipe(jp2hip.LOSSY, levels=7, tile_w=256, tile_h=256)
