@@ -243,7 +243,8 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
             cs_bytes = t2_headers(in, t2);
             t2ms += now_ms() - t0;
             if (cs_bytes <= target) break;
-            budget -= (cs_bytes - target) << it;  // exponential back-off, as the oracle
+            // exponential back-off + 1/16 of the overshoot + 64 B, as the oracle
+            budget -= ((cs_bytes - target) << it) + ((cs_bytes - target) >> 4) + 64;
         }
     }
     // t2 now describes the final layer table; fetch the bytes it includes
@@ -423,7 +424,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
             for (int l = 0; l < L; l++) budgets[l] = budget >> (L - 1 - l);
             if (!round()) return fail(err);
             if (cs_bytes <= target) break;
-            budget -= (cs_bytes - target) << it;  // as encode_core / the oracle
+            budget -= ((cs_bytes - target) << it) + ((cs_bytes - target) >> 4) + 64;  // as encode_core
         }
     }
     // this rank's included bytes

@@ -242,16 +242,23 @@ struct PredictArgs {
     uint8_t *pmin;
 };
 
+// Thread per (block, plane) slot; neighbouring blocks land in few bins, so
+// the workgroup sums into an LDS histogram first.
 __global__ void __launch_bounds__(256) k_plane_hist(PredictArgs a) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.nblocks) return;
-    const int P = a.P[b];
-    const double wgt = a.weight[b];
-    for (int p = 0; p < P; p++) {
-        const size_t i = (size_t)b * 32 + p;
-        const int k = plane_bin(a.dref[i] + a.dsig[i], wgt, a.est[i]);
-        if (k >= 0) atomicAdd(&a.hist[k], (unsigned long long)a.est[i]);
+    __shared__ unsigned long long lh[kSlopeBins];
+    for (int i = threadIdx.x; i < kSlopeBins; i += 256) lh[i] = 0;
+    __syncthreads();
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // block * 32 + plane
+    if (i < (size_t)a.nblocks * 32) {
+        const int b = (int)(i >> 5), p = (int)(i & 31);
+        if (p < a.P[b]) {
+            const int k = plane_bin(a.dref[i] + a.dsig[i], a.weight[b], a.est[i]);
+            if (k >= 0) atomicAdd(&lh[k], (unsigned long long)a.est[i]);
+        }
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kSlopeBins; k += 256)
+        if (lh[k]) atomicAdd(&a.hist[k], lh[k]);
 }
 
 // kstar = #{k in [1, kSlopeBins) : sum_{j >= k} hist[j] >= goal} (the
@@ -622,7 +629,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         pa.kcut = (int *)kcut.ptr;
         pa.pmin = (uint8_t *)pmin.ptr;
         HIPCHECK(hipMemsetAsync(hist.ptr, 0, sizeof(unsigned long long) * kSlopeBins, stream));
-        hipLaunchKernelGGL(k_plane_hist, dim3((nb + 255) / 256), dim3(256), 0, stream, pa);
+        hipLaunchKernelGGL(k_plane_hist, dim3((nb * 32 + 255) / 256), dim3(256), 0, stream, pa);
         HIPCHECK(hipGetLastError());
         if (reduce) {
             h_hist.resize(kSlopeBins);

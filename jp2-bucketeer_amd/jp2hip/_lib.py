@@ -12,7 +12,7 @@ from ctypes import (CFUNCTYPE, POINTER, Structure, byref, c_char_p, c_double, c_
                     c_int64, c_size_t, c_uint8, c_uint64, c_void_p)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libjp2hip.so")
+LIB_PATH = os.environ.get("JP2HIP_LIBRARY") or os.path.join(HERE, "libjp2hip.so")  # override: experiments only
 
 LOSSY = 0      # Conversion.LOSSY    (Conversion.java:9)
 LOSSLESS = 1   # Conversion.LOSSLESS (Conversion.java:9)

@@ -1616,7 +1616,11 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
             cs.n = 0;
             write_codestream(&E, &cs);
             if ((int64_t)cs.n <= target) break;
-            budget -= ((int64_t)cs.n - target) << it; /* exponential back-off */
+            if (getenv("ORACLE_RATE_DEBUG")) fprintf(stderr, "rate it %d budget %lld size %zu target %lld\n", it, (long long)budget, cs.n, (long long)target);
+            /* exponential back-off, plus 1/16 of the overshoot and 64 bytes so
+             * the second pass (headers grow with the data they describe)
+             * normally lands under the target instead of needing a third */
+            budget -= (((int64_t)cs.n - target) << it) + (((int64_t)cs.n - target) >> 4) + 64;
         }
     }
     free(S);
