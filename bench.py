@@ -368,15 +368,19 @@ def run_c5(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inflight", type=int, default=int(os.environ.get("JP2HIP_INFLIGHT", "6")),
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("JP2HIP_INFLIGHT", "12")),
                     help="independent images in flight per GPU (separate contexts/streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lossless", action="store_true")
     ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
                     help="c2: the headline (replicas); c5: one oversized image tile-split across ranks")
     args = ap.parse_args()
+    # one hardware queue per in-flight context (HIP's default of 4 makes
+    # streams share queues, and kernels of a shared queue run one at a time);
+    # must be set before anything initialises HIP
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(16, args.inflight))))
     if args.workload == "c5":
         res = run_c5(args)
         if res is not None:

@@ -117,8 +117,10 @@ class GpuEncoder {
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
     bool apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate,
                           bool profile, StageTimes &st, std::string &err);
+    bool host_wait(std::string &err);
     static constexpr int kNumEvents = 12;
     int device = 0;
+    hipEvent_t sync_ev = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,

@@ -479,9 +479,10 @@ GpuEncoder::~GpuEncoder() {
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
                      &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
-                     &stream_buf, &counts, &dspp, &dbgbuf};
+                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
+    if (sync_ev) (void)hipEventDestroy(sync_ev);
     if (stream) (void)hipStreamDestroy(stream);
     for (int i = 0; i < kNumEvents; i++)
         if (ev[i]) (void)hipEventDestroy(ev[i]);
@@ -493,6 +494,16 @@ bool GpuEncoder::init(int dev, std::string &err) {
     HIPCHECK(hipSetDevice(dev));
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (int i = 0; i < kNumEvents; i++) HIPCHECK(hipEventCreate(&ev[i]));
+    HIPCHECK(hipEventCreateWithFlags(&sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+    return true;
+}
+
+// Host waits for this context's stream by sleeping on an event rather than
+// spinning: with many images in flight the spinning callers would take the
+// cores the tier-2 threads need.
+bool GpuEncoder::host_wait(std::string &err) {
+    HIPCHECK(hipEventRecord(sync_ev, stream));
+    HIPCHECK(hipEventSynchronize(sync_ev));
     return true;
 }
 
@@ -500,14 +511,14 @@ bool GpuEncoder::upload_source(const void *host, size_t len, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     if (!ensure<uint8_t>(src, len, err)) return false;
     HIPCHECK(hipMemcpyAsync(src.ptr, host, len, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     return true;
 }
 
 bool GpuEncoder::dump(const char *dir, const char *name, const DevBuf &b, size_t bytes,
                       std::string &err) {
     std::vector<uint8_t> h(bytes);
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     if (bytes) HIPCHECK(hipMemcpy(h.data(), b.ptr, bytes, hipMemcpyDeviceToHost));
     std::string path = std::string(dir) + "/" + name;
     FILE *f = fopen(path.c_str(), "wb");
@@ -635,7 +646,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
             h_hist.resize(kSlopeBins);
             HIPCHECK(hipMemcpyAsync(h_hist.data(), hist.ptr, sizeof(int64_t) * kSlopeBins, hipMemcpyDeviceToHost,
                                     stream));
-            HIPCHECK(hipStreamSynchronize(stream));
+            if (!host_wait(err)) return false;
             if (!(*reduce)(h_hist)) {
                 err = "split: slope-prediction exchange failed";
                 return false;
@@ -657,7 +668,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     h_pmin.resize(nb);
     HIPCHECK(hipMemcpyAsync(h_P.data(), P.ptr, nb, hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipMemcpyAsync(h_pmin.data(), pmin.ptr, nb, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     h_slot.resize(nb);
     uint64_t stream_bytes = 0;
     int maxP = 0;
@@ -767,7 +778,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         HIPCHECK(hipMemcpyAsync(&tail[0], (int32_t *)segoff.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
         HIPCHECK(hipMemcpyAsync(&tail[1], (int32_t *)segcnt.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
     }
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     nseg = tail[0] + tail[1];
     if (!ensure<uint64_t>(segkey, std::max(nseg, 1), err) || !ensure<uint64_t>(segkey2, std::max(nseg, 1), err) ||
         !ensure<int64_t>(segval, std::max(nseg, 1), err) || !ensure<int64_t>(segval2, std::max(nseg, 1), err) ||
@@ -799,7 +810,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     HIPCHECK(hipMemcpyAsync(h_npasses.data(), npasses.ptr, nb, hipMemcpyDeviceToHost, stream));
     int herr = 0;
     HIPCHECK(hipMemcpyAsync(&herr, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     if (herr) {
         err = "tier-1 output capacity exceeded";
         return false;
@@ -878,7 +889,7 @@ bool GpuEncoder::apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, 
         HIPCHECK(hipMemcpyAsync(h_lrate.data(), lrate.ptr, sizeof(int32_t) * h_lrate.size(), hipMemcpyDeviceToHost,
                                 stream));
     }
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     if (profile) {
         float t;
         HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[7]));
@@ -895,7 +906,7 @@ bool GpuEncoder::segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum
         HIPCHECK(hipMemcpyAsync(keys.data(), segkey2.ptr, sizeof(uint64_t) * nseg, hipMemcpyDeviceToHost, stream));
         HIPCHECK(hipMemcpyAsync(cum.data(), segcum.ptr, sizeof(int64_t) * nseg, hipMemcpyDeviceToHost, stream));
     }
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     return true;
 }
 
@@ -924,7 +935,7 @@ bool GpuEncoder::gather(const Plan &plan, const std::vector<int32_t> &final_len,
     HIPCHECK(hipGetLastError());
     if (total) HIPCHECK(hipMemcpyAsync(h_packed, packed.ptr, total, hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipEventRecord(ev[9], stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    if (!host_wait(err)) return false;
     if (profile) {
         float t;
         HIPCHECK(hipEventElapsedTime(&t, ev[8], ev[9]));
