@@ -377,10 +377,11 @@ def main():
     ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
                     help="c2: the headline (replicas); c5: one oversized image tile-split across ranks")
     args = ap.parse_args()
-    # one hardware queue per in-flight context (HIP's default of 4 makes
-    # streams share queues, and kernels of a shared queue run one at a time);
-    # must be set before anything initialises HIP
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(16, args.inflight))))
+    # one hardware queue per in-flight context plus a few for the runtime's
+    # own streams (HIP's default of 4 makes contexts share queues, and the
+    # kernels of a shared queue run one at a time); must be set before
+    # anything initialises HIP.  Sweep: profiles/r01/sweep_q2.txt
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, args.inflight + 4))))
     if args.workload == "c5":
         res = run_c5(args)
         if res is not None:

@@ -86,6 +86,12 @@ typedef struct jp2hip_layout {
     int32_t rows_per_strip;
     int32_t nstrips;                         /* entries in strip_offsets    */
     const uint64_t *strip_offsets;           /* byte offset of each strip   */
+    int32_t compression;                     /* TIFF Compression: 1 (or 0)  */
+                                             /* none, 5 LZW, 32773 PackBits */
+    int32_t predictor;                       /* TIFF Predictor: 1 none,     */
+                                             /* 2 horizontal differencing   */
+    const uint64_t *strip_bytes;             /* compressed size per strip   */
+                                             /* (compression 5 / 32773)     */
 } jp2hip_layout;
 
 typedef struct jp2hip_stats {
@@ -133,7 +139,12 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
                        const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
                        jp2hip_stats *stats);
 
-/* Parse a baseline TIFF's header into a layout (offsets into the file). */
+/* Parse a baseline TIFF's header into a layout (offsets into the file).
+ * Strips may be uncompressed, LZW (5) or PackBits (32773), with or without
+ * horizontal differencing (Predictor 2); compressed strips are decoded on
+ * the GPU (one lane per strip) before ingest.  For a compressed file
+ * `offsets` receives 2 * nstrips entries: the strip offsets, then their byte
+ * counts (layout->strip_bytes points at the second half). */
 int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout,
                        uint64_t *offsets, int32_t max_offsets);
 

@@ -83,7 +83,7 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     size_t ifd = t.u32(4);
     if (ifd + 2 > len) return fail("tiff: IFD offset out of range");
     uint32_t ne = t.u16(ifd);
-    uint32_t w = 0, h = 0, spp = 1, bps = 8, comp = 1, planar = 1, rps = 0xFFFFFFFFu, fmt = 1;
+    uint32_t w = 0, h = 0, spp = 1, bps = 8, comp = 1, planar = 1, rps = 0xFFFFFFFFu, fmt = 1, pred = 1;
     size_t e_off = 0, e_cnt = 0;
     uint32_t n_off = 0;
     for (uint32_t i = 0; i < ne; i++) {
@@ -99,12 +99,19 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
         case 278: rps = t.val(e, 0); break;
         case 279: e_cnt = e; break;
         case 284: planar = t.val(e, 0); break;
+        case 317: pred = t.val(e, 0); break;
         case 339: fmt = t.val(e, 0); break;
         default: break;
         }
     }
     if (!w || !h || !e_off) return fail("tiff: missing ImageWidth/ImageLength/StripOffsets");
-    if (comp != 1) return fail("tiff: compression " + std::to_string(comp) + " is not supported (uncompressed only)");
+    // strips: uncompressed, LZW or PackBits (decoded on the GPU, kernels.hip
+    // k_unlzw / k_unpackbits); Deflate / JPEG / CCITT are not supported
+    if (comp != 1 && comp != 5 && comp != 32773)
+        return fail("tiff: compression " + std::to_string(comp) +
+                    " is not supported (uncompressed, LZW and PackBits only)");
+    if (pred != 1 && pred != 2) return fail("tiff: predictor " + std::to_string(pred) + " is not supported");
+    if (comp != 1 && !e_cnt) return fail("tiff: compressed strips need StripByteCounts");
     if (bps != 8 && bps != 16) return fail("tiff: " + std::to_string(bps) + " bits/sample is not supported");
     if (fmt != 1) return fail("tiff: only unsigned integer samples are supported");
     if (spp < 1 || spp > 4) return fail("tiff: " + std::to_string(spp) + " samples/pixel is not supported");
@@ -113,12 +120,19 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     uint32_t per_plane = (h + rps - 1) / rps;
     uint32_t need = per_plane * (planar == 2 ? spp : 1);
     if (n_off < need) return fail("tiff: too few strips");
-    offs.resize(need);
+    const bool packed = comp != 1;
+    offs.resize(packed ? 2 * (size_t)need : need);
     size_t row = (size_t)w * (planar == 2 ? 1 : spp) * (bps / 8);
     for (uint32_t s = 0; s < need; s++) {
         offs[s] = t.val(e_off, s);
         uint32_t y0 = (s % per_plane) * rps;
         uint32_t rows = std::min(rps, h - y0);
+        if (packed) {
+            const uint64_t nb = t.val(e_cnt, s);
+            if (offs[s] + nb > len) return fail("tiff: strip " + std::to_string(s) + " out of range");
+            offs[need + s] = nb;
+            continue;
+        }
         if (offs[s] + row * rows > len) return fail("tiff: strip " + std::to_string(s) + " out of range");
         if (e_cnt && t.val(e_cnt, s) < row * rows) return fail("tiff: strip byte count too small");
     }
@@ -131,6 +145,9 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     lay->rows_per_strip = (int32_t)rps;
     lay->nstrips = (int32_t)need;
     lay->strip_offsets = offs.data();
+    lay->compression = (int32_t)comp;
+    lay->predictor = (int32_t)pred;
+    lay->strip_bytes = packed ? offs.data() + need : nullptr;
     return 0;
 }
 
@@ -175,6 +192,31 @@ void undershoot_terms(const jp2hip::GpuEncoder &g, int64_t &coded, int64_t &skip
     for (size_t b = 0; b < pm.size(); b++) skipped |= pm[b] > 0;
 }
 
+// LZW / PackBits strips are decoded on the GPU into the context's staging
+// buffer first; afterwards (d_src, lay) describe uncompressed strips.
+bool unpack_if_compressed(jp2hip_ctx *ctx, const void *&d_src, size_t src_len, const jp2hip_layout *&lay,
+                          jp2hip_layout &ulay, std::vector<uint64_t> &uoffs, std::string &err) {
+    if (lay->compression <= 1) return true;
+    if (lay->compression != 5 && lay->compression != 32773) {
+        err = "layout: compression " + std::to_string(lay->compression) + " is not supported";
+        return false;
+    }
+    if (!lay->strip_bytes || !lay->strip_offsets || lay->nstrips <= 0 || lay->rows_per_strip <= 0) {
+        err = "layout: compressed strips need strip_offsets and strip_bytes";
+        return false;
+    }
+    for (int i = 0; i < lay->nstrips; i++)  // the decoders trust these bounds
+        if (lay->strip_offsets[i] > src_len || lay->strip_bytes[i] > src_len - lay->strip_offsets[i]) {
+            err = "layout: compressed strip " + std::to_string(i) + " lies outside the source buffer";
+            return false;
+        }
+    const void *d2 = nullptr;
+    if (!ctx->gpu.unpack_strips(d_src, *lay, ulay, uoffs, &d2, err)) return false;
+    d_src = d2;
+    lay = &ulay;
+    return true;
+}
+
 // The whole encode with the source already in device memory.  On success
 // *out is a malloc'd buffer holding the complete file.
 int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *lay,
@@ -187,9 +229,11 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     if (recipe) rc = *recipe;
     else default_recipe(&rc, conversion);
     if (!lay || !d_src) return fail("null source or layout");
-    (void)src_len;
     Plan plan;
     std::string err;
+    jp2hip_layout ulay;
+    std::vector<uint64_t> uoffs;
+    if (!unpack_if_compressed(ctx, d_src, src_len, lay, ulay, uoffs, err)) return fail(err);
     if (!build_plan(plan, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     const bool prof = ctx->cfg.profile != 0;
     StageTimes st;
@@ -318,6 +362,8 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
     if (!lay || !d_src) return fail("null source or layout");
     Plan full;
     std::string err;
+    // every rank sees the same layout, so all of them stop here together
+    if (lay->compression > 1) return fail("split: compressed strips are not supported; decode the TIFF first");
     if (!build_plan(full, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     int tr0, tr1;
     split_tile_rows(full.nty, rank, world, tr0, tr1);
@@ -555,6 +601,7 @@ int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout, u
     }
     std::memcpy(offsets, offs.data(), offs.size() * sizeof(uint64_t));
     layout->strip_offsets = offsets;
+    layout->strip_bytes = layout->compression > 1 ? offsets + layout->nstrips : nullptr;
     return 0;
 }
 

@@ -203,7 +203,7 @@ struct jp2hip_batch {
             if (offs.size() < 1024) offs.resize(1024);
             int prc = jp2hip_tiff_layout(j.src, j.src_len, &lay, offs.data(), (int32_t)offs.size());
             if (prc != 0 && lay.height > 0 && (size_t)lay.height > offs.size()) {  // more strips than slots
-                offs.resize((size_t)lay.height * (size_t)std::max(1, lay.components));
+                offs.resize(2 * (size_t)lay.height * (size_t)std::max(1, lay.components));  // + byte counts
                 prc = jp2hip_tiff_layout(j.src, j.src_len, &lay, offs.data(), (int32_t)offs.size());
             }
             if (prc != 0) {

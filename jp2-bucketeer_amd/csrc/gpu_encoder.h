@@ -80,6 +80,10 @@ class GpuEncoder {
     // host -> device copy of a source buffer into the internal `src` buffer
     bool upload_source(const void *host, size_t len, std::string &err);
     const void *source() const { return src.ptr; }
+    // LZW / PackBits strips (+ Predictor 2) -> an uncompressed staging copy
+    // in HBM; `out` describes it (offsets in out_offs)
+    bool unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2hip_layout &out,
+                       std::vector<uint64_t> &out_offs, const void **d_out, std::string &err);
 
     // Sums a slope-prediction histogram over the ranks of a tile-split
     // encode, in place; false = exchange failed (or another rank failed).
@@ -125,7 +129,7 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        est, hist, kcut, pmin, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        est, hist, kcut, pmin, stage, soff, lzwtab, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
         dbgbuf;
     int nseg = 0;
     uint8_t *h_packed = nullptr;

@@ -105,6 +105,125 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
 }
 
 // --------------------------------------------------------------------------
+// S1a: compressed strips (TIFF 6.0 sections 9, 13, 14).  The strips of an LZW
+// or PackBits TIFF are decoded in HBM before ingest: one lane per strip (each
+// strip is an independent byte stream), output strip s at s * stride of a
+// staging buffer, so ingest then reads an uncompressed layout.  Horizontal
+// differencing (Predictor 2) is undone afterwards, one lane per row.
+// --------------------------------------------------------------------------
+struct UnpackArgs {
+    const uint8_t *src;
+    const uint64_t *off, *cnt;  // per strip: byte offset and compressed size
+    int nstrips, per_plane, rps, h;
+    uint64_t row_bytes, stride;  // decoded row and strip stride (bytes)
+    uint8_t *dst;
+    uint32_t *tab;  // LZW: 4096 entries (start, length) per strip
+    int *err;
+};
+
+__device__ __forceinline__ uint64_t strip_out_bytes(const UnpackArgs &a, int s) {
+    const int y0 = (s % a.per_plane) * a.rps;
+    return (uint64_t)min(a.rps, a.h - y0) * a.row_bytes;
+}
+
+// LZW, MSB-first codes of 9..12 bits with TIFF's early width change; the
+// string of table entry k is (start, length) inside the strip's own output
+// (entry k = string(prev) + first byte of the next string, which is exactly
+// where the decoder wrote them), so decoding is copying, as in LZ77.
+__global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= a.nstrips) return;
+    const uint8_t *in = a.src + a.off[s];
+    const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
+    uint8_t *out = a.dst + (uint64_t)s * a.stride;
+    uint2 *tab = (uint2 *)(a.tab + (size_t)s * 8192);
+    uint64_t ip = 0, pos = 0, acc = 0, prev_pos = 0;
+    int nbits = 0, width = 9, next = 258;
+    uint32_t prev_len = 0;
+    bool bad = false;
+    for (;;) {
+        while (nbits < width && ip < n) { acc = (acc << 8) | in[ip++]; nbits += 8; }
+        if (nbits < width) break;  // input exhausted: treat as end of information
+        const int code = (int)((acc >> (nbits - width)) & ((1u << width) - 1u));
+        nbits -= width;
+        if (code == 257) break;
+        if (code == 256) { width = 9; next = 258; prev_len = 0; continue; }
+        const uint64_t cur = pos;
+        uint32_t len;
+        if (code < 256) {
+            if (pos >= cap) { bad = true; break; }
+            out[pos++] = (uint8_t)code;
+            len = 1;
+        } else {
+            uint64_t from;
+            if (code < next) { const uint2 e = tab[code]; from = e.x; len = e.y; }
+            else if (code == next && prev_len) { from = prev_pos; len = prev_len + 1; }
+            else { bad = true; break; }
+            if (pos + len > cap) { bad = true; break; }
+            for (uint32_t i = 0; i < len; i++) out[pos + i] = out[from + i];  // may overlap forward
+            pos += len;
+        }
+        if (prev_len && next < 4096) {
+            tab[next] = make_uint2((uint32_t)prev_pos, prev_len + 1);
+            next++;
+            if (next >= (1 << width) - 1 && width < 12) width++;
+        }
+        prev_pos = cur;
+        prev_len = len;
+    }
+    if (bad || pos != cap) atomicOr(a.err, 2);
+}
+
+// PackBits: n in 0..127 copies n+1 literal bytes, -127..-1 repeats the next
+// byte 1-n times, -128 is a no-op.
+__global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= a.nstrips) return;
+    const uint8_t *in = a.src + a.off[s];
+    const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
+    uint8_t *out = a.dst + (uint64_t)s * a.stride;
+    uint64_t ip = 0, pos = 0;
+    bool bad = false;
+    while (ip < n && pos < cap) {
+        const int c = (int8_t)in[ip++];
+        if (c >= 0) {
+            if (ip + c + 1 > n || pos + c + 1 > cap) { bad = true; break; }
+            for (int i = 0; i <= c; i++) out[pos++] = in[ip++];
+        } else if (c != -128) {
+            if (ip >= n || pos + 1 - c > cap) { bad = true; break; }
+            const uint8_t v = in[ip++];
+            for (int i = 0; i < 1 - c; i++) out[pos++] = v;
+        }
+    }
+    if (bad || pos != cap) atomicOr(a.err, 2);
+}
+
+// Predictor 2: each sample adds the same component of the pixel to its left
+// (modulo 2^bits, in the file's byte order for 16-bit samples).
+__global__ void __launch_bounds__(256) k_unpredict(uint8_t *dst, int nrows, int rows_per_strip_buf, int rps, int h,
+                                                    int per_plane, uint64_t stride, int w, int spp, int bits,
+                                                    int big_endian) {
+    const int r = blockIdx.x * 256 + threadIdx.x;  // global decoded row: strip * rps + row in strip
+    if (r >= nrows) return;
+    const int s = r / rows_per_strip_buf, y = r % rows_per_strip_buf;
+    if ((s % per_plane) * rps + y >= h || y >= rps) return;
+    const uint64_t rb = (uint64_t)w * spp * (bits >> 3);
+    uint8_t *row = dst + (uint64_t)s * stride + (uint64_t)y * rb;
+    if (bits == 8) {
+        for (int i = spp; i < w * spp; i++) row[i] = (uint8_t)(row[i] + row[i - spp]);
+    } else {
+        auto rd = [&](int i) -> uint32_t {
+            return big_endian ? ((uint32_t)row[2 * i] << 8) | row[2 * i + 1] : row[2 * i] | ((uint32_t)row[2 * i + 1] << 8);
+        };
+        for (int i = spp; i < w * spp; i++) {
+            const uint32_t v = (rd(i) + rd(i - spp)) & 0xFFFFu;
+            if (big_endian) { row[2 * i] = (uint8_t)(v >> 8); row[2 * i + 1] = (uint8_t)v; }
+            else { row[2 * i] = (uint8_t)v; row[2 * i + 1] = (uint8_t)(v >> 8); }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // S4: quantisation + bit-planes.  One wavefront per code-block; lane = column.
 // Layout per block (uint64 words): B[p][64 rows] for p < Mb, then
 // S[p][64 rows] = OR_{q>=p} B[q], then sign[64 rows].
@@ -479,7 +598,7 @@ GpuEncoder::~GpuEncoder() {
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
                      &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
-                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin};
+                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &stage, &soff, &lzwtab};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -525,6 +644,62 @@ bool GpuEncoder::dump(const char *dir, const char *name, const DevBuf &b, size_t
     if (!f) { err = "cannot write dump " + path; return false; }
     fwrite(h.data(), 1, bytes, f);
     fclose(f);
+    return true;
+}
+
+bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2hip_layout &out,
+                               std::vector<uint64_t> &out_offs, const void **d_out, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    const int ns = lay.nstrips;
+    const int per_plane = (lay.height + lay.rows_per_strip - 1) / lay.rows_per_strip;
+    const uint64_t row_bytes = (uint64_t)lay.width * (lay.planar == 2 ? 1 : lay.components) * (lay.bits / 8);
+    const uint64_t stride = ((uint64_t)lay.rows_per_strip * row_bytes + 255) & ~255ull;
+    if (!ensure<uint8_t>(stage, stride * ns, err) || !ensure<uint64_t>(soff, (size_t)ns * 2, err) ||
+        !ensure<int>(this->err, 4, err))
+        return false;
+    if (lay.compression == 5 && !ensure<uint32_t>(lzwtab, (size_t)ns * 8192, err)) return false;
+    HIPCHECK(hipMemcpyAsync(soff.ptr, lay.strip_offsets, sizeof(uint64_t) * ns, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync((uint64_t *)soff.ptr + ns, lay.strip_bytes, sizeof(uint64_t) * ns, hipMemcpyHostToDevice,
+                            stream));
+    HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
+    UnpackArgs ua;
+    ua.src = (const uint8_t *)d_src;
+    ua.off = (const uint64_t *)soff.ptr;
+    ua.cnt = (const uint64_t *)soff.ptr + ns;
+    ua.nstrips = ns;
+    ua.per_plane = per_plane;
+    ua.rps = lay.rows_per_strip;
+    ua.h = lay.height;
+    ua.row_bytes = row_bytes;
+    ua.stride = stride;
+    ua.dst = (uint8_t *)stage.ptr;
+    ua.tab = (uint32_t *)lzwtab.ptr;
+    ua.err = (int *)this->err.ptr;
+    if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
+    else hipLaunchKernelGGL(k_unpackbits, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
+    HIPCHECK(hipGetLastError());
+    if (lay.predictor == 2) {
+        const int nrows = ns * lay.rows_per_strip;
+        hipLaunchKernelGGL(k_unpredict, dim3((nrows + 255) / 256), dim3(256), 0, stream, (uint8_t *)stage.ptr, nrows,
+                           lay.rows_per_strip, lay.rows_per_strip, lay.height, per_plane, stride, lay.width,
+                           lay.planar == 2 ? 1 : lay.components, lay.bits, lay.big_endian);
+        HIPCHECK(hipGetLastError());
+    }
+    int herr = 0;
+    HIPCHECK(hipMemcpyAsync(&herr, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+    if (!host_wait(err)) return false;
+    if (herr) {
+        err = "tiff: corrupt compressed strip";
+        return false;
+    }
+    out = lay;
+    out_offs.resize(ns);
+    for (int i = 0; i < ns; i++) out_offs[i] = (uint64_t)i * stride;
+    out.strip_offsets = out_offs.data();
+    out.compression = 1;
+    out.predictor = 1;
+    out.strip_bytes = nullptr;
+    *d_out = stage.ptr;
     return true;
 }
 

@@ -42,7 +42,9 @@ class Layout(Structure):
     _fields_ = [("width", c_int32), ("height", c_int32), ("components", c_int32),
                 ("bits", c_int32), ("planar", c_int32), ("big_endian", c_int32),
                 ("rows_per_strip", c_int32), ("nstrips", c_int32),
-                ("strip_offsets", POINTER(c_uint64))]
+                ("strip_offsets", POINTER(c_uint64)),
+                ("compression", c_int32), ("predictor", c_int32),
+                ("strip_bytes", POINTER(c_uint64))]
 
 
 class Stats(Structure):
@@ -151,8 +153,11 @@ def tiff_layout(data: bytes):
     if lib().jp2hip_tiff_layout(buf, len(data), byref(lay), offs, cap) != 0:
         raise Jp2hipError(last_error())
     n = lay.nstrips
-    keep = (c_uint64 * n)(*offs[:n])
+    m = 2 * n if lay.compression > 1 else n  # compressed: offsets, then byte counts
+    keep = (c_uint64 * m)(*offs[:m])
     lay.strip_offsets = ctypes.cast(keep, POINTER(c_uint64))
+    if lay.compression > 1:
+        lay.strip_bytes = ctypes.cast(ctypes.byref(keep, 8 * n), POINTER(c_uint64))
     return lay, keep
 
 

@@ -262,3 +262,19 @@ def tile_parts(cs: bytes):
             break
         p += psot
     return out
+
+
+def tiff_bytes_compressed(img: np.ndarray, compression: str, predictor: bool = False, rows_per_strip: int = 16) -> bytes:
+    """LZW ("tiff_lzw") or PackBits ("packbits") strip TIFF written by Pillow's
+    libtiff (test fixture generator only), optionally with Predictor 2."""
+    import io
+    from PIL import Image, TiffImagePlugin
+    kw = {}
+    if predictor:
+        ti = TiffImagePlugin.ImageFileDirectory_v2()
+        ti[317] = 2
+        kw["tiffinfo"] = ti
+    row = img.shape[1] * (img.shape[2] if img.ndim == 3 else 1) * img.dtype.itemsize
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, format="TIFF", compression=compression, strip_size=row * rows_per_strip, **kw)
+    return b.getvalue()

@@ -95,14 +95,29 @@ def test_tiff_layout_rejects(bad, msg):
         jp2hip.tiff_layout(bad)
 
 
-def test_tiff_layout_rejects_compressed():
+def test_tiff_layout_rejects_unsupported_compression():
     data = bytearray(im.tiff_bytes(im.synth_rgb8(8, 8)))
-    # Compression tag (259) value -> 5 (LZW)
+    # Compression tag (259) value -> 8 (Deflate)
     i = data.find(bytes([0x03, 0x01, 0x03, 0x00, 0x01, 0x00, 0x00, 0x00, 0x01, 0x00]))
     assert i > 0
-    data[i + 8] = 5
-    with pytest.raises(jp2hip.Jp2hipError, match="compression 5"):
+    data[i + 8] = 8
+    with pytest.raises(jp2hip.Jp2hipError, match="compression 8"):
         jp2hip.tiff_layout(bytes(data))
+
+
+@pytest.mark.parametrize("comp,code,pred", [("tiff_lzw", 5, False), ("tiff_lzw", 5, True), ("packbits", 32773, False)])
+def test_tiff_layout_compressed_strips(comp, code, pred):
+    """LZW / PackBits strips: offsets, then byte counts, match the file's tags."""
+    from PIL import Image
+    import io
+    img = im.synth_rgb8(70, 90, seed=2)
+    data = im.tiff_bytes_compressed(img, comp, predictor=pred, rows_per_strip=16)
+    lay, keep = jp2hip.tiff_layout(data)
+    tags = Image.open(io.BytesIO(data)).tag_v2
+    assert lay.compression == code and lay.predictor == (2 if pred else 1)
+    assert lay.rows_per_strip == 16 and lay.nstrips == 5
+    assert [lay.strip_offsets[i] for i in range(5)] == list(tags[273])
+    assert [lay.strip_bytes[i] for i in range(5)] == list(tags[279])
 
 
 def test_conversion_ordinals_match_reference():

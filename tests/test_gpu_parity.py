@@ -154,6 +154,31 @@ def test_tiff_variants_same_output(encoder):
     assert a == b
 
 
+@pytest.mark.parametrize("comp,pred,kind", [("tiff_lzw", False, "rgb8"), ("tiff_lzw", True, "rgb8"),
+                                            ("packbits", False, "rgb8"), ("tiff_lzw", True, "gray16"),
+                                            ("packbits", False, "gray16")])
+def test_compressed_strips_same_output(encoder, comp, pred, kind):
+    """LZW / PackBits (+ Predictor 2) strips decoded on the GPU: the file equals
+    the encode of the same pixels from an uncompressed TIFF (and the oracle)."""
+    img = im.synth_rgb8(301, 517, seed=9) if kind == "rgb8" else im.synth_u16(301, 517, comps=1, seed=9)
+    for conv in (jp2hip.LOSSLESS, jp2hip.LOSSY):
+        rc = jp2hip.recipe(conv)
+        plain, _ = encoder.encode_tiff(im.tiff_bytes(img), conv, rc)
+        got, _ = encoder.encode_tiff(im.tiff_bytes_compressed(img, comp, predictor=pred, rows_per_strip=24), conv, rc)
+        assert got == plain
+    assert plain == ol.encode(img, ol.copy_recipe(rc))
+
+
+def test_corrupt_compressed_strip_fails_loudly(encoder):
+    img = im.synth_rgb8(64, 64, seed=1)
+    data = bytearray(im.tiff_bytes_compressed(img, "packbits", rows_per_strip=64))
+    lay, keep = jp2hip.tiff_layout(bytes(data))
+    o, n = lay.strip_offsets[0], lay.strip_bytes[0]
+    data[o:o + n] = bytes([0x80]) * n  # PackBits no-ops only: the strip decodes short
+    with pytest.raises(jp2hip.Jp2hipError, match="corrupt"):
+        encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
+
+
 def test_encode_file_atomic(encoder, tmp_path):
     img = _img(120, 160, 3, 8, seed=6)
     src = tmp_path / "in.tif"
