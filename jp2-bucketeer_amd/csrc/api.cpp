@@ -47,28 +47,33 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// ---- baseline TIFF header parsing (tags 256-339, classic TIFF only) ----
+// ---- baseline TIFF header parsing (tags 256-339; classic TIFF and BigTIFF) ----
 struct TiffReader {
     const uint8_t *b;
     size_t n;
     bool le;
-    uint32_t u16(size_t o) const {
-        if (o + 2 > n) return 0;
-        return le ? (uint32_t)(b[o] | (b[o + 1] << 8)) : (uint32_t)((b[o] << 8) | b[o + 1]);
+    bool big = false;  // BigTIFF: 8-byte offsets, 20-byte IFD entries
+    uint64_t un(size_t o, int k) const {
+        if (o + (size_t)k > n || o + (size_t)k < o) return 0;
+        uint64_t v = 0;
+        for (int i = 0; i < k; i++) v |= (uint64_t)b[o + (le ? i : k - 1 - i)] << (8 * i);
+        return v;
     }
-    uint32_t u32(size_t o) const {
-        if (o + 4 > n) return 0;
-        return le ? ((uint32_t)b[o] | ((uint32_t)b[o + 1] << 8) | ((uint32_t)b[o + 2] << 16) |
-                     ((uint32_t)b[o + 3] << 24))
-                  : (((uint32_t)b[o] << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) |
-                     (uint32_t)b[o + 3]);
-    }
-    uint32_t val(size_t e, uint32_t i) const {
-        uint32_t type = u16(e + 2), cnt = u32(e + 4);
-        uint32_t sz = type == 3 ? 2 : (type == 4 ? 4 : 1);
-        size_t base = (uint64_t)sz * cnt <= 4 ? e + 8 : u32(e + 8);
+    uint32_t u16(size_t o) const { return (uint32_t)un(o, 2); }
+    uint32_t u32(size_t o) const { return (uint32_t)un(o, 4); }
+    uint64_t u64(size_t o) const { return un(o, 8); }
+    size_t entry_size() const { return big ? 20 : 12; }
+    uint64_t count(size_t e) const { return big ? u64(e + 4) : u32(e + 4); }
+    // value i of the entry at e (SHORT, LONG, LONG8 or BYTE)
+    uint64_t val(size_t e, uint64_t i) const {
+        const uint32_t type = u16(e + 2);
+        const uint64_t cnt = count(e);
+        const uint32_t sz = type == 3 ? 2 : (type == 4 ? 4 : (type == 16 ? 8 : 1));
+        const size_t inl = big ? 8 : 4, voff = big ? e + 12 : e + 8;
+        const uint64_t base = (uint64_t)sz * cnt <= inl ? voff : (big ? u64(voff) : u32(voff));
         if (i >= cnt) return 0;
-        return sz == 2 ? u16(base + 2 * i) : (sz == 4 ? u32(base + 4 * i) : (base + i < n ? b[base + i] : 0));
+        const size_t at = (size_t)(base + (uint64_t)sz * i);
+        return sz == 2 ? u16(at) : (sz == 4 ? u32(at) : (sz == 8 ? u64(at) : (at < n ? b[at] : 0)));
     }
 };
 
@@ -78,29 +83,38 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     if (buf[0] == 'I' && buf[1] == 'I') t.le = true;
     else if (buf[0] == 'M' && buf[1] == 'M') t.le = false;
     else return fail("tiff: bad byte-order mark");
-    if (t.u16(2) == 43) return fail("tiff: BigTIFF is not supported yet");
-    if (t.u16(2) != 42) return fail("tiff: not a TIFF file");
-    size_t ifd = t.u32(4);
-    if (ifd + 2 > len) return fail("tiff: IFD offset out of range");
-    uint32_t ne = t.u16(ifd);
+    size_t ifd, ifd_hdr;
+    if (t.u16(2) == 43) {  // BigTIFF: offset size 8, reserved 0, first IFD at 8
+        if (t.u16(4) != 8 || t.u16(6) != 0 || len < 16) return fail("tiff: bad BigTIFF header");
+        t.big = true;
+        ifd = (size_t)t.u64(8);
+        ifd_hdr = 8;
+    } else if (t.u16(2) == 42) {
+        ifd = t.u32(4);
+        ifd_hdr = 2;
+    } else {
+        return fail("tiff: not a TIFF file");
+    }
+    if (ifd + ifd_hdr > len || ifd + ifd_hdr < ifd) return fail("tiff: IFD offset out of range");
+    const uint64_t ne = t.big ? t.u64(ifd) : t.u16(ifd);
     uint32_t w = 0, h = 0, spp = 1, bps = 8, comp = 1, planar = 1, rps = 0xFFFFFFFFu, fmt = 1, pred = 1;
     size_t e_off = 0, e_cnt = 0;
     uint32_t n_off = 0;
-    for (uint32_t i = 0; i < ne; i++) {
-        size_t e = ifd + 2 + 12 * (size_t)i;
-        if (e + 12 > len) return fail("tiff: truncated IFD");
+    if (ne > (len - ifd - ifd_hdr) / t.entry_size()) return fail("tiff: truncated IFD");
+    for (uint64_t i = 0; i < ne; i++) {
+        size_t e = ifd + ifd_hdr + t.entry_size() * (size_t)i;
         switch (t.u16(e)) {
-        case 256: w = t.val(e, 0); break;
-        case 257: h = t.val(e, 0); break;
-        case 258: bps = t.val(e, 0); break;
-        case 259: comp = t.val(e, 0); break;
-        case 273: e_off = e; n_off = t.u32(e + 4); break;
-        case 277: spp = t.val(e, 0); break;
-        case 278: rps = t.val(e, 0); break;
+        case 256: w = (uint32_t)t.val(e, 0); break;
+        case 257: h = (uint32_t)t.val(e, 0); break;
+        case 258: bps = (uint32_t)t.val(e, 0); break;
+        case 259: comp = (uint32_t)t.val(e, 0); break;
+        case 273: e_off = e; n_off = (uint32_t)std::min<uint64_t>(t.count(e), 0xFFFFFFFFu); break;
+        case 277: spp = (uint32_t)t.val(e, 0); break;
+        case 278: rps = (uint32_t)std::min<uint64_t>(t.val(e, 0), 0xFFFFFFFFu); break;
         case 279: e_cnt = e; break;
-        case 284: planar = t.val(e, 0); break;
-        case 317: pred = t.val(e, 0); break;
-        case 339: fmt = t.val(e, 0); break;
+        case 284: planar = (uint32_t)t.val(e, 0); break;
+        case 317: pred = (uint32_t)t.val(e, 0); break;
+        case 339: fmt = (uint32_t)t.val(e, 0); break;
         default: break;
         }
     }

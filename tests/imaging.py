@@ -278,3 +278,39 @@ def tiff_bytes_compressed(img: np.ndarray, compression: str, predictor: bool = F
     b = io.BytesIO()
     Image.fromarray(img).save(b, format="TIFF", compression=compression, strip_size=row * rows_per_strip, **kw)
     return b.getvalue()
+
+
+def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False) -> bytes:
+    """Uncompressed chunky BigTIFF (version 43, LONG8 strip offsets / counts)."""
+    if img.ndim == 2:
+        img = img[..., None]
+    h, w, nc = img.shape
+    bits = img.dtype.itemsize * 8
+    e = ">" if big_endian else "<"
+    rps = min(rows_per_strip, h)
+    nst = (h + rps - 1) // rps
+    strips = [np.ascontiguousarray(img[s * rps:(s + 1) * rps]) for s in range(nst)]
+    strips = [b.astype(b.dtype.newbyteorder(e)).tobytes() for b in strips]
+    ntags = 10
+    ifd_off = 16
+    arr_off = ifd_off + 8 + 20 * ntags + 8
+    so_off, sbc_off = arr_off, arr_off + 8 * nst
+    data = sbc_off + 8 * nst
+    offs = []
+    for s in strips:
+        offs.append(data)
+        data += len(s)
+
+    def ent(t, typ, cnt, vals):
+        fmt = {3: "H", 4: "I", 16: "Q"}[typ]
+        raw = struct.pack(e + fmt * len(vals), *vals)
+        return struct.pack(e + "HHQ", t, typ, cnt) + (raw + b"\0" * 8)[:8]
+
+    tags = [ent(256, 4, 1, [w]), ent(257, 4, 1, [h]), ent(258, 3, nc, [bits] * nc), ent(259, 3, 1, [1]),
+            ent(262, 3, 1, [2 if nc >= 3 else 1]),
+            ent(273, 16, nst, [offs[0]] if nst == 1 else [so_off]), ent(277, 3, 1, [nc]), ent(278, 4, 1, [rps]),
+            ent(279, 16, nst, [len(strips[0])] if nst == 1 else [sbc_off]), ent(284, 3, 1, [1])]
+    hdr = (b"MM" if big_endian else b"II") + struct.pack(e + "HHHQ", 43, 8, 0, ifd_off)
+    ifd = struct.pack(e + "Q", ntags) + b"".join(tags) + struct.pack(e + "Q", 0)
+    arrays = struct.pack(e + "Q" * nst, *offs) + struct.pack(e + "Q" * nst, *[len(s) for s in strips])
+    return hdr + ifd + arrays + b"".join(strips)

@@ -120,6 +120,24 @@ def test_tiff_layout_compressed_strips(comp, code, pred):
     assert [lay.strip_bytes[i] for i in range(5)] == list(tags[279])
 
 
+@pytest.mark.parametrize("big_endian", [False, True])
+def test_tiff_layout_bigtiff(big_endian):
+    """BigTIFF (version 43, LONG8 offsets) parses to the same layout as the
+    classic file of the same pixels, offsets aside."""
+    img = im.synth_rgb8(100, 70, seed=4)
+    lay, keep = jp2hip.tiff_layout(im.bigtiff_bytes(img, rows_per_strip=16, big_endian=big_endian))
+    ref, _ = jp2hip.tiff_layout(im.tiff_bytes(img, rows_per_strip=16, big_endian=big_endian))
+    for f in ("width", "height", "components", "bits", "planar", "big_endian", "rows_per_strip", "nstrips"):
+        assert getattr(lay, f) == getattr(ref, f), f
+    data = im.bigtiff_bytes(img, rows_per_strip=16, big_endian=big_endian)
+    row = 70 * 3
+    for s in range(lay.nstrips):
+        o = lay.strip_offsets[s]
+        rows = min(16, 100 - 16 * s)
+        got = np.frombuffer(data[o:o + row * rows], np.uint8).reshape(rows, 70, 3)
+        assert np.array_equal(got, img[16 * s:16 * s + rows])
+
+
 def test_conversion_ordinals_match_reference():
     assert int(Conversion.LOSSY) == 0 and int(Conversion.LOSSLESS) == 1
 

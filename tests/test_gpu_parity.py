@@ -169,6 +169,14 @@ def test_compressed_strips_same_output(encoder, comp, pred, kind):
     assert plain == ol.encode(img, ol.copy_recipe(rc))
 
 
+def test_bigtiff_same_output(encoder):
+    img = im.synth_u16(230, 410, comps=3, seed=6)
+    for conv in (jp2hip.LOSSLESS, jp2hip.LOSSY):
+        a, _ = encoder.encode_tiff(im.tiff_bytes(img, rows_per_strip=32), conv)
+        b, _ = encoder.encode_tiff(im.bigtiff_bytes(img, rows_per_strip=32, big_endian=True), conv)
+        assert a == b
+
+
 def test_corrupt_compressed_strip_fails_loudly(encoder):
     img = im.synth_rgb8(64, 64, seed=1)
     data = bytearray(im.tiff_bytes_compressed(img, "packbits", rows_per_strip=64))
