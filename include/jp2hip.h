@@ -92,6 +92,9 @@ typedef struct jp2hip_layout {
                                              /* 2 horizontal differencing   */
     const uint64_t *strip_bytes;             /* compressed size per strip   */
                                              /* (compression 5 / 32773)     */
+    int32_t tile_width, tile_height;         /* tiled TIFF (0: strips): the */
+                                             /* "strips" above are then the */
+                                             /* tiles, row-major per plane  */
 } jp2hip_layout;
 
 typedef struct jp2hip_stats {
@@ -144,7 +147,9 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
  * horizontal differencing (Predictor 2); compressed strips are decoded on
  * the GPU (one lane per strip) before ingest.  For a compressed file
  * `offsets` receives 2 * nstrips entries: the strip offsets, then their byte
- * counts (layout->strip_bytes points at the second half). */
+ * counts (layout->strip_bytes points at the second half).  Tiled TIFFs
+ * (TileWidth/TileLength) are described the same way, one entry per tile,
+ * and always carry the byte counts; they are untiled in HBM before ingest. */
 int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout,
                        uint64_t *offsets, int32_t max_offsets);
 

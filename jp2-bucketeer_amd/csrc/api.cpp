@@ -99,7 +99,7 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     const uint64_t ne = t.big ? t.u64(ifd) : t.u16(ifd);
     uint32_t w = 0, h = 0, spp = 1, bps = 8, comp = 1, planar = 1, rps = 0xFFFFFFFFu, fmt = 1, pred = 1;
     size_t e_off = 0, e_cnt = 0;
-    uint32_t n_off = 0;
+    uint32_t n_off = 0, tw = 0, th = 0;
     if (ne > (len - ifd - ifd_hdr) / t.entry_size()) return fail("tiff: truncated IFD");
     for (uint64_t i = 0; i < ne; i++) {
         size_t e = ifd + ifd_hdr + t.entry_size() * (size_t)i;
@@ -114,27 +114,38 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
         case 279: e_cnt = e; break;
         case 284: planar = (uint32_t)t.val(e, 0); break;
         case 317: pred = (uint32_t)t.val(e, 0); break;
+        case 322: tw = (uint32_t)t.val(e, 0); break;
+        case 323: th = (uint32_t)t.val(e, 0); break;
+        case 324: e_off = e; n_off = (uint32_t)std::min<uint64_t>(t.count(e), 0xFFFFFFFFu); break;  // TileOffsets
+        case 325: e_cnt = e; break;                                                                  // TileByteCounts
         case 339: fmt = (uint32_t)t.val(e, 0); break;
         default: break;
         }
     }
     if (!w || !h || !e_off) return fail("tiff: missing ImageWidth/ImageLength/StripOffsets");
+    const bool tiled = tw || th;
+    if (tiled && (!tw || !th || (tw % 16) || (th % 16) || tw > 65536 || th > 65536))
+        return fail("tiff: bad TileWidth/TileLength");
+    if (tiled && !e_cnt) return fail("tiff: tiles need TileByteCounts");
     // strips: uncompressed, LZW or PackBits (decoded on the GPU, kernels.hip
     // k_unlzw / k_unpackbits); Deflate / JPEG / CCITT are not supported
     if (comp != 1 && comp != 5 && comp != 32773)
         return fail("tiff: compression " + std::to_string(comp) +
                     " is not supported (uncompressed, LZW and PackBits only)");
     if (pred != 1 && pred != 2) return fail("tiff: predictor " + std::to_string(pred) + " is not supported");
+    if (pred == 2 && comp == 1) return fail("tiff: predictor 2 without compression is not supported");
     if (comp != 1 && !e_cnt) return fail("tiff: compressed strips need StripByteCounts");
     if (bps != 8 && bps != 16) return fail("tiff: " + std::to_string(bps) + " bits/sample is not supported");
     if (fmt != 1) return fail("tiff: only unsigned integer samples are supported");
     if (spp < 1 || spp > 4) return fail("tiff: " + std::to_string(spp) + " samples/pixel is not supported");
     if (planar != 1 && planar != 2) return fail("tiff: bad PlanarConfiguration");
     if (rps > h) rps = h;
-    uint32_t per_plane = (h + rps - 1) / rps;
+    if (tiled) rps = th;  // per-unit rows (tiles are never clipped)
+    const uint32_t across = tiled ? (w + tw - 1) / tw : 1;
+    uint32_t per_plane = tiled ? across * ((h + th - 1) / th) : (h + rps - 1) / rps;
     uint32_t need = per_plane * (planar == 2 ? spp : 1);
-    if (n_off < need) return fail("tiff: too few strips");
-    const bool packed = comp != 1;
+    if (n_off < need) return fail(tiled ? "tiff: too few tiles" : "tiff: too few strips");
+    const bool packed = comp != 1 || tiled;
     offs.resize(packed ? 2 * (size_t)need : need);
     size_t row = (size_t)w * (planar == 2 ? 1 : spp) * (bps / 8);
     for (uint32_t s = 0; s < need; s++) {
@@ -144,6 +155,8 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
         if (packed) {
             const uint64_t nb = t.val(e_cnt, s);
             if (offs[s] + nb > len) return fail("tiff: strip " + std::to_string(s) + " out of range");
+            const uint64_t unit = (uint64_t)tw * (planar == 2 ? 1 : spp) * (bps / 8) * th;
+            if (tiled && comp == 1 && nb < unit) return fail("tiff: tile byte count too small");
             offs[need + s] = nb;
             continue;
         }
@@ -162,6 +175,8 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     lay->compression = (int32_t)comp;
     lay->predictor = (int32_t)pred;
     lay->strip_bytes = packed ? offs.data() + need : nullptr;
+    lay->tile_width = (int32_t)tw;
+    lay->tile_height = (int32_t)th;
     return 0;
 }
 
@@ -210,13 +225,14 @@ void undershoot_terms(const jp2hip::GpuEncoder &g, int64_t &coded, int64_t &skip
 // buffer first; afterwards (d_src, lay) describe uncompressed strips.
 bool unpack_if_compressed(jp2hip_ctx *ctx, const void *&d_src, size_t src_len, const jp2hip_layout *&lay,
                           jp2hip_layout &ulay, std::vector<uint64_t> &uoffs, std::string &err) {
-    if (lay->compression <= 1) return true;
-    if (lay->compression != 5 && lay->compression != 32773) {
+    if (lay->compression <= 1 && lay->tile_width <= 0) return true;
+    if (lay->compression > 1 && lay->compression != 5 && lay->compression != 32773) {
         err = "layout: compression " + std::to_string(lay->compression) + " is not supported";
         return false;
     }
-    if (!lay->strip_bytes || !lay->strip_offsets || lay->nstrips <= 0 || lay->rows_per_strip <= 0) {
-        err = "layout: compressed strips need strip_offsets and strip_bytes";
+    if (!lay->strip_bytes || !lay->strip_offsets || lay->nstrips <= 0 || lay->rows_per_strip <= 0 ||
+        (lay->tile_width > 0) != (lay->tile_height > 0)) {
+        err = "layout: compressed strips / tiles need strip_offsets and strip_bytes";
         return false;
     }
     for (int i = 0; i < lay->nstrips; i++)  // the decoders trust these bounds
@@ -377,7 +393,8 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
     Plan full;
     std::string err;
     // every rank sees the same layout, so all of them stop here together
-    if (lay->compression > 1) return fail("split: compressed strips are not supported; decode the TIFF first");
+    if (lay->compression > 1 || lay->tile_width > 0)
+        return fail("split: compressed or tiled TIFFs are not supported; rewrite as uncompressed strips first");
     if (!build_plan(full, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     int tr0, tr1;
     split_tile_rows(full.nty, rank, world, tr0, tr1);
@@ -615,7 +632,7 @@ int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout, u
     }
     std::memcpy(offsets, offs.data(), offs.size() * sizeof(uint64_t));
     layout->strip_offsets = offsets;
-    layout->strip_bytes = layout->compression > 1 ? offsets + layout->nstrips : nullptr;
+    layout->strip_bytes = (layout->compression > 1 || layout->tile_width > 0) ? offsets + layout->nstrips : nullptr;
     return 0;
 }
 

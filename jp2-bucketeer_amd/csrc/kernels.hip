@@ -113,15 +113,17 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
 // --------------------------------------------------------------------------
 struct UnpackArgs {
     const uint8_t *src;
-    const uint64_t *off, *cnt;  // per strip: byte offset and compressed size
+    const uint64_t *off, *cnt;  // per strip (tile): byte offset and compressed size
     int nstrips, per_plane, rps, h;
     uint64_t row_bytes, stride;  // decoded row and strip stride (bytes)
+    uint64_t unit_bytes;         // tiles: every unit decodes to this many bytes
     uint8_t *dst;
     uint32_t *tab;  // LZW: 4096 entries (start, length) per strip
     int *err;
 };
 
 __device__ __forceinline__ uint64_t strip_out_bytes(const UnpackArgs &a, int s) {
+    if (a.unit_bytes) return a.unit_bytes;
     const int y0 = (s % a.per_plane) * a.rps;
     return (uint64_t)min(a.rps, a.h - y0) * a.row_bytes;
 }
@@ -221,6 +223,20 @@ __global__ void __launch_bounds__(256) k_unpredict(uint8_t *dst, int nrows, int 
             else { row[2 * i] = (uint8_t)v; row[2 * i + 1] = (uint8_t)(v >> 8); }
         }
     }
+}
+
+// Tiled TIFF -> one row-major strip per plane: thread per pixel of a row.
+// Tile t of plane p starts at base + (toff ? toff[t] : t * tstride).
+__global__ void __launch_bounds__(256) k_untile(const uint8_t *base, const uint64_t *toff, uint64_t tstride, int w,
+                                                 int h, int tw, int th, int across, int per_plane, int px_bytes,
+                                                 uint8_t *out) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, p = blockIdx.z;
+    if (x >= w) return;
+    const int t = p * per_plane + (y / th) * across + x / tw;
+    const uint8_t *src = base + (toff ? toff[t] : (uint64_t)t * tstride) +
+                         ((uint64_t)(y % th) * tw + (x % tw)) * px_bytes;
+    uint8_t *dst = out + (uint64_t)p * w * h * px_bytes + ((uint64_t)y * w + x) * px_bytes;
+    for (int i = 0; i < px_bytes; i++) dst[i] = src[i];
 }
 
 // --------------------------------------------------------------------------
@@ -598,7 +614,7 @@ GpuEncoder::~GpuEncoder() {
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
                      &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
-                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &stage, &soff, &lzwtab};
+                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &stage, &soff, &lzwtab, &untiled};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -650,40 +666,72 @@ bool GpuEncoder::dump(const char *dir, const char *name, const DevBuf &b, size_t
 bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2hip_layout &out,
                                std::vector<uint64_t> &out_offs, const void **d_out, std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    const int ns = lay.nstrips;
-    const int per_plane = (lay.height + lay.rows_per_strip - 1) / lay.rows_per_strip;
-    const uint64_t row_bytes = (uint64_t)lay.width * (lay.planar == 2 ? 1 : lay.components) * (lay.bits / 8);
-    const uint64_t stride = ((uint64_t)lay.rows_per_strip * row_bytes + 255) & ~255ull;
-    if (!ensure<uint8_t>(stage, stride * ns, err) || !ensure<uint64_t>(soff, (size_t)ns * 2, err) ||
-        !ensure<int>(this->err, 4, err))
-        return false;
+    const int ns = lay.nstrips;  // strips, or tiles
+    const bool tiled = lay.tile_width > 0;
+    const int spp_row = lay.planar == 2 ? 1 : lay.components;
+    const int px_bytes = spp_row * (lay.bits / 8);
+    const int unit_w = tiled ? lay.tile_width : lay.width, unit_h = tiled ? lay.tile_height : lay.rows_per_strip;
+    const int planes = lay.planar == 2 ? lay.components : 1;
+    const int across = tiled ? (lay.width + lay.tile_width - 1) / lay.tile_width : 1;
+    const int per_plane = tiled ? across * ((lay.height + lay.tile_height - 1) / lay.tile_height)
+                                : (lay.height + lay.rows_per_strip - 1) / lay.rows_per_strip;
+    const uint64_t row_bytes = (uint64_t)unit_w * px_bytes;
+    const uint64_t stride = ((uint64_t)unit_h * row_bytes + 255) & ~255ull;
+    const bool decode = lay.compression > 1;
+    if (!ensure<uint64_t>(soff, (size_t)ns * 2, err) || !ensure<int>(this->err, 4, err)) return false;
+    if (decode && !ensure<uint8_t>(stage, stride * ns, err)) return false;
     if (lay.compression == 5 && !ensure<uint32_t>(lzwtab, (size_t)ns * 8192, err)) return false;
     HIPCHECK(hipMemcpyAsync(soff.ptr, lay.strip_offsets, sizeof(uint64_t) * ns, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync((uint64_t *)soff.ptr + ns, lay.strip_bytes, sizeof(uint64_t) * ns, hipMemcpyHostToDevice,
                             stream));
     HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
-    UnpackArgs ua;
-    ua.src = (const uint8_t *)d_src;
-    ua.off = (const uint64_t *)soff.ptr;
-    ua.cnt = (const uint64_t *)soff.ptr + ns;
-    ua.nstrips = ns;
-    ua.per_plane = per_plane;
-    ua.rps = lay.rows_per_strip;
-    ua.h = lay.height;
-    ua.row_bytes = row_bytes;
-    ua.stride = stride;
-    ua.dst = (uint8_t *)stage.ptr;
-    ua.tab = (uint32_t *)lzwtab.ptr;
-    ua.err = (int *)this->err.ptr;
-    if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
-    else hipLaunchKernelGGL(k_unpackbits, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
-    HIPCHECK(hipGetLastError());
-    if (lay.predictor == 2) {
-        const int nrows = ns * lay.rows_per_strip;
-        hipLaunchKernelGGL(k_unpredict, dim3((nrows + 255) / 256), dim3(256), 0, stream, (uint8_t *)stage.ptr, nrows,
-                           lay.rows_per_strip, lay.rows_per_strip, lay.height, per_plane, stride, lay.width,
-                           lay.planar == 2 ? 1 : lay.components, lay.bits, lay.big_endian);
+    if (decode) {
+        UnpackArgs ua;
+        ua.src = (const uint8_t *)d_src;
+        ua.off = (const uint64_t *)soff.ptr;
+        ua.cnt = (const uint64_t *)soff.ptr + ns;
+        ua.nstrips = ns;
+        ua.per_plane = per_plane;
+        ua.rps = lay.rows_per_strip;
+        ua.h = lay.height;
+        ua.row_bytes = row_bytes;
+        ua.stride = stride;
+        ua.unit_bytes = tiled ? (uint64_t)unit_h * row_bytes : 0;
+        ua.dst = (uint8_t *)stage.ptr;
+        ua.tab = (uint32_t *)lzwtab.ptr;
+        ua.err = (int *)this->err.ptr;
+        if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
+        else hipLaunchKernelGGL(k_unpackbits, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
         HIPCHECK(hipGetLastError());
+        if (lay.predictor == 2) {  // per decoded row of a strip / of a tile
+            const int nrows = ns * unit_h;
+            hipLaunchKernelGGL(k_unpredict, dim3((nrows + 255) / 256), dim3(256), 0, stream, (uint8_t *)stage.ptr,
+                               nrows, unit_h, unit_h, tiled ? unit_h : lay.height, tiled ? 1 : per_plane, stride,
+                               unit_w, spp_row, lay.bits, lay.big_endian);
+            HIPCHECK(hipGetLastError());
+        }
+    } else if (lay.predictor == 2) {
+        err = "tiff: Predictor 2 on uncompressed data is not supported";
+        return false;
+    }
+    const void *res = decode ? stage.ptr : d_src;
+    out = lay;
+    out_offs.resize(tiled ? planes : ns);
+    if (tiled) {  // tiles -> one row-major strip per plane
+        const uint64_t plane_bytes = (uint64_t)lay.width * lay.height * px_bytes;
+        if (!ensure<uint8_t>(untiled, plane_bytes * planes, err)) return false;
+        hipLaunchKernelGGL(k_untile, dim3((lay.width + 255) / 256, lay.height, planes), dim3(256), 0, stream,
+                           (const uint8_t *)res, decode ? nullptr : (const uint64_t *)soff.ptr, stride, lay.width,
+                           lay.height, lay.tile_width, lay.tile_height, across, per_plane, px_bytes,
+                           (uint8_t *)untiled.ptr);
+        HIPCHECK(hipGetLastError());
+        for (int p = 0; p < planes; p++) out_offs[p] = (uint64_t)p * plane_bytes;
+        out.rows_per_strip = lay.height;
+        out.nstrips = planes;
+        out.tile_width = out.tile_height = 0;
+        res = untiled.ptr;
+    } else {
+        for (int i = 0; i < ns; i++) out_offs[i] = (uint64_t)i * stride;
     }
     int herr = 0;
     HIPCHECK(hipMemcpyAsync(&herr, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -692,14 +740,11 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
         err = "tiff: corrupt compressed strip";
         return false;
     }
-    out = lay;
-    out_offs.resize(ns);
-    for (int i = 0; i < ns; i++) out_offs[i] = (uint64_t)i * stride;
     out.strip_offsets = out_offs.data();
     out.compression = 1;
     out.predictor = 1;
     out.strip_bytes = nullptr;
-    *d_out = stage.ptr;
+    *d_out = res;
     return true;
 }
 

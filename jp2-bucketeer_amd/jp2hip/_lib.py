@@ -44,7 +44,8 @@ class Layout(Structure):
                 ("rows_per_strip", c_int32), ("nstrips", c_int32),
                 ("strip_offsets", POINTER(c_uint64)),
                 ("compression", c_int32), ("predictor", c_int32),
-                ("strip_bytes", POINTER(c_uint64))]
+                ("strip_bytes", POINTER(c_uint64)),
+                ("tile_width", c_int32), ("tile_height", c_int32)]
 
 
 class Stats(Structure):
@@ -153,10 +154,11 @@ def tiff_layout(data: bytes):
     if lib().jp2hip_tiff_layout(buf, len(data), byref(lay), offs, cap) != 0:
         raise Jp2hipError(last_error())
     n = lay.nstrips
-    m = 2 * n if lay.compression > 1 else n  # compressed: offsets, then byte counts
+    packed = lay.compression > 1 or lay.tile_width > 0
+    m = 2 * n if packed else n  # compressed / tiled: offsets, then byte counts
     keep = (c_uint64 * m)(*offs[:m])
     lay.strip_offsets = ctypes.cast(keep, POINTER(c_uint64))
-    if lay.compression > 1:
+    if packed:
         lay.strip_bytes = ctypes.cast(ctypes.byref(keep, 8 * n), POINTER(c_uint64))
     return lay, keep
 

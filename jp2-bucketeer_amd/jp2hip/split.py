@@ -150,7 +150,7 @@ def band_strips(tif: bytes, layout: Layout, offsets, row0: int, row1: int):
     rank uploads only its band of a multi-GB TIFF.  Offsets of strips outside
     the band are 0 and never read (kernels.hip k_ingest / dwt.hip band_load
     touch only the rows of their band)."""
-    if layout.compression > 1:
+    if layout.compression > 1 or layout.tile_width > 0:
         raise Jp2hipError("band-only upload needs uncompressed strips; upload the whole file")
     rps, h, w = layout.rows_per_strip, layout.height, layout.width
     per_plane = (h + rps - 1) // rps

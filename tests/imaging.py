@@ -314,3 +314,63 @@ def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False) -> bytes
     ifd = struct.pack(e + "Q", ntags) + b"".join(tags) + struct.pack(e + "Q", 0)
     arrays = struct.pack(e + "Q" * nst, *offs) + struct.pack(e + "Q" * nst, *[len(s) for s in strips])
     return hdr + ifd + arrays + b"".join(strips)
+
+
+def packbits_encode(raw: bytes) -> bytes:
+    """PackBits with literal runs only (valid, if not small)."""
+    out = bytearray()
+    for i in range(0, len(raw), 128):
+        chunk = raw[i:i + 128]
+        out.append(len(chunk) - 1)
+        out += chunk
+    return bytes(out)
+
+
+def tiled_tiff_bytes(img: np.ndarray, tile=(32, 48), planar=False, big_endian=False, packbits=False) -> bytes:
+    """Classic tiled TIFF (TileWidth/TileLength/TileOffsets/TileByteCounts),
+    uncompressed or PackBits; edge tiles padded with zeros as TIFF requires."""
+    if img.ndim == 2:
+        img = img[..., None]
+    h, w, nc = img.shape
+    tw, th = tile
+    bits = img.dtype.itemsize * 8
+    e = ">" if big_endian else "<"
+    across, down = (w + tw - 1) // tw, (h + th - 1) // th
+    planes = [img[..., c:c + 1] for c in range(nc)] if planar else [img]
+    tiles = []
+    for pl in planes:
+        for ty in range(down):
+            for tx in range(across):
+                t = np.zeros((th, tw, pl.shape[2]), img.dtype)
+                part = pl[ty * th:(ty + 1) * th, tx * tw:(tx + 1) * tw]
+                t[:part.shape[0], :part.shape[1]] = part
+                raw = t.astype(t.dtype.newbyteorder(e)).tobytes()
+                tiles.append(packbits_encode(raw) if packbits else raw)
+    nt = len(tiles)
+    ntags = 13
+    ifd_off = 8
+    extra_base = ifd_off + 2 + 12 * ntags + 4
+    bps_off = extra_base
+    to_off = bps_off + 2 * max(nc, 2)
+    tbc_off = to_off + 4 * nt
+    data = tbc_off + 4 * nt
+    offs = []
+    for t in tiles:
+        offs.append(data)
+        data += len(t)
+
+    def ent(tag, typ, cnt, val):
+        v = struct.pack(e + "HH", val, 0) if (typ == 3 and cnt == 1) else struct.pack(e + "I", val)
+        return struct.pack(e + "HHI", tag, typ, cnt) + v
+
+    tags = [ent(256, 4, 1, w), ent(257, 4, 1, h), ent(258, 3, nc, bps_off) if nc > 1 else ent(258, 3, 1, bits),
+            ent(259, 3, 1, 32773 if packbits else 1), ent(262, 3, 1, 2 if nc >= 3 else 1), ent(277, 3, 1, nc),
+            ent(284, 3, 1, 2 if planar else 1), ent(322, 4, 1, tw), ent(323, 4, 1, th),
+            ent(324, 4, nt, to_off if nt > 1 else offs[0]), ent(325, 4, nt, tbc_off if nt > 1 else len(tiles[0])),
+            ent(339, 3, 1, 1), ent(338, 3, 1, 2) if nc in (2, 4) else ent(305, 2, 1, 0)]
+    tags.sort(key=lambda t: struct.unpack(e + "H", t[:2])[0])
+    hdr = (b"MM\0*" if big_endian else b"II*\0") + struct.pack(e + "I", ifd_off)
+    ifd = struct.pack(e + "H", ntags) + b"".join(tags) + struct.pack(e + "I", 0)
+    extra = struct.pack(e + "H" * max(nc, 2), *([bits] * max(nc, 2)))
+    extra += struct.pack(e + "I" * nt, *offs) + struct.pack(e + "I" * nt, *[len(t) for t in tiles])
+    return hdr + ifd + extra + b"".join(tiles)

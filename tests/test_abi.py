@@ -138,6 +138,18 @@ def test_tiff_layout_bigtiff(big_endian):
         assert np.array_equal(got, img[16 * s:16 * s + rows])
 
 
+@pytest.mark.parametrize("kw", [{}, {"packbits": True}, {"planar": True, "big_endian": True}])
+def test_tiff_layout_tiled(kw):
+    img = im.synth_rgb8(70, 90, seed=3)
+    lay, keep = jp2hip.tiff_layout(im.tiled_tiff_bytes(img, tile=(32, 48), **kw))
+    assert (lay.tile_width, lay.tile_height) == (32, 48)
+    assert lay.nstrips == 3 * 2 * (3 if kw.get("planar") else 1)
+    assert lay.compression == (32773 if kw.get("packbits") else 1)
+    unit = 32 * 48 * (1 if kw.get("planar") else 3)
+    sizes = [lay.strip_bytes[i] for i in range(lay.nstrips)]
+    assert all(n == unit for n in sizes) if not kw.get("packbits") else all(n > unit for n in sizes)
+
+
 def test_conversion_ordinals_match_reference():
     assert int(Conversion.LOSSY) == 0 and int(Conversion.LOSSLESS) == 1
 

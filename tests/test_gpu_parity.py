@@ -177,6 +177,22 @@ def test_bigtiff_same_output(encoder):
         assert a == b
 
 
+@pytest.mark.parametrize("kw,kind", [({}, "rgb8"), ({"packbits": True}, "rgb8"),
+                                     ({"planar": True, "big_endian": True}, "rgb16"),
+                                     ({"packbits": True, "big_endian": True}, "gray16")])
+def test_tiled_tiff_same_output(encoder, kw, kind):
+    """Tiled TIFFs (edge tiles padded) are untiled in HBM: same file as the
+    strip TIFF of the same pixels."""
+    if kind == "rgb8":
+        img = im.synth_rgb8(301, 517, seed=5)
+    else:
+        img = im.synth_u16(301, 517, comps=3 if kind == "rgb16" else 1, seed=5)
+    for conv in (jp2hip.LOSSLESS, jp2hip.LOSSY):
+        a, _ = encoder.encode_tiff(im.tiff_bytes(img), conv)
+        b, _ = encoder.encode_tiff(im.tiled_tiff_bytes(img, tile=(64, 48), **kw), conv)
+        assert a == b
+
+
 def test_corrupt_compressed_strip_fails_loudly(encoder):
     img = im.synth_rgb8(64, 64, seed=1)
     data = bytearray(im.tiff_bytes_compressed(img, "packbits", rows_per_strip=64))
