@@ -436,7 +436,7 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
         B++;
         m.C &= 0x7FFFFFFu;
     }
-    ring[m.bp >= 0 ? (m.bp & 63) : 64] = (uint8_t)B;
+    ring[m.bp & 63] = (uint8_t)B;  // bp = -1 -> slot 63, see mq_step
     m.bp++;
     const bool ff = B == 0xFF;
     m.B = ff ? (m.C >> 20) : (m.C >> 19);
@@ -466,7 +466,9 @@ __device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint3
     const uint32_t C2 = carry ? (C1 & 0x7FFFFFFu) : C1;
     const bool ff = Bc == 0xFFu;
     const bool emit = valid && bo;
-    ring[(emit && m.bp >= 0) ? (m.bp & 63) : 64] = (uint8_t)Bc;
+    // byte -1 (the MQ coder's initial pending byte, never output) lands in
+    // slot 63, which byte 63 overwrites before that group is flushed
+    ring[emit ? (m.bp & 63) : 64] = (uint8_t)Bc;
     uint32_t Cx = bo ? (C2 & (ff ? 0xFFFFFu : 0x7FFFFu)) : C1;
     int CTx = bo ? (ff ? 7 : 8) : m.CT - n;
     int rem = n - s1;
@@ -525,7 +527,7 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 // pass; s >= 1 is pass (s+2)%3 (0 SPP, 1 MRP, 2 CUP) of plane k = (s+2)/3,
 // planes counted from the top.
 __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
-    __shared__ uint32_t cxs[19 * 64];
+    __shared__ uint32_t cxs[32 * 64];  // 19 contexts; indices 19..31 absorb bytes read past a pass end
     __shared__ uint32_t mqt[48];
     __shared__ uint32_t rings[64 * 17];  // 68 bytes per lane: 64-byte ring + dummy slot
     const int lane = threadIdx.x;
@@ -599,18 +601,20 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
         const uint4 nxt = ptr[1];
         const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
         const int n = min(16, left);
-        uint32_t t = cx[min((w[0] & 0xFFu) >> 1, 18u) * 64];
+        uint32_t t = cx[__builtin_amdgcn_ubfe(w[0], 1, 5) * 64];
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            const uint32_t byte = (w[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
-            uint32_t nbyte = 0, nt = 0;
+            // decision byte = (context << 1) | d; context in bits 1..5
+            const uint32_t cur_cx = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8 + 1, 5);
+            const uint32_t d = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 1);
+            uint32_t nxt_cx = 0, nt = 0;
             if (j < 15) {
-                nbyte = (w[(j + 1) >> 2] >> (((j + 1) & 3) * 8)) & 0xFFu;
-                nt = cx[min(nbyte >> 1, 18u) * 64];  // may be past the pass end
+                nxt_cx = __builtin_amdgcn_ubfe(w[(j + 1) >> 2], ((j + 1) & 3) * 8 + 1, 5);
+                nt = cx[nxt_cx * 64];  // may be past the pass end (then unused)
             }
-            const uint32_t tn = mq_step(m, t, mqt, byte & 1u, j < n, ring);
-            cx[min(byte >> 1, 18u) * 64] = tn;
-            t = ((nbyte >> 1) == (byte >> 1)) ? tn : nt;
+            const uint32_t tn = mq_step(m, t, mqt, d, j < n, ring);
+            cx[cur_cx * 64] = tn;
+            t = (nxt_cx == cur_cx) ? tn : nt;
         }
         ring_flush(m, ring, fl);
         left -= n;
