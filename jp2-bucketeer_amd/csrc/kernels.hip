@@ -265,8 +265,14 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     int32_t *sm = a.sm + d.sm_off;
     uint32_t vmax = 0;
     uint32_t lim = (1u << d.Mb) - 1u;
-    for (int y = 0; y < d.h; y++) {
-        if (!act) continue;
+    // the lane's column stays in registers (sign | magnitude; 0 outside the
+    // block) for the bit-plane and distortion passes: the coefficients are
+    // read from HBM once
+    uint32_t col[64];
+#pragma unroll
+    for (int y = 0; y < 64; y++) {
+        col[y] = 0;
+        if (!act || y >= d.h) continue;
         int32_t raw = src[(size_t)y * a.plane_w + lane];
         uint32_t v, s;
         if (a.reversible) {
@@ -279,14 +285,14 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             v = (uint32_t)floorf(t);
         }
         if (v > lim) v = lim;
-        sm[y * 64 + lane] = (int32_t)((s << 31) | v);
+        col[y] = (s << 31) | v;
+        sm[y * 64 + lane] = (int32_t)col[y];
         vmax = max(vmax, v);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
     int P = vmax ? 32 - __clz(vmax) : 0;
     if (lane == 0) a.P[b] = (uint8_t)P;
-    __syncthreads();  // sm visible to the wave (same lanes re-read their own column anyway)
     uint64_t *B = a.bp + d.bp_off;
     uint64_t *S = B + (size_t)d.Mb * 64;
     uint64_t *SG = B + (size_t)2 * d.Mb * 64;
@@ -297,9 +303,11 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     auto dil = [](uint64_t m) { return m | (m << 1) | (m >> 1); };
     uint64_t up = 0, mid = 0;
     uint32_t cntS = 0, nnb = 0;
-    for (int y = 0; y < d.h; y++) {
-        uint32_t word = act ? (uint32_t)sm[y * 64 + lane] : 0u;
-        uint32_t v = word & 0x7FFFFFFFu;
+#pragma unroll
+    for (int y = 0; y < 64; y++) {
+        if (y >= d.h) continue;  // (continue, not break: the loop must unroll)
+        const uint32_t word = col[y];
+        const uint32_t v = word & 0x7FFFFFFFu;
         uint64_t myB = 0, myS = 0;
         for (int p = 0; p < P; p++) {
             uint64_t bm = __ballot((v >> p) & 1u);
@@ -326,15 +334,14 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     bool lossless = a.reversible != 0;
     for (int p = 0; p < P; p++) {
         int64_t ref = 0, sig = 0;
-        if (act) {
-            for (int y = 0; y < d.h; y++) {
-                uint32_t v = (uint32_t)sm[y * 64 + lane] & 0x7FFFFFFFu;
-                uint32_t hi = v >> p;
-                if (hi == 0) continue;
-                int64_t g = dist_gain(v, p, lossless);
-                if (hi == 1) sig += g;
-                else ref += g;
-            }
+#pragma unroll
+        for (int y = 0; y < 64; y++) {
+            const uint32_t v = col[y] & 0x7FFFFFFFu;  // 0 outside the block
+            const uint32_t hi = v >> p;
+            if (hi == 0) continue;
+            const int64_t g = dist_gain(v, p, lossless);
+            if (hi == 1) sig += g;
+            else ref += g;
         }
         ref = wave_sum64(ref);
         sig = wave_sum64(sig);
