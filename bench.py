@@ -111,6 +111,25 @@ def pmc_traffic(kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def sq_counters(kernel):
+    """Occupancy / VALU figures of `kernel` from the newest committed SQ PMC
+    summary (profiles/rNN/t1_sq_counters.json, tests/tools/sq_summary.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "t1_sq_counters.json")))
+    if not files:
+        return None
+    try:
+        k = json.load(open(files[-1]))["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not k:
+        return None
+    keep = {x: k[x] for x in ("valu_busy", "wait_share", "waves_resident", "SQ_WAVES", "SQ_INSTS_VALU",
+                              "SQ_INSTS_SALU", "SQ_INSTS_LDS") if x in k}
+    keep["source"] = os.path.relpath(files[-1], ROOT)
+    return keep
+
+
 def cpu_converter_opj(img, nproc):
     """north_star's CPU reference converter: opj_compress (Kakadu is absent),
     `nproc` concurrent single-image processes with the Appendix A recipe."""
@@ -168,12 +187,13 @@ def run(args):
             _, st = e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
             all_stats.append(st.as_dict())
     # single-image latency (one context, nothing else in flight)
-    lat = []
+    lat, alone = [], []
     for _ in range(2):
         t = time.perf_counter()
         _, st = encs[0].encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
         lat.append(time.perf_counter() - t)
         all_stats.append(st.as_dict())
+        alone.append(st.as_dict())
     barrier(world)
     torch.cuda.synchronize()
     stages = [[] for _ in range(nf)]
@@ -222,6 +242,7 @@ def run(args):
         alg = {"k_t1_mq": t1_alg, "k_t1_cm": t1_alg, "k_dwt": dwt_alg, "k_quant": 4 * C * npx * 2,
                "k_ingest": (C + 4 * C) * npx, "k_pcrd": 0}
         ach = alg[dom] / (kern[dom] * 1e-3) / 1e9
+        dwt_alone = float(np.mean([x["dwt_ms"] for x in alone]))
         traffic, traffic_src = pmc_traffic(dom)
         # SURVEY.md 8(d) full path: B_path = B_dwt + 4C + 3*bpp/8 per pixel
         bpp = 8 * avg["out_bytes"] / npx
@@ -250,11 +271,18 @@ def run(args):
             "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
                               "achieved": round(b_path * px_per_s_gpu / 1e9, 2), "peak": HBM_PEAK / 1e9,
                               "unit": "GB/s", "frac": round(b_path * px_per_s_gpu / HBM_PEAK, 5)},
+            # DWT stage time from HIP events on the context's stream: under
+            # load (12 images in flight, the event span includes waiting for
+            # CUs other images hold) and alone (one image on the GPU)
             "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                              "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                              "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
                              "alg_bytes_per_px": round(dwt_bytes_per_px(C, 1, L), 3),
-                             "stage_ms": round(avg["dwt_ms"], 4)},
+                             "stage_ms": round(avg["dwt_ms"], 4),
+                             "alone": {"stage_ms": round(dwt_alone, 4),
+                                       "achieved": round(dwt_alg / (dwt_alone * 1e-3) / 1e9, 2),
+                                       "frac": round(dwt_alg / (dwt_alone * 1e-3) / HBM_PEAK, 5)}},
+            "t1_counters": {"k_t1_mq": sq_counters("k_t1_mq"), "k_t1_cm": sq_counters("k_t1_cm")},
             "stages_ms": {k: round(avg[k], 4) for k in ("ingest_ms", "dwt_ms", "quant_ms", "t1_cm_ms",
                                                         "t1_mq_ms", "pcrd_ms", "d2h_ms", "t2_ms",
                                                         "total_ms")},
