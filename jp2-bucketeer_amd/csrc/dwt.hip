@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "gpu_encoder.h"
 
@@ -373,7 +374,8 @@ static void launch_band(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a
 }
 template <bool REV, bool INGEST>
 static void launch_band_rb(int RB, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
-    if (RB == 16) launch_band<REV, INGEST, 16>(g, lds, st, a);
+    if (RB == 32) launch_band<REV, INGEST, 32>(g, lds, st, a);
+    else if (RB == 16) launch_band<REV, INGEST, 16>(g, lds, st, a);
     else launch_band<REV, INGEST, 8>(g, lds, st, a);
 }
 
@@ -410,7 +412,11 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             return hipGetLastError() == hipSuccess;
         }
         // kept rows per workgroup: 16, or 8 for rows wider than 2048
-        const int R = maxW <= 2048 ? 16 : 8;
+        int R = 8;  // kept rows per workgroup (8: more workgroups in flight; 16/32 measured slower)
+        if (const char *e = getenv("JP2HIP_DWT_RB")) {  // experiment knob
+            const int r = atoi(e);
+            if ((r == 8 || r == 16 || r == 32) && (size_t)r * maxW <= (size_t)kDwtLdsWordsWide) R = r;
+        }
         a.level = lv;
         a.R = R;
         a.src = scratch[(lv - 1) & 1];
