@@ -235,9 +235,9 @@ typedef int (*jp2hip_upload_fn)(void *user, const char *image_id_utf8, const cha
 
 typedef struct jp2hip_batch_config {
     int32_t device;              /* HIP device ordinal                               */
-    int32_t contexts;            /* images in flight on the GPU (<=0: 3)             */
-    int32_t reader_threads;      /* TIFF readers (<=0: 2)                            */
-    int32_t uploader_threads;    /* JPX writers + uploaders (<=0: 2)                 */
+    int32_t contexts;            /* images in flight on the GPU (<=0: 12)            */
+    int32_t reader_threads;      /* TIFF readers (<=0: 4)                            */
+    int32_t uploader_threads;    /* JPX writers + uploaders (<=0: 4)                 */
     int32_t host_threads;        /* tier-2 threads per context (<=0: 16 / contexts)  */
     int32_t delete_after_upload; /* derivative-image=true: remove the JPX once sent  */
     int32_t write_output;        /* 0: keep the JPX in memory, skip the file write   */

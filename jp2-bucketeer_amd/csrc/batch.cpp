@@ -289,9 +289,9 @@ int jp2hip_batch_create(jp2hip_batch **out, const jp2hip_batch_config *cfg, jp2h
     jp2hip_batch_config c;
     std::memset(&c, 0, sizeof c);
     if (cfg) c = *cfg;
-    if (c.contexts <= 0) c.contexts = 3;
-    if (c.reader_threads <= 0) c.reader_threads = 2;
-    if (c.uploader_threads <= 0) c.uploader_threads = 2;
+    if (c.contexts <= 0) c.contexts = 12;  // ~12 images in flight per GPU
+    if (c.reader_threads <= 0) c.reader_threads = 4;
+    if (c.uploader_threads <= 0) c.uploader_threads = 4;
     if (c.host_threads <= 0) c.host_threads = std::max(2, 16 / c.contexts);
     jp2hip_batch *b = new jp2hip_batch();
     b->cfg = c;

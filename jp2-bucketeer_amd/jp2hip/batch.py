@@ -124,9 +124,12 @@ class BatchQueue:
     ``upload(image_id, jpx_path) -> bool`` is the S3 stand-in; None selects
     the built-in stub that reads every byte of the file."""
 
-    def __init__(self, device: int = 0, contexts: int = 3, reader_threads: int = 2,
-                 uploader_threads: int = 2, host_threads: int = 0, delete_after_upload: bool = True,
+    def __init__(self, device: int = 0, contexts: int = 12, reader_threads: int = 4,
+                 uploader_threads: int = 4, host_threads: int = 0, delete_after_upload: bool = True,
                  write_output: bool = True, upload=None):
+        # one HW queue per context (+4 for the runtime); only takes effect if
+        # nothing in this process has initialised HIP yet (DESIGN.md 5)
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, (contexts or 12) + 4))))
         L = _bind()
         cfg = BatchConfig(device, contexts, reader_threads, uploader_threads, host_threads,
                           1 if delete_after_upload else 0, 1 if write_output else 0, 0)
