@@ -323,6 +323,78 @@ def c5_band(rank, world, threads=16):
     return buf.tobytes(), lay, offs, (r0, r1)
 
 
+def run_c4(args):
+    """C4 (configs[3]) at reduced size: a Bucketeer batch CSV of synthetic
+    5000x7000 RGB8 TIFFs (cycling over a few distinct files, as SURVEY.md 8(d)
+    prescribes for the 10k-row batch), lossless (ImageWorker hard-codes it),
+    through one GPU's native batch queue per rank: TIFF read -> encode -> JPX
+    write -> stub upload (reads every byte) -> delete.  The timed span runs from
+    the first submit to the last upload, file I/O included; rows are sharded
+    round-robin over ranks (no collective)."""
+    import csv as _csv
+    import shutil
+
+    import imaging as im
+    from jp2hip import batch as jb
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="gloo")
+    work = tempfile.mkdtemp(prefix=f"jp2hip_c4_{rank}_")
+    try:
+        ndistinct, rows = 4, args.steps
+        paths = []
+        for i in range(ndistinct):
+            pth = os.path.join(work, f"synth{i:02d}.tif")
+            with open(pth, "wb") as f:
+                f.write(im.tiff_bytes(im.synth_rgb8(7000, 5000, seed=i), rows_per_strip=64))
+            paths.append(pth)
+        csv_path = os.path.join(work, "batch.csv")
+        with open(csv_path, "w", newline="", encoding="utf-8") as f:
+            wr = _csv.writer(f)
+            wr.writerow(["Item ARK", "File Name"])
+            for i in range(rows * world):
+                wr.writerow([f"ark:/99999/synth{i:05d}", os.path.basename(paths[i % ndistinct])])
+        items = jb.shard(jb.read_batch_csv(csv_path, path_prefix=work), rank, world)
+        out_dir = os.path.join(work, "out")
+        os.makedirs(out_dir, exist_ok=True)
+        with jb.BatchQueue(device=local) as q:
+            # warm-up: one image per context, so device buffers exist
+            for k, it in enumerate(items[:12]):
+                q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k))
+            q.drain()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for it in items:
+                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)))
+            res = q.drain()
+            dt = time.perf_counter() - t0
+        ok = sum(1 for r in res if r["status"] == 0)
+        mp = 5000 * 7000 / 1e6 * ok
+        if world > 1:
+            import torch
+            t = torch.tensor([dt, mp], dtype=torch.float64)
+            dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+            dt, mp = float(t[0]), float(t[1])
+            dist.destroy_process_group()
+        if rank != 0:
+            return None
+        return {"metric": METRIC, "value": round(mp / dt, 3), "unit": "MP/s", "n_gpus": world,
+                "steps": rows, "warmup": 1, "ms_per_step": round(dt * 1e3 / rows, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "i32",
+                "data": f"synthetic 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0..{ndistinct - 1}) on local disk",
+                "config": {"workload": "C4: Bucketeer batch CSV -> per-GPU native queue (read, lossless 5/3 encode, "
+                                       "JPX write, stub upload, delete-after-upload), Kakadu recipe",
+                           "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"shards x{world}"}}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def run_c5(args):
     """C5 (configs[4]): one 40000x30000 Gray16 image, lossy 9/7 3 bpp, 7
     levels, tile-split across the ranks (jp2hip.split).  One step = the whole
@@ -402,14 +474,20 @@ def main():
                     help="independent images in flight per GPU (separate contexts/streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lossless", action="store_true")
-    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
-                    help="c2: the headline (replicas); c5: one oversized image tile-split across ranks")
+    ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
+                    help="c2: the headline (replicas); c4: CSV batch through the native per-GPU queue; "
+                         "c5: one oversized image tile-split across ranks")
     args = ap.parse_args()
     # one hardware queue per in-flight context plus a few for the runtime's
     # own streams (HIP's default of 4 makes contexts share queues, and the
     # kernels of a shared queue run one at a time); must be set before
     # anything initialises HIP.  Sweep: profiles/r01/sweep_q2.txt
     os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, args.inflight + 4))))
+    if args.workload == "c4":
+        res = run_c4(args)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        return
     if args.workload == "c5":
         res = run_c5(args)
         if res is not None:
