@@ -27,6 +27,23 @@ __device__ __forceinline__ int64_t dist_gain(uint32_t v, int p, bool lossless) {
     return dist_at(v, p + 1, lossless) - dist_at(v, p, lossless);
 }
 
+// The same quantities in 32-bit arithmetic for planes q <= 14: |error| below
+// plane q is < 2^(q+1) half-units (the residual 2(v mod 2^q) + 1 - 2^q once
+// significant, 2v + 1 < 2^(q+1) before), so its square is < 2^30.
+__device__ __forceinline__ uint32_t err_small(uint32_t v, int q, bool lossless) {
+    const int32_t d = lossless ? 0 : 1;
+    if ((v >> q) != 0) {
+        if (lossless && q == 0) return 0u;
+        const int32_t e = 2 * (int32_t)(v & ((1u << q) - 1u)) + d - (1 << q);
+        return (uint32_t)(e < 0 ? -e : e);
+    }
+    return 2u * v + (uint32_t)d;
+}
+__device__ __forceinline__ int64_t dist_gain_small(uint32_t v, int p, bool lossless) {  // p <= 13
+    const uint32_t e1 = err_small(v, p + 1, lossless), e0 = err_small(v, p, lossless);
+    return (int64_t)(e1 * e1) - (int64_t)(e0 * e0);
+}
+
 __device__ __forceinline__ int64_t wave_sum64(int64_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

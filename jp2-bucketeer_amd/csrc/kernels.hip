@@ -334,14 +334,26 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     bool lossless = a.reversible != 0;
     for (int p = 0; p < P; p++) {
         int64_t ref = 0, sig = 0;
+        if (p <= 13) {  // wave-uniform: 32-bit squares suffice (device_common.h)
 #pragma unroll
-        for (int y = 0; y < 64; y++) {
-            const uint32_t v = col[y] & 0x7FFFFFFFu;  // 0 outside the block
-            const uint32_t hi = v >> p;
-            if (hi == 0) continue;
-            const int64_t g = dist_gain(v, p, lossless);
-            if (hi == 1) sig += g;
-            else ref += g;
+            for (int y = 0; y < 64; y++) {
+                const uint32_t v = col[y] & 0x7FFFFFFFu;  // 0 outside the block
+                const uint32_t hi = v >> p;
+                if (hi == 0) continue;
+                const int64_t g = dist_gain_small(v, p, lossless);
+                if (hi == 1) sig += g;
+                else ref += g;
+            }
+        } else {
+#pragma unroll
+            for (int y = 0; y < 64; y++) {
+                const uint32_t v = col[y] & 0x7FFFFFFFu;
+                const uint32_t hi = v >> p;
+                if (hi == 0) continue;
+                const int64_t g = dist_gain(v, p, lossless);
+                if (hi == 1) sig += g;
+                else ref += g;
+            }
         }
         ref = wave_sum64(ref);
         sig = wave_sum64(sig);
