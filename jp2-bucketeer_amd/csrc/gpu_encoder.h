@@ -51,6 +51,7 @@ struct T1MqArgs {
     int32_t *lengths;
     int *err;
     int lanes;  // blocks per wavefront (1..64)
+    unsigned long long *span;  // [2] execution span in 100 MHz ticks (min start, max end)
     int64_t *dbg;  // optional per-block census [block][4] (debug)
 };
 // fused ingest + DWT (dwt.hip)
@@ -129,7 +130,7 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        est, hist, kcut, pmin, stage, soff, lzwtab, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        est, hist, kcut, pmin, mqspan, stage, soff, lzwtab, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
         dbgbuf;
     int nseg = 0;
     uint8_t *h_packed = nullptr;

@@ -526,17 +526,31 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 // Segment s of a block with P coded planes: s = 0 is the top plane's cleanup
 // pass; s >= 1 is pass (s+2)%3 (0 SPP, 1 MRP, 2 CUP) of plane k = (s+2)/3,
 // planes counted from the top.
+__device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const uint32_t *mqt, uint32_t *rings);
+
+// The launch's execution span is recorded in 100 MHz wall-clock ticks
+// (span[0] = earliest wave start, span[1] = latest lane end; vector atomics),
+// so the encoder reports the kernel's own duration -- what rocprofv3 reports
+// -- rather than an event interval that also holds time spent waiting for
+// CUs behind other images' kernels.
 __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     __shared__ uint32_t cxs[32 * 64];  // 19 contexts; indices 19..31 absorb bytes read past a pass end
     __shared__ uint32_t mqt[48];
     __shared__ uint32_t rings[64 * 17];  // 68 bytes per lane: 64-byte ring + dummy slot
+    if (threadIdx.x == 0) atomicMin(&a.span[0], (unsigned long long)wall_clock64());
     const int lane = threadIdx.x;
-    uint8_t *ring = (uint8_t *)rings + lane * 68;
-    int fl = 0;  // bytes already copied from the ring
     if (lane < 47)
         mqt[lane] = (uint32_t)c_qe[lane] | ((uint32_t)c_nmps[lane] << 16) | ((uint32_t)c_nlps[lane] << 22) |
                     ((uint32_t)(lane == 0 || lane == 6 || lane == 14) << 28);
     __syncthreads();
+    mq_block(a, cxs, mqt, rings);
+    atomicMax(&a.span[1], (unsigned long long)wall_clock64());
+}
+
+__device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const uint32_t *mqt, uint32_t *rings) {
+    const int lane = threadIdx.x;
+    uint8_t *ring = (uint8_t *)rings + lane * 68;
+    int fl = 0;  // bytes already copied from the ring
     // only the first `lanes` lanes of each wave take a block
     if (lane >= a.lanes) return;
     const int gi = blockIdx.x * a.lanes + lane;
