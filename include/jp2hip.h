@@ -87,11 +87,12 @@ typedef struct jp2hip_layout {
     int32_t nstrips;                         /* entries in strip_offsets    */
     const uint64_t *strip_offsets;           /* byte offset of each strip   */
     int32_t compression;                     /* TIFF Compression: 1 (or 0)  */
-                                             /* none, 5 LZW, 32773 PackBits */
+                                             /* none, 5 LZW, 8 / 32946      */
+                                             /* Deflate, 32773 PackBits     */
     int32_t predictor;                       /* TIFF Predictor: 1 none,     */
                                              /* 2 horizontal differencing   */
     const uint64_t *strip_bytes;             /* compressed size per strip   */
-                                             /* (compression 5 / 32773)     */
+                                             /* (compression > 1)           */
     int32_t tile_width, tile_height;         /* tiled TIFF (0: strips): the */
                                              /* "strips" above are then the */
                                              /* tiles, row-major per plane  */
@@ -143,7 +144,8 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
                        jp2hip_stats *stats);
 
 /* Parse a baseline TIFF's header into a layout (offsets into the file).
- * Strips may be uncompressed, LZW (5) or PackBits (32773), with or without
+ * Strips may be uncompressed, LZW (5), Deflate (8, 32946; zlib streams) or
+ * PackBits (32773), with or without
  * horizontal differencing (Predictor 2); compressed strips are decoded on
  * the GPU (one lane per strip) before ingest.  For a compressed file
  * `offsets` receives 2 * nstrips entries: the strip offsets, then their byte

@@ -127,11 +127,11 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     if (tiled && (!tw || !th || (tw % 16) || (th % 16) || tw > 65536 || th > 65536))
         return fail("tiff: bad TileWidth/TileLength");
     if (tiled && !e_cnt) return fail("tiff: tiles need TileByteCounts");
-    // strips: uncompressed, LZW or PackBits (decoded on the GPU, kernels.hip
-    // k_unlzw / k_unpackbits); Deflate / JPEG / CCITT are not supported
-    if (comp != 1 && comp != 5 && comp != 32773)
+    // strips: uncompressed, LZW, Deflate or PackBits (decoded on the GPU,
+    // kernels.hip k_unlzw / k_inflate / k_unpackbits); JPEG / CCITT are not
+    if (comp != 1 && comp != 5 && comp != 8 && comp != 32946 && comp != 32773)
         return fail("tiff: compression " + std::to_string(comp) +
-                    " is not supported (uncompressed, LZW and PackBits only)");
+                    " is not supported (uncompressed, LZW, Deflate and PackBits only)");
     if (pred != 1 && pred != 2) return fail("tiff: predictor " + std::to_string(pred) + " is not supported");
     if (pred == 2 && comp == 1) return fail("tiff: predictor 2 without compression is not supported");
     if (comp != 1 && !e_cnt) return fail("tiff: compressed strips need StripByteCounts");
@@ -221,12 +221,13 @@ void undershoot_terms(const jp2hip::GpuEncoder &g, int64_t &coded, int64_t &skip
     for (size_t b = 0; b < pm.size(); b++) skipped |= pm[b] > 0;
 }
 
-// LZW / PackBits strips are decoded on the GPU into the context's staging
+// LZW / Deflate / PackBits strips are decoded on the GPU into the context's staging
 // buffer first; afterwards (d_src, lay) describe uncompressed strips.
 bool unpack_if_compressed(jp2hip_ctx *ctx, const void *&d_src, size_t src_len, const jp2hip_layout *&lay,
                           jp2hip_layout &ulay, std::vector<uint64_t> &uoffs, std::string &err) {
     if (lay->compression <= 1 && lay->tile_width <= 0) return true;
-    if (lay->compression > 1 && lay->compression != 5 && lay->compression != 32773) {
+    if (lay->compression > 1 && lay->compression != 5 && lay->compression != 8 && lay->compression != 32946 &&
+        lay->compression != 32773) {
         err = "layout: compression " + std::to_string(lay->compression) + " is not supported";
         return false;
     }

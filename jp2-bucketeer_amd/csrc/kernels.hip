@@ -105,9 +105,10 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
 }
 
 // --------------------------------------------------------------------------
-// S1a: compressed strips (TIFF 6.0 sections 9, 13, 14).  The strips of an LZW
-// or PackBits TIFF are decoded in HBM before ingest: one lane per strip (each
-// strip is an independent byte stream), output strip s at s * stride of a
+// S1a: compressed strips (TIFF 6.0 sections 9, 13, 14; Deflate per the TIFF
+// Technical Notes).  The strips of an LZW, Deflate or PackBits TIFF are
+// decoded in HBM before ingest: one lane per strip (each strip is an
+// independent byte stream), output strip s at s * stride of a
 // staging buffer, so ingest then reads an uncompressed layout.  Horizontal
 // differencing (Predictor 2) is undone afterwards, one lane per row.
 // --------------------------------------------------------------------------
@@ -196,6 +197,151 @@ __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
             const uint8_t v = in[ip++];
             for (int i = 0; i < 1 - c; i++) out[pos++] = v;
         }
+    }
+    if (bad || pos != cap) atomicOr(a.err, 2);
+}
+
+// Deflate (RFC 1951) in a zlib wrapper (RFC 1950): TIFF compression 8
+// (Adobe Deflate) and 32946 (the older Deflate code), one lane per strip.
+// Canonical Huffman codes are kept as 16 per-length counts plus the symbols
+// in code order, and a code is decoded by walking the lengths (no lookup
+// table to build, so a block's tables cost ~1 KB of lane scratch).
+__constant__ uint16_t kInfLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                         31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kInfLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kInfDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
+                                          193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kInfDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t kInfClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct InfBits {  // LSB-first bit reader; buf holds cnt (< 8 after a read) unread bits
+    const uint8_t *in;
+    uint64_t n, ip;
+    uint32_t buf;
+    int cnt;
+    bool bad;
+    __device__ __forceinline__ uint32_t get(int need) {
+        uint32_t v = buf;
+        while (cnt < need) {
+            if (ip >= n) { bad = true; return 0; }
+            v |= (uint32_t)in[ip++] << cnt;
+            cnt += 8;
+        }
+        buf = v >> need;
+        cnt -= need;
+        return v & ((1u << need) - 1u);
+    }
+};
+
+__device__ int inf_decode(InfBits &b, const uint16_t *cnt, const uint16_t *sym) {
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; len++) {
+        code |= (int)b.get(1);
+        const int count = cnt[len];
+        if (code - count < first) return sym[index + (code - first)];
+        index += count;
+        first = (first + count) << 1;
+        code <<= 1;
+        if (b.bad) return -1;
+    }
+    return -1;
+}
+
+// false: over-subscribed lengths (an incomplete code is accepted; its unused
+// codes fail in inf_decode)
+__device__ bool inf_build(uint16_t *cnt, uint16_t *sym, const uint8_t *len, int n) {
+    for (int l = 0; l < 16; l++) cnt[l] = 0;
+    for (int s = 0; s < n; s++) cnt[len[s]]++;
+    int left = 1;
+    for (int l = 1; l < 16; l++) {
+        left = (left << 1) - cnt[l];
+        if (left < 0) return false;
+    }
+    uint16_t offs[16];
+    offs[1] = 0;
+    for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
+    for (int s = 0; s < n; s++)
+        if (len[s]) sym[offs[len[s]]++] = (uint16_t)s;
+    return true;
+}
+
+__global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= a.nstrips) return;
+    const uint8_t *in = a.src + a.off[s];
+    const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
+    uint8_t *out = a.dst + (uint64_t)s * a.stride;
+    uint64_t pos = 0;
+    bool bad = n < 2 || (in[0] & 15) != 8 || (in[0] >> 4) > 7 || ((in[0] << 8) | in[1]) % 31 || (in[1] & 0x20);
+    InfBits b{in, n, 2, 0u, 0, false};
+    uint16_t lcnt[16], lsym[288], dcnt[16], dsym[30];
+    uint8_t lens[320];
+    bool last = false;
+    while (!bad && !last) {
+        last = b.get(1);
+        const int type = (int)b.get(2);
+        if (type == 0) {  // stored: skip to the byte boundary, LEN, ~LEN, bytes
+            b.buf = 0;
+            b.cnt = 0;
+            if (b.ip + 4 > n) { bad = true; break; }
+            const uint32_t len = in[b.ip] | ((uint32_t)in[b.ip + 1] << 8);
+            const uint32_t nlen = in[b.ip + 2] | ((uint32_t)in[b.ip + 3] << 8);
+            b.ip += 4;
+            if (len != (~nlen & 0xFFFFu) || b.ip + len > n || pos + len > cap) { bad = true; break; }
+            for (uint32_t i = 0; i < len; i++) out[pos + i] = in[b.ip + i];
+            b.ip += len;
+            pos += len;
+            continue;
+        }
+        if (type == 1) {  // fixed codes
+            for (int i = 0; i < 288; i++) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+            for (int i = 0; i < 30; i++) lens[288 + i] = 5;
+            inf_build(lcnt, lsym, lens, 288);
+            inf_build(dcnt, dsym, lens + 288, 30);
+        } else if (type == 2) {  // dynamic codes
+            const int nlen = (int)b.get(5) + 257, ndist = (int)b.get(5) + 1, ncode = (int)b.get(4) + 4;
+            if (nlen > 286 || ndist > 30) { bad = true; break; }
+            for (int i = 0; i < 19; i++) lens[kInfClOrder[i]] = i < ncode ? (uint8_t)b.get(3) : 0;
+            if (b.bad || !inf_build(lcnt, lsym, lens, 19)) { bad = true; break; }
+            int i = 0;
+            while (i < nlen + ndist) {
+                const int sy = inf_decode(b, lcnt, lsym);
+                if (sy < 0 || b.bad) { bad = true; break; }
+                if (sy < 16) { lens[i++] = (uint8_t)sy; continue; }
+                uint8_t v = 0;
+                int rep;
+                if (sy == 16) {
+                    if (i == 0) { bad = true; break; }
+                    v = lens[i - 1];
+                    rep = 3 + (int)b.get(2);
+                } else if (sy == 17) rep = 3 + (int)b.get(3);
+                else rep = 11 + (int)b.get(7);
+                if (i + rep > nlen + ndist) { bad = true; break; }
+                while (rep--) lens[i++] = v;
+            }
+            if (bad || lens[256] == 0) { bad = true; break; }
+            if (!inf_build(lcnt, lsym, lens, nlen) || !inf_build(dcnt, dsym, lens + nlen, ndist)) { bad = true; break; }
+        } else { bad = true; break; }
+        for (;;) {  // literal / length-distance symbols up to end-of-block
+            int sy = inf_decode(b, lcnt, lsym);
+            if (sy < 0 || b.bad) { bad = true; break; }
+            if (sy < 256) {
+                if (pos >= cap) { bad = true; break; }
+                out[pos++] = (uint8_t)sy;
+                continue;
+            }
+            if (sy == 256) break;
+            sy -= 257;
+            if (sy >= 29) { bad = true; break; }
+            const uint32_t len = kInfLenBase[sy] + b.get(kInfLenExtra[sy]);
+            const int d = inf_decode(b, dcnt, dsym);
+            if (d < 0 || d >= 30) { bad = true; break; }
+            const uint32_t dist = kInfDistBase[d] + b.get(kInfDistExtra[d]);
+            if (b.bad || dist > pos || pos + len > cap) { bad = true; break; }
+            for (uint32_t k = 0; k < len; k++) out[pos + k] = out[pos - dist + k];  // may overlap forward
+            pos += len;
+        }
+        if (b.bad) bad = true;
     }
     if (bad || pos != cap) atomicOr(a.err, 2);
 }
@@ -720,6 +866,8 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
         ua.tab = (uint32_t *)lzwtab.ptr;
         ua.err = (int *)this->err.ptr;
         if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
+        else if (lay.compression == 8 || lay.compression == 32946)
+            hipLaunchKernelGGL(k_inflate, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
         else hipLaunchKernelGGL(k_unpackbits, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
         HIPCHECK(hipGetLastError());
         if (lay.predictor == 2) {  // per decoded row of a strip / of a tile

@@ -265,7 +265,8 @@ def tile_parts(cs: bytes):
 
 
 def tiff_bytes_compressed(img: np.ndarray, compression: str, predictor: bool = False, rows_per_strip: int = 16) -> bytes:
-    """LZW ("tiff_lzw") or PackBits ("packbits") strip TIFF written by Pillow's
+    """LZW ("tiff_lzw"), Deflate ("tiff_adobe_deflate" = 8, "tiff_deflate" =
+    32946) or PackBits ("packbits") strip TIFF written by Pillow's
     libtiff (test fixture generator only), optionally with Predictor 2."""
     import io
     from PIL import Image, TiffImagePlugin
@@ -277,7 +278,13 @@ def tiff_bytes_compressed(img: np.ndarray, compression: str, predictor: bool = F
     row = img.shape[1] * (img.shape[2] if img.ndim == 3 else 1) * img.dtype.itemsize
     b = io.BytesIO()
     Image.fromarray(img).save(b, format="TIFF", compression=compression, strip_size=row * rows_per_strip, **kw)
-    return b.getvalue()
+    data = b.getvalue()
+    if compression == "tiff_deflate":  # libtiff writes 8 for both; keep the old code's value in the tag
+        tag = struct.pack("<HHIHH", 259, 3, 1, 8, 0)
+        i = data.find(tag)
+        assert i > 0
+        data = data[:i] + struct.pack("<HHIHH", 259, 3, 1, 32946, 0) + data[i + len(tag):]
+    return data
 
 
 def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False) -> bytes:
@@ -326,9 +333,13 @@ def packbits_encode(raw: bytes) -> bytes:
     return bytes(out)
 
 
-def tiled_tiff_bytes(img: np.ndarray, tile=(32, 48), planar=False, big_endian=False, packbits=False) -> bytes:
+def tiled_tiff_bytes(img: np.ndarray, tile=(32, 48), planar=False, big_endian=False, packbits=False,
+                     deflate=False) -> bytes:
     """Classic tiled TIFF (TileWidth/TileLength/TileOffsets/TileByteCounts),
-    uncompressed or PackBits; edge tiles padded with zeros as TIFF requires."""
+    uncompressed, PackBits or Deflate (zlib levels 0 / 1 / 9 in turn, so
+    stored, fixed-Huffman and dynamic-Huffman blocks all occur); edge tiles
+    padded with zeros as TIFF requires."""
+    import zlib
     if img.ndim == 2:
         img = img[..., None]
     h, w, nc = img.shape
@@ -345,7 +356,10 @@ def tiled_tiff_bytes(img: np.ndarray, tile=(32, 48), planar=False, big_endian=Fa
                 part = pl[ty * th:(ty + 1) * th, tx * tw:(tx + 1) * tw]
                 t[:part.shape[0], :part.shape[1]] = part
                 raw = t.astype(t.dtype.newbyteorder(e)).tobytes()
-                tiles.append(packbits_encode(raw) if packbits else raw)
+                if deflate:
+                    tiles.append(zlib.compress(raw, (0, 1, 9)[len(tiles) % 3]))
+                else:
+                    tiles.append(packbits_encode(raw) if packbits else raw)
     nt = len(tiles)
     ntags = 13
     ifd_off = 8
@@ -364,7 +378,7 @@ def tiled_tiff_bytes(img: np.ndarray, tile=(32, 48), planar=False, big_endian=Fa
         return struct.pack(e + "HHI", tag, typ, cnt) + v
 
     tags = [ent(256, 4, 1, w), ent(257, 4, 1, h), ent(258, 3, nc, bps_off) if nc > 1 else ent(258, 3, 1, bits),
-            ent(259, 3, 1, 32773 if packbits else 1), ent(262, 3, 1, 2 if nc >= 3 else 1), ent(277, 3, 1, nc),
+            ent(259, 3, 1, 8 if deflate else 32773 if packbits else 1), ent(262, 3, 1, 2 if nc >= 3 else 1), ent(277, 3, 1, nc),
             ent(284, 3, 1, 2 if planar else 1), ent(322, 4, 1, tw), ent(323, 4, 1, th),
             ent(324, 4, nt, to_off if nt > 1 else offs[0]), ent(325, 4, nt, tbc_off if nt > 1 else len(tiles[0])),
             ent(339, 3, 1, 1), ent(338, 3, 1, 2) if nc in (2, 4) else ent(305, 2, 1, 0)]

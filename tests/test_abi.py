@@ -97,17 +97,19 @@ def test_tiff_layout_rejects(bad, msg):
 
 def test_tiff_layout_rejects_unsupported_compression():
     data = bytearray(im.tiff_bytes(im.synth_rgb8(8, 8)))
-    # Compression tag (259) value -> 8 (Deflate)
+    # Compression tag (259) value -> 7 (JPEG)
     i = data.find(bytes([0x03, 0x01, 0x03, 0x00, 0x01, 0x00, 0x00, 0x00, 0x01, 0x00]))
     assert i > 0
-    data[i + 8] = 8
-    with pytest.raises(jp2hip.Jp2hipError, match="compression 8"):
+    data[i + 8] = 7
+    with pytest.raises(jp2hip.Jp2hipError, match="compression 7"):
         jp2hip.tiff_layout(bytes(data))
 
 
-@pytest.mark.parametrize("comp,code,pred", [("tiff_lzw", 5, False), ("tiff_lzw", 5, True), ("packbits", 32773, False)])
+@pytest.mark.parametrize("comp,code,pred", [("tiff_lzw", 5, False), ("tiff_lzw", 5, True), ("packbits", 32773, False),
+                                            ("tiff_adobe_deflate", 8, False), ("tiff_adobe_deflate", 8, True),
+                                            ("tiff_deflate", 32946, False)])
 def test_tiff_layout_compressed_strips(comp, code, pred):
-    """LZW / PackBits strips: offsets, then byte counts, match the file's tags."""
+    """LZW / Deflate / PackBits strips: offsets, then byte counts, match the file's tags."""
     from PIL import Image
     import io
     img = im.synth_rgb8(70, 90, seed=2)

@@ -156,9 +156,10 @@ def test_tiff_variants_same_output(encoder):
 
 @pytest.mark.parametrize("comp,pred,kind", [("tiff_lzw", False, "rgb8"), ("tiff_lzw", True, "rgb8"),
                                             ("packbits", False, "rgb8"), ("tiff_lzw", True, "gray16"),
-                                            ("packbits", False, "gray16")])
+                                            ("packbits", False, "gray16"), ("tiff_adobe_deflate", False, "rgb8"),
+                                            ("tiff_adobe_deflate", True, "gray16"), ("tiff_deflate", True, "rgb8")])
 def test_compressed_strips_same_output(encoder, comp, pred, kind):
-    """LZW / PackBits (+ Predictor 2) strips decoded on the GPU: the file equals
+    """LZW / Deflate / PackBits (+ Predictor 2) strips decoded on the GPU: the file equals
     the encode of the same pixels from an uncompressed TIFF (and the oracle)."""
     img = im.synth_rgb8(301, 517, seed=9) if kind == "rgb8" else im.synth_u16(301, 517, comps=1, seed=9)
     for conv in (jp2hip.LOSSLESS, jp2hip.LOSSY):
@@ -179,7 +180,8 @@ def test_bigtiff_same_output(encoder):
 
 @pytest.mark.parametrize("kw,kind", [({}, "rgb8"), ({"packbits": True}, "rgb8"),
                                      ({"planar": True, "big_endian": True}, "rgb16"),
-                                     ({"packbits": True, "big_endian": True}, "gray16")])
+                                     ({"packbits": True, "big_endian": True}, "gray16"),
+                                     ({"deflate": True}, "rgb8"), ({"deflate": True, "planar": True}, "rgb16")])
 def test_tiled_tiff_same_output(encoder, kw, kind):
     """Tiled TIFFs (edge tiles padded) are untiled in HBM: same file as the
     strip TIFF of the same pixels."""
@@ -199,6 +201,24 @@ def test_corrupt_compressed_strip_fails_loudly(encoder):
     lay, keep = jp2hip.tiff_layout(bytes(data))
     o, n = lay.strip_offsets[0], lay.strip_bytes[0]
     data[o:o + n] = bytes([0x80]) * n  # PackBits no-ops only: the strip decodes short
+    with pytest.raises(jp2hip.Jp2hipError, match="corrupt"):
+        encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
+
+
+@pytest.mark.parametrize("damage", ["header", "truncate", "bad_block"])
+def test_corrupt_deflate_strip_fails_loudly(encoder, damage):
+    """A bad zlib header, a strip cut short, or a reserved block type (3) all
+    report a corrupt strip instead of encoding garbage."""
+    img = im.synth_rgb8(64, 64, seed=1)
+    data = bytearray(im.tiff_bytes_compressed(img, "tiff_adobe_deflate", rows_per_strip=32))
+    lay, keep = jp2hip.tiff_layout(bytes(data))
+    o, n = lay.strip_offsets[1], lay.strip_bytes[1]
+    if damage == "header":
+        data[o] = 0x79  # CM 9: not Deflate
+    elif damage == "truncate":
+        data[o + n // 2:o + n] = bytes(n - n // 2)  # second half zeroed: stored blocks of the wrong length / short
+    else:
+        data[o + 2] = 0x07  # BFINAL 1, BTYPE 3
     with pytest.raises(jp2hip.Jp2hipError, match="corrupt"):
         encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
 
