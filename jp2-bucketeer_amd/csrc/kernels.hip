@@ -119,7 +119,7 @@ struct UnpackArgs {
     uint64_t row_bytes, stride;  // decoded row and strip stride (bytes)
     uint64_t unit_bytes;         // tiles: every unit decodes to this many bytes
     uint8_t *dst;
-    uint32_t *tab;  // LZW: 4096 entries (start, length) per strip
+    uint32_t *tab;  // unused (the LZW string table lives in LDS)
     int *err;
 };
 
@@ -133,19 +133,33 @@ __device__ __forceinline__ uint64_t strip_out_bytes(const UnpackArgs &a, int s) 
 // string of table entry k is (start, length) inside the strip's own output
 // (entry k = string(prev) + first byte of the next string, which is exactly
 // where the decoder wrote them), so decoding is copying, as in LZ77.
+// One strip per single-lane workgroup: a strip's decode is one serial chain,
+// so strips must not share a wave (divergent lanes run each other's paths);
+// the 4096-entry string table lives in LDS, and a string is copied 8 bytes
+// of independent loads at a time.
 __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
-    const int s = blockIdx.x * 64 + threadIdx.x;
-    if (s >= a.nstrips) return;
+    __shared__ uint2 tab[4096];
+    const int s = blockIdx.x;
+    if (s >= a.nstrips || threadIdx.x) return;
     const uint8_t *in = a.src + a.off[s];
     const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
-    uint2 *tab = (uint2 *)(a.tab + (size_t)s * 8192);
     uint64_t ip = 0, pos = 0, acc = 0, prev_pos = 0;
     int nbits = 0, width = 9, next = 258;
     uint32_t prev_len = 0;
     bool bad = false;
     for (;;) {
-        while (nbits < width && ip < n) { acc = (acc << 8) | in[ip++]; nbits += 8; }
+        if (nbits < width) {  // top up to >= 32 bits with independent byte loads
+            if (ip + 4 <= n) {
+                const uint32_t w4 = ((uint32_t)in[ip] << 24) | ((uint32_t)in[ip + 1] << 16) |
+                                    ((uint32_t)in[ip + 2] << 8) | in[ip + 3];
+                acc = (acc << 32) | w4;
+                ip += 4;
+                nbits += 32;
+            } else {
+                while (nbits < width && ip < n) { acc = (acc << 8) | in[ip++]; nbits += 8; }
+            }
+        }
         if (nbits < width) break;  // input exhausted: treat as end of information
         const int code = (int)((acc >> (nbits - width)) & ((1u << width) - 1u));
         nbits -= width;
@@ -159,11 +173,22 @@ __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
             len = 1;
         } else {
             uint64_t from;
+            bool kwk = false;  // string(prev) + its own first byte: the last byte is the first
             if (code < next) { const uint2 e = tab[code]; from = e.x; len = e.y; }
-            else if (code == next && prev_len) { from = prev_pos; len = prev_len + 1; }
+            else if (code == next && prev_len) { from = prev_pos; len = prev_len + 1; kwk = true; }
             else { bad = true; break; }
             if (pos + len > cap) { bad = true; break; }
-            for (uint32_t i = 0; i < len; i++) out[pos + i] = out[from + i];  // may overlap forward
+            const uint32_t body = kwk ? len - 1 : len;  // source bytes all lie before pos
+            uint32_t k = 0;
+            for (; k + 8 <= body; k += 8) {
+                uint8_t t[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) t[j] = out[from + k + j];
+#pragma unroll
+                for (int j = 0; j < 8; j++) out[pos + k + j] = t[j];
+            }
+            for (; k < body; k++) out[pos + k] = out[from + k];
+            if (kwk) out[pos + body] = out[from];
             pos += len;
         }
         if (prev_len && next < 4096) {
@@ -178,9 +203,11 @@ __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
 }
 
 // PackBits: n in 0..127 copies n+1 literal bytes, -127..-1 repeats the next
-// byte 1-n times, -128 is a no-op.
+// byte 1-n times, -128 is a no-op.  One strip per wave: every lane walks the
+// same run headers (uniform control flow), and a run's bytes are written by
+// the 64 lanes together.
 __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
-    const int s = blockIdx.x * 64 + threadIdx.x;
+    const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= a.nstrips) return;
     const uint8_t *in = a.src + a.off[s];
     const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
@@ -191,14 +218,17 @@ __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
         const int c = (int8_t)in[ip++];
         if (c >= 0) {
             if (ip + c + 1 > n || pos + c + 1 > cap) { bad = true; break; }
-            for (int i = 0; i <= c; i++) out[pos++] = in[ip++];
+            for (int i = lane; i <= c; i += 64) out[pos + i] = in[ip + i];
+            ip += c + 1;
+            pos += c + 1;
         } else if (c != -128) {
             if (ip >= n || pos + 1 - c > cap) { bad = true; break; }
             const uint8_t v = in[ip++];
-            for (int i = 0; i < 1 - c; i++) out[pos++] = v;
+            for (int i = lane; i < 1 - c; i += 64) out[pos + i] = v;
+            pos += 1 - c;
         }
     }
-    if (bad || pos != cap) atomicOr(a.err, 2);
+    if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
 }
 
 // Deflate (RFC 1951) in a zlib wrapper (RFC 1950): TIFF compression 8
@@ -214,42 +244,79 @@ __constant__ uint16_t kInfDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    1
 __constant__ uint8_t kInfDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kInfClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-struct InfBits {  // LSB-first bit reader; buf holds cnt (< 8 after a read) unread bits
+// LSB-first bit reader: up to 64 bits buffered, refilled 32 bits at a time
+// from a word loaded one refill ahead, so the HBM latency of the input
+// overlaps the decoding of the bits already held.
+struct InfBits {
     const uint8_t *in;
-    uint64_t n, ip;
-    uint32_t buf;
+    uint64_t n, ip;  // ip: next byte not yet in buf or pf
+    uint64_t buf;
     int cnt;
-    bool bad;
-    __device__ __forceinline__ uint32_t get(int need) {
-        uint32_t v = buf;
-        while (cnt < need) {
-            if (ip >= n) { bad = true; return 0; }
-            v |= (uint32_t)in[ip++] << cnt;
-            cnt += 8;
-        }
-        buf = v >> need;
-        cnt -= need;
-        return v & ((1u << need) - 1u);
+    uint32_t pf;     // the 4 bytes at ip - 4 .. ip - 1 once pf_ok
+    bool pf_ok, bad;
+    __device__ __forceinline__ uint32_t load4(uint64_t p) const {
+        return in[p] | ((uint32_t)in[p + 1] << 8) | ((uint32_t)in[p + 2] << 16) | ((uint32_t)in[p + 3] << 24);
     }
+    __device__ __forceinline__ void init(const uint8_t *src, uint64_t len, uint64_t start) {
+        in = src; n = len; ip = start; buf = 0; cnt = 0; bad = false;
+        pf_ok = ip + 4 <= n;
+        if (pf_ok) { pf = load4(ip); ip += 4; }
+    }
+    __device__ __forceinline__ void refill() {
+        if (cnt > 32) return;
+        if (pf_ok) {
+            buf |= (uint64_t)pf << cnt;
+            cnt += 32;
+            pf_ok = ip + 4 <= n;
+            if (pf_ok) { pf = load4(ip); ip += 4; }
+        } else {
+            while (cnt <= 56 && ip < n) { buf |= (uint64_t)in[ip++] << cnt; cnt += 8; }
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(int k) { refill(); return (uint32_t)buf & ((1u << k) - 1u); }
+    __device__ __forceinline__ void drop(int k) {
+        if (cnt < k) { bad = true; cnt = 0; buf = 0; return; }
+        buf >>= k; cnt -= k;
+    }
+    __device__ __forceinline__ uint32_t get(int k) {  // k <= 16
+        const uint32_t v = peek(k);
+        drop(k);
+        return v;
+    }
+    __device__ __forceinline__ void align() { drop(cnt & 7); }
 };
 
-__device__ int inf_decode(InfBits &b, const uint16_t *cnt, const uint16_t *sym) {
+// Canonical Huffman table: 16 per-length counts, the symbols in code order,
+// and a 2^FB-entry direct lookup ((len << 9) | sym) for codes of <= FB bits
+// (0: longer code, decoded by walking the lengths).
+__device__ int inf_walk(InfBits &b, const uint16_t *cnt, const uint16_t *sym) {
     int code = 0, first = 0, index = 0;
     for (int len = 1; len <= 15; len++) {
         code |= (int)b.get(1);
+        if (b.bad) return -1;
         const int count = cnt[len];
         if (code - count < first) return sym[index + (code - first)];
         index += count;
         first = (first + count) << 1;
         code <<= 1;
-        if (b.bad) return -1;
     }
     return -1;
 }
 
+template <int FB>
+__device__ __forceinline__ int inf_decode(InfBits &b, const uint16_t *fast, const uint16_t *cnt, const uint16_t *sym) {
+    const uint32_t e = fast[b.peek(FB)];
+    if (e) {
+        b.drop((int)(e >> 9));
+        return b.bad ? -1 : (int)(e & 511u);
+    }
+    return inf_walk(b, cnt, sym);
+}
+
 // false: over-subscribed lengths (an incomplete code is accepted; its unused
-// codes fail in inf_decode)
-__device__ bool inf_build(uint16_t *cnt, uint16_t *sym, const uint8_t *len, int n) {
+// codes fail in inf_walk)
+template <int FB>
+__device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const uint8_t *len, int n) {
     for (int l = 0; l < 16; l++) cnt[l] = 0;
     for (int s = 0; s < n; s++) cnt[len[s]]++;
     int left = 1;
@@ -257,55 +324,82 @@ __device__ bool inf_build(uint16_t *cnt, uint16_t *sym, const uint8_t *len, int 
         left = (left << 1) - cnt[l];
         if (left < 0) return false;
     }
-    uint16_t offs[16];
+    uint16_t offs[16], next[16];
     offs[1] = 0;
     for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
-    for (int s = 0; s < n; s++)
-        if (len[s]) sym[offs[len[s]]++] = (uint16_t)s;
+    int code = 0;
+    next[0] = 0;
+    for (int l = 1; l < 16; l++) {
+        code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
+        next[l] = (uint16_t)code;
+    }
+    for (int i = 0; i < (1 << FB); i++) fast[i] = 0;
+    for (int s = 0; s < n; s++) {
+        const int l = len[s];
+        if (!l) continue;
+        sym[offs[l]++] = (uint16_t)s;
+        const uint32_t c = next[l]++;
+        if (l <= FB) {
+            const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);  // stream order: code MSB first
+            for (uint32_t i = r; i < (1u << FB); i += 1u << l) fast[i] = (uint16_t)((l << 9) | s);
+        }
+    }
     return true;
 }
 
+// One strip per single-lane workgroup (see k_unlzw); the code tables and the
+// 32 KB sliding window live in LDS, so matches copy from LDS, not from HBM,
+// and the output reaches HBM from the window in 16-byte stores every 4 KB
+// (per-byte global stores would make every input refill wait on them).
 __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
-    const int s = blockIdx.x * 64 + threadIdx.x;
-    if (s >= a.nstrips) return;
+    constexpr int LB = 10, DB = 8;
+    constexpr uint32_t WM = 32767;
+    __shared__ uint16_t lcnt[16], lsym[288], dcnt[16], dsym[32], lfast[1 << LB], dfast[1 << DB];
+    __shared__ uint8_t lens[320];
+    __shared__ __attribute__((aligned(16))) uint8_t win[WM + 1];
+    const int s = blockIdx.x;
+    if (s >= a.nstrips || threadIdx.x) return;
     const uint8_t *in = a.src + a.off[s];
     const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
-    uint64_t pos = 0;
+    uint64_t pos = 0, flushed = 0;
+    auto flush = [&](uint64_t upto) {
+        for (; flushed + 16 <= upto; flushed += 16)
+            *(uint4 *)(out + flushed) = *(const uint4 *)&win[(uint32_t)flushed & WM];
+        for (; flushed < upto; flushed++) out[flushed] = win[(uint32_t)flushed & WM];
+    };
     bool bad = n < 2 || (in[0] & 15) != 8 || (in[0] >> 4) > 7 || ((in[0] << 8) | in[1]) % 31 || (in[1] & 0x20);
-    InfBits b{in, n, 2, 0u, 0, false};
-    uint16_t lcnt[16], lsym[288], dcnt[16], dsym[30];
-    uint8_t lens[320];
+    InfBits b;
+    b.init(in, n, 2);
     bool last = false;
     while (!bad && !last) {
         last = b.get(1);
         const int type = (int)b.get(2);
-        if (type == 0) {  // stored: skip to the byte boundary, LEN, ~LEN, bytes
-            b.buf = 0;
-            b.cnt = 0;
-            if (b.ip + 4 > n) { bad = true; break; }
-            const uint32_t len = in[b.ip] | ((uint32_t)in[b.ip + 1] << 8);
-            const uint32_t nlen = in[b.ip + 2] | ((uint32_t)in[b.ip + 3] << 8);
-            b.ip += 4;
-            if (len != (~nlen & 0xFFFFu) || b.ip + len > n || pos + len > cap) { bad = true; break; }
-            for (uint32_t i = 0; i < len; i++) out[pos + i] = in[b.ip + i];
-            b.ip += len;
-            pos += len;
+        if (b.bad) { bad = true; break; }
+        if (type == 0) {  // stored: to the byte boundary, LEN, ~LEN, bytes
+            b.align();
+            const uint32_t len = b.get(16), nlen = b.get(16);
+            if (b.bad || len != (~nlen & 0xFFFFu) || pos + len > cap) { bad = true; break; }
+            for (uint32_t i = 0; i < len; i++) {
+                win[(uint32_t)pos & WM] = (uint8_t)b.get(8);
+                if (++pos - flushed >= 4096) flush(flushed + 4096);
+            }
+            if (b.bad) { bad = true; break; }
             continue;
         }
         if (type == 1) {  // fixed codes
             for (int i = 0; i < 288; i++) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
             for (int i = 0; i < 30; i++) lens[288 + i] = 5;
-            inf_build(lcnt, lsym, lens, 288);
-            inf_build(dcnt, dsym, lens + 288, 30);
+            inf_build<LB>(lcnt, lsym, lfast, lens, 288);
+            inf_build<DB>(dcnt, dsym, dfast, lens + 288, 30);
         } else if (type == 2) {  // dynamic codes
             const int nlen = (int)b.get(5) + 257, ndist = (int)b.get(5) + 1, ncode = (int)b.get(4) + 4;
             if (nlen > 286 || ndist > 30) { bad = true; break; }
             for (int i = 0; i < 19; i++) lens[kInfClOrder[i]] = i < ncode ? (uint8_t)b.get(3) : 0;
-            if (b.bad || !inf_build(lcnt, lsym, lens, 19)) { bad = true; break; }
+            if (b.bad || !inf_build<7>(lcnt, lsym, lfast, lens, 19)) { bad = true; break; }
             int i = 0;
             while (i < nlen + ndist) {
-                const int sy = inf_decode(b, lcnt, lsym);
+                const int sy = inf_decode<7>(b, lfast, lcnt, lsym);
                 if (sy < 0 || b.bad) { bad = true; break; }
                 if (sy < 16) { lens[i++] = (uint8_t)sy; continue; }
                 uint8_t v = 0;
@@ -319,30 +413,46 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
                 if (i + rep > nlen + ndist) { bad = true; break; }
                 while (rep--) lens[i++] = v;
             }
-            if (bad || lens[256] == 0) { bad = true; break; }
-            if (!inf_build(lcnt, lsym, lens, nlen) || !inf_build(dcnt, dsym, lens + nlen, ndist)) { bad = true; break; }
+            if (bad || b.bad || lens[256] == 0) { bad = true; break; }
+            if (!inf_build<LB>(lcnt, lsym, lfast, lens, nlen) || !inf_build<DB>(dcnt, dsym, dfast, lens + nlen, ndist)) {
+                bad = true;
+                break;
+            }
         } else { bad = true; break; }
         for (;;) {  // literal / length-distance symbols up to end-of-block
-            int sy = inf_decode(b, lcnt, lsym);
-            if (sy < 0 || b.bad) { bad = true; break; }
+            int sy = inf_decode<LB>(b, lfast, lcnt, lsym);
+            if (sy < 0) { bad = true; break; }
             if (sy < 256) {
                 if (pos >= cap) { bad = true; break; }
-                out[pos++] = (uint8_t)sy;
+                win[(uint32_t)pos++ & WM] = (uint8_t)sy;
+                if (pos - flushed >= 4096) flush(flushed + 4096);
                 continue;
             }
             if (sy == 256) break;
             sy -= 257;
             if (sy >= 29) { bad = true; break; }
             const uint32_t len = kInfLenBase[sy] + b.get(kInfLenExtra[sy]);
-            const int d = inf_decode(b, dcnt, dsym);
+            const int d = inf_decode<DB>(b, dfast, dcnt, dsym);
             if (d < 0 || d >= 30) { bad = true; break; }
             const uint32_t dist = kInfDistBase[d] + b.get(kInfDistExtra[d]);
             if (b.bad || dist > pos || pos + len > cap) { bad = true; break; }
-            for (uint32_t k = 0; k < len; k++) out[pos + k] = out[pos - dist + k];  // may overlap forward
+            const uint32_t src = (uint32_t)(pos - dist), dst = (uint32_t)pos;
+            uint32_t k = 0;
+            if (dist >= 8)  // 8 independent LDS reads, then the writes
+                for (; k + 8 <= len; k += 8) {
+                    uint8_t t[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) t[j] = win[(src + k + j) & WM];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) win[(dst + k + j) & WM] = t[j];
+                }
+            for (; k < len; k++) win[(dst + k) & WM] = win[(src + k) & WM];  // may overlap forward (dist < len)
             pos += len;
+            if (pos - flushed >= 4096) flush(flushed + 4096);
         }
         if (b.bad) bad = true;
     }
+    if (!bad) flush(pos);
     if (bad || pos != cap) atomicOr(a.err, 2);
 }
 
@@ -845,7 +955,6 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
     const bool decode = lay.compression > 1;
     if (!ensure<uint64_t>(soff, (size_t)ns * 2, err) || !ensure<int>(this->err, 4, err)) return false;
     if (decode && !ensure<uint8_t>(stage, stride * ns, err)) return false;
-    if (lay.compression == 5 && !ensure<uint32_t>(lzwtab, (size_t)ns * 8192, err)) return false;
     HIPCHECK(hipMemcpyAsync(soff.ptr, lay.strip_offsets, sizeof(uint64_t) * ns, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipMemcpyAsync((uint64_t *)soff.ptr + ns, lay.strip_bytes, sizeof(uint64_t) * ns, hipMemcpyHostToDevice,
                             stream));
@@ -863,12 +972,12 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
         ua.stride = stride;
         ua.unit_bytes = tiled ? (uint64_t)unit_h * row_bytes : 0;
         ua.dst = (uint8_t *)stage.ptr;
-        ua.tab = (uint32_t *)lzwtab.ptr;
+        ua.tab = nullptr;
         ua.err = (int *)this->err.ptr;
-        if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
+        if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3(ns), dim3(1), 0, stream, ua);
         else if (lay.compression == 8 || lay.compression == 32946)
-            hipLaunchKernelGGL(k_inflate, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
-        else hipLaunchKernelGGL(k_unpackbits, dim3((ns + 63) / 64), dim3(64), 0, stream, ua);
+            hipLaunchKernelGGL(k_inflate, dim3(ns), dim3(1), 0, stream, ua);
+        else hipLaunchKernelGGL(k_unpackbits, dim3(ns), dim3(64), 0, stream, ua);
         HIPCHECK(hipGetLastError());
         if (lay.predictor == 2) {  // per decoded row of a strip / of a tile
             const int nrows = ns * unit_h;
