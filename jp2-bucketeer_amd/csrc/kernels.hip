@@ -244,46 +244,49 @@ __constant__ uint16_t kInfDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    1
 __constant__ uint8_t kInfDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kInfClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// LSB-first bit reader: up to 64 bits buffered, refilled 32 bits at a time
-// from a word loaded one refill ahead, so the HBM latency of the input
-// overlaps the decoding of the bits already held.
+// LSB-first bit reader over the strip's aligned 32-bit words: a queue of 8
+// words is loaded ahead of the 64-bit buffer, so each word's HBM latency is
+// hidden behind the decoding of the 28 bytes before it.  Words past the
+// stream read as zero (never loaded); `remaining` counts the real bits, and
+// consuming past them sets `bad`.
 struct InfBits {
-    const uint8_t *in;
-    uint64_t n, ip;  // ip: next byte not yet in buf or pf
-    uint64_t buf;
+    const uint32_t *w;
+    uint64_t nw, k, remaining, buf;
     int cnt;
-    uint32_t pf;     // the 4 bytes at ip - 4 .. ip - 1 once pf_ok
-    bool pf_ok, bad;
-    __device__ __forceinline__ uint32_t load4(uint64_t p) const {
-        return in[p] | ((uint32_t)in[p + 1] << 8) | ((uint32_t)in[p + 2] << 16) | ((uint32_t)in[p + 3] << 24);
-    }
-    __device__ __forceinline__ void init(const uint8_t *src, uint64_t len, uint64_t start) {
-        in = src; n = len; ip = start; buf = 0; cnt = 0; bad = false;
-        pf_ok = ip + 4 <= n;
-        if (pf_ok) { pf = load4(ip); ip += 4; }
+    uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
+    bool bad;
+    __device__ __forceinline__ uint32_t ld(uint64_t i) const { return i < nw ? w[i] : 0u; }
+    __device__ __forceinline__ void init(const uint8_t *in, uint64_t n) {
+        const uint64_t addr = (uint64_t)(uintptr_t)in, head = addr & 3;
+        w = (const uint32_t *)(uintptr_t)(addr - head);  // aligned word: same page as a stream byte
+        nw = (head + n + 3) >> 2;
+        buf = (uint64_t)ld(0) >> (8 * head);
+        cnt = 32 - 8 * (int)head;
+        q0 = ld(1); q1 = ld(2); q2 = ld(3); q3 = ld(4); q4 = ld(5); q5 = ld(6); q6 = ld(7); q7 = ld(8);
+        k = 9;
+        remaining = n * 8;
+        bad = false;
     }
     __device__ __forceinline__ void refill() {
         if (cnt > 32) return;
-        if (pf_ok) {
-            buf |= (uint64_t)pf << cnt;
-            cnt += 32;
-            pf_ok = ip + 4 <= n;
-            if (pf_ok) { pf = load4(ip); ip += 4; }
-        } else {
-            while (cnt <= 56 && ip < n) { buf |= (uint64_t)in[ip++] << cnt; cnt += 8; }
-        }
+        buf |= (uint64_t)q0 << cnt;
+        cnt += 32;
+        q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
+        q7 = ld(k++);
     }
-    __device__ __forceinline__ uint32_t peek(int k) { refill(); return (uint32_t)buf & ((1u << k) - 1u); }
-    __device__ __forceinline__ void drop(int k) {
-        if (cnt < k) { bad = true; cnt = 0; buf = 0; return; }
-        buf >>= k; cnt -= k;
+    __device__ __forceinline__ uint32_t peek(int kb) { refill(); return (uint32_t)buf & ((1u << kb) - 1u); }
+    __device__ __forceinline__ void drop(int kb) {
+        if (remaining < (uint64_t)kb) { bad = true; remaining = 0; }
+        else remaining -= kb;
+        buf >>= kb;
+        cnt -= kb;
     }
-    __device__ __forceinline__ uint32_t get(int k) {  // k <= 16
-        const uint32_t v = peek(k);
-        drop(k);
+    __device__ __forceinline__ uint32_t get(int kb) {  // kb <= 16
+        const uint32_t v = peek(kb);
+        drop(kb);
         return v;
     }
-    __device__ __forceinline__ void align() { drop(cnt & 7); }
+    __device__ __forceinline__ void align() { refill(); drop((int)(remaining & 7)); }  // to the next byte
 };
 
 // Canonical Huffman table: 16 per-length counts, the symbols in code order,
@@ -356,9 +359,16 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
     constexpr uint32_t WM = 32767;
     __shared__ uint16_t lcnt[16], lsym[288], dcnt[16], dsym[32], lfast[1 << LB], dfast[1 << DB];
     __shared__ uint8_t lens[320];
+    __shared__ uint16_t lbase[29], dbase[30];
+    __shared__ uint8_t lextra[29], dextra[30];
     __shared__ __attribute__((aligned(16))) uint8_t win[WM + 1];
     const int s = blockIdx.x;
     if (s >= a.nstrips || threadIdx.x) return;
+    for (int i = 0; i < 30; i++) {  // per-match lookups from LDS, not the constant bank
+        if (i < 29) { lbase[i] = kInfLenBase[i]; lextra[i] = kInfLenExtra[i]; }
+        dbase[i] = kInfDistBase[i];
+        dextra[i] = kInfDistExtra[i];
+    }
     const uint8_t *in = a.src + a.off[s];
     const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
@@ -370,7 +380,8 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
     };
     bool bad = n < 2 || (in[0] & 15) != 8 || (in[0] >> 4) > 7 || ((in[0] << 8) | in[1]) % 31 || (in[1] & 0x20);
     InfBits b;
-    b.init(in, n, 2);
+    b.init(in, n);
+    b.get(16);  // zlib CMF, FLG (checked above)
     bool last = false;
     while (!bad && !last) {
         last = b.get(1);
@@ -431,10 +442,10 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
             if (sy == 256) break;
             sy -= 257;
             if (sy >= 29) { bad = true; break; }
-            const uint32_t len = kInfLenBase[sy] + b.get(kInfLenExtra[sy]);
+            const uint32_t len = lbase[sy] + b.get(lextra[sy]);
             const int d = inf_decode<DB>(b, dfast, dcnt, dsym);
             if (d < 0 || d >= 30) { bad = true; break; }
-            const uint32_t dist = kInfDistBase[d] + b.get(kInfDistExtra[d]);
+            const uint32_t dist = dbase[d] + b.get(dextra[d]);
             if (b.bad || dist > pos || pos + len > cap) { bad = true; break; }
             const uint32_t src = (uint32_t)(pos - dist), dst = (uint32_t)pos;
             uint32_t k = 0;

@@ -1,0 +1,73 @@
+// Host build of k_inflate (kernels.hip), for the CPU test suite: the kernel's
+// text is spliced in by tests/test_inflate_host.py between this file's shims
+// and main(), compiled with clang++ -fsanitize=address, and run on zlib
+// streams (levels 0/1/6/9 at every byte alignment) and damaged streams.
+// [[SHIMS]]
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+#include <zlib.h>
+#define __device__
+#define __forceinline__ inline
+#define __global__
+#define __launch_bounds__(x)
+#define __shared__ static
+#define __constant__ static const
+struct uint4 { uint32_t x, y, z, w; };
+static struct { int x; } blockIdx, threadIdx;
+static inline int atomicOr(int *p, int v) { int o = *p; *p |= v; return o; }
+using std::min;
+// [[MAIN]]
+using namespace jp2hip;
+
+static int run(const std::vector<uint8_t> &z, int off, const std::vector<uint8_t> &raw) {
+    std::vector<uint8_t> buf(z.size() + 16, 0xA5);
+    std::memcpy(buf.data() + off, z.data(), z.size());
+    std::vector<uint8_t> out(raw.size() + 256);
+    uint64_t o = off, c = z.size();
+    int err = 0;
+    UnpackArgs a{};
+    a.src = buf.data(); a.off = &o; a.cnt = &c; a.nstrips = 1;
+    a.unit_bytes = raw.size(); a.stride = raw.size() + 256; a.dst = out.data(); a.err = &err;
+    blockIdx.x = 0; threadIdx.x = 0;
+    k_inflate(a);
+    if (err) return 1;
+    return std::memcmp(out.data(), raw.data(), raw.size()) ? 2 : 0;
+}
+
+int main() {
+    std::vector<uint8_t> raw(300000);
+    uint32_t r = 1;
+    for (size_t i = 0; i < raw.size(); i++) {
+        r = r * 1103515245u + 12345u;
+        raw[i] = (uint8_t)((i / 7) % 50 + ((r >> 16) & 7));
+    }
+    int fails = 0;
+    for (int lvl : {0, 1, 6, 9}) {
+        uLongf cl = compressBound(raw.size());
+        std::vector<uint8_t> z(cl);
+        compress2(z.data(), &cl, raw.data(), raw.size(), lvl);
+        z.resize(cl);
+        for (int off = 0; off < 4; off++) {
+            const int rc = run(z, off, raw);
+            printf("level %d offset %d -> %d\n", lvl, off, rc);
+            fails += rc != 0;
+        }
+        std::vector<uint8_t> t(z.begin(), z.begin() + z.size() / 2);  // truncated: must fail
+        const int rt = run(t, 1, raw);
+        printf("level %d truncated -> %d\n", lvl, rt);
+        fails += rt != 1;
+    }
+    uLongf cl = compressBound(raw.size());
+    std::vector<uint8_t> z(cl);
+    compress2(z.data(), &cl, raw.data(), raw.size(), 6);
+    z.resize(cl);
+    z[2] = 0x07;  // BFINAL 1, BTYPE 3 (reserved)
+    const int rb = run(z, 0, raw);
+    printf("reserved block -> %d\n", rb);
+    fails += rb != 1;
+    printf("%s\n", fails ? "FAIL" : "OK");
+    return fails ? 1 : 0;
+}
