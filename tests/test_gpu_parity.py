@@ -205,6 +205,17 @@ def test_corrupt_compressed_strip_fails_loudly(encoder):
         encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
 
 
+def test_corrupt_lzw_strip_fails_loudly(encoder):
+    """An LZW strip whose first code (511) is past the table end fails."""
+    img = im.synth_rgb8(64, 64, seed=1)
+    data = bytearray(im.tiff_bytes_compressed(img, "tiff_lzw", rows_per_strip=32))
+    lay, keep = jp2hip.tiff_layout(bytes(data))
+    o, n = lay.strip_offsets[1], lay.strip_bytes[1]
+    data[o:o + n] = b"\xff" * n
+    with pytest.raises(jp2hip.Jp2hipError, match="corrupt"):
+        encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
+
+
 @pytest.mark.parametrize("damage", ["header", "truncate", "bad_block"])
 def test_corrupt_deflate_strip_fails_loudly(encoder, damage):
     """A bad zlib header, a strip cut short, or a reserved block type (3) all
