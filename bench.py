@@ -312,7 +312,7 @@ def c5_band(rank, world, threads=16):
     from jp2hip import split as js
     from jp2hip._lib import Layout
     w, h, rps = C5["w"], C5["h"], C5["rps"]
-    r0, r1 = js.split_rows(h, C5["tile"], rank, world)
+    r0, r1 = js.split_rows(h, C5["tile"], rank, world, 1024)
     buf = np.empty((r1 - r0, w), "<u2")
     groups = list(range(r0, r1, C5["tile"]))
 

@@ -71,11 +71,18 @@ typedef struct jp2hip_recipe {
     double qstep;            /* irreversible base step (Kakadu Qstep=1/256)    */
     double rate_bpp;         /* "-rate 3"; <= 0 means "-rate -" (all passes)   */
     int32_t format;          /* JP2HIP_FORMAT_*                                */
-    int32_t comment;         /* emit a COM marker                              */
+    int32_t comment;         /* emit Kakadu-style COM markers: a version       */
+                             /* string and "Kdu-Layer-Info" (layer slopes and  */
+                             /* bytes, test.jpx's second COM)                  */
     int32_t slope_skip;      /* rate-driven (rate_bpp > 0) only: do not code   */
                              /* bit-planes whose predicted slope lies far      */
                              /* below the rate target's, as kdu_compress's     */
                              /* block coder does under "-rate"; 0 = code all   */
+    int32_t flush_period;    /* -flush_period 1024 (KakaduConverter.java:40):  */
+                             /* tile-parts go out per stripe of tile rows that */
+                             /* completes a flush -- resolution 0 of every     */
+                             /* tile in the stripe, then resolution 1, ...     */
+                             /* (test.jpx's order); <= 0: tile after tile      */
 } jp2hip_recipe;
 
 /* Where the samples live inside a source buffer (a baseline TIFF's strips). */
@@ -126,6 +133,10 @@ const char *jp2hip_last_error(void);
 /* 1 if a gfx950 device is usable (ConverterFactory.checkSystemKakadu analogue). */
 int jp2hip_probe(void);
 
+/* Number of visible HIP devices that are gfx950 (0 if none): how many GPUs a
+ * converter spreads its contexts over (device ordinals 0..n-1). */
+int jp2hip_device_count(void);
+
 /* Fill the Bucketeer recipe for JP2HIP_LOSSY / JP2HIP_LOSSLESS. */
 void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion);
 
@@ -138,7 +149,9 @@ void jp2hip_destroy(jp2hip_ctx *ctx);
 int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path_utf8, const char *out_path_utf8,
                        int conversion, const jp2hip_recipe *recipe, jp2hip_stats *stats);
 
-/* TIFF bytes in host memory -> encoded bytes (*out malloc'd; jp2hip_free). */
+/* TIFF bytes in host memory -> encoded bytes.  *out is pinned host memory
+ * (the code-stream is copied straight into it from HBM); release it with
+ * jp2hip_free, never free(). */
 int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int conversion,
                        const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
                        jp2hip_stats *stats);
@@ -162,6 +175,8 @@ int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len,
                          const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
                          jp2hip_stats *stats);
 
+/* Releases an *out buffer of the encode calls (returned to a small pool of
+ * pinned buffers, so steady-state encodes pin nothing new). */
 void jp2hip_free(void *p);
 
 /* ------------------------------------------------------------------------
@@ -187,9 +202,11 @@ typedef struct jp2hip_split {
     void *user;
 } jp2hip_split;
 
-/* Image rows [*row0, *row1) whose tiles rank `rank` encodes. */
-void jp2hip_split_rows(int32_t height, int32_t tile_h, int32_t rank, int32_t world, int32_t *row0,
-                       int32_t *row1);
+/* Image rows [*row0, *row1) whose tiles rank `rank` encodes: whole
+ * -flush_period stripes of tile rows (recipe.flush_period), so every rank's
+ * tile-parts are one contiguous run of the file. */
+void jp2hip_split_rows(int32_t height, int32_t tile_h, int32_t flush_period, int32_t rank, int32_t world,
+                       int32_t *row0, int32_t *row1);
 
 /* This rank's part of the file: *out (jp2hip_free) goes at byte *file_offset
  * of a *file_len-byte file.  Rank 0's part starts with the file and main

@@ -14,8 +14,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -30,7 +32,6 @@ struct jp2hip_ctx {
     jp2hip::GpuEncoder gpu;
     jp2hip_config cfg;
     int threads = 1;
-    jp2hip::T2State t2;  // tier-2 arenas, reused call to call
 };
 
 namespace {
@@ -40,6 +41,70 @@ thread_local std::string g_err;
 int fail(const std::string &msg) {
     g_err = msg;
     return -1;
+}
+
+// Encoded files are returned in pinned host memory: the final code-stream D2H
+// lands in the caller's buffer directly (no staging copy; a C3 file is
+// ~340 MB) and jp2hip_free() hands the buffer back to a small pool, so steady
+// state allocates and pins nothing.  jp2hip_free() of a pointer the pool does
+// not know is plain free().
+struct PinnedPool {
+    std::mutex mu;
+    std::unordered_map<void *, size_t> live;   // handed out: capacity
+    std::multimap<size_t, void *> idle;        // returned: capacity -> buffer
+    size_t idle_bytes = 0;
+    static constexpr size_t kIdleCap = (size_t)4 << 30;
+};
+PinnedPool &pinned_pool() {
+    static PinnedPool *p = new PinnedPool();  // never destroyed: buffers may be freed at exit
+    return *p;
+}
+
+uint8_t *out_alloc(size_t n) {
+    PinnedPool &P = pinned_pool();
+    n = std::max<size_t>(n, 1);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        auto it = P.idle.lower_bound(n);
+        if (it != P.idle.end() && it->first <= 2 * n + ((size_t)1 << 20)) {
+            void *b = it->second;
+            P.live[b] = it->first;
+            P.idle_bytes -= it->first;
+            P.idle.erase(it);
+            return (uint8_t *)b;
+        }
+    }
+    const size_t cap = n + n / 8 + 4096;  // room for a slightly larger file next time
+    void *b = nullptr;
+    if (hipHostMalloc(&b, cap, hipHostMallocDefault) != hipSuccess || !b) return nullptr;
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.live[b] = cap;
+    return (uint8_t *)b;
+}
+
+void out_free(void *p) {
+    if (!p) return;
+    PinnedPool &P = pinned_pool();
+    std::vector<void *> drop;
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        auto it = P.live.find(p);
+        if (it == P.live.end()) {
+            std::free(p);
+            return;
+        }
+        const size_t cap = it->second;
+        P.live.erase(it);
+        P.idle.emplace(cap, p);
+        P.idle_bytes += cap;
+        while (P.idle_bytes > PinnedPool::kIdleCap && !P.idle.empty()) {  // largest first
+            auto last = std::prev(P.idle.end());
+            P.idle_bytes -= last->first;
+            drop.push_back(last->second);
+            P.idle.erase(last);
+        }
+    }
+    for (void *b : drop) (void)hipHostFree(b);
 }
 
 double now_ms() {
@@ -98,6 +163,7 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     if (ifd + ifd_hdr > len || ifd + ifd_hdr < ifd) return fail("tiff: IFD offset out of range");
     const uint64_t ne = t.big ? t.u64(ifd) : t.u16(ifd);
     uint32_t w = 0, h = 0, spp = 1, bps = 8, comp = 1, planar = 1, rps = 0xFFFFFFFFu, fmt = 1, pred = 1;
+    uint32_t photo = 0xFFFFFFFFu;  // absent: inferred from SamplesPerPixel
     size_t e_off = 0, e_cnt = 0;
     uint32_t n_off = 0, tw = 0, th = 0;
     if (ne > (len - ifd - ifd_hdr) / t.entry_size()) return fail("tiff: truncated IFD");
@@ -108,6 +174,7 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
         case 257: h = (uint32_t)t.val(e, 0); break;
         case 258: bps = (uint32_t)t.val(e, 0); break;
         case 259: comp = (uint32_t)t.val(e, 0); break;
+        case 262: photo = (uint32_t)t.val(e, 0); break;
         case 273: e_off = e; n_off = (uint32_t)std::min<uint64_t>(t.count(e), 0xFFFFFFFFu); break;
         case 277: spp = (uint32_t)t.val(e, 0); break;
         case 278: rps = (uint32_t)std::min<uint64_t>(t.val(e, 0), 0xFFFFFFFFu); break;
@@ -139,6 +206,16 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
     if (fmt != 1) return fail("tiff: only unsigned integer samples are supported");
     if (spp < 1 || spp > 4) return fail("tiff: " + std::to_string(spp) + " samples/pixel is not supported");
     if (planar != 1 && planar != 2) return fail("tiff: bad PlanarConfiguration");
+    // PhotometricInterpretation: BlackIsZero gray (+ alpha) or RGB (+ alpha);
+    // the colour transform assumes RGB in components 0..2
+    if (photo == 0xFFFFFFFFu) photo = spp >= 3 ? 2 : 1;
+    if (photo == 0) return fail("tiff: PhotometricInterpretation 0 (WhiteIsZero) is not supported");
+    if (photo != 1 && photo != 2)
+        return fail("tiff: PhotometricInterpretation " + std::to_string(photo) +
+                    " is not supported (BlackIsZero gray or RGB only)");
+    if (photo == 2 && spp < 3) return fail("tiff: RGB needs 3 or 4 samples/pixel");
+    if (photo == 1 && spp > 2) return fail("tiff: BlackIsZero with more than 2 samples/pixel is not supported");
+    if (rps == 0 && !tiled) rps = h;  // RowsPerStrip 0 is invalid; libtiff reads it as one strip
     if (rps > h) rps = h;
     if (tiled) rps = th;  // per-unit rows (tiles are never clipped)
     const uint32_t across = tiled ? (w + tw - 1) / tw : 1;
@@ -154,13 +231,14 @@ int parse_tiff(const uint8_t *buf, size_t len, jp2hip_layout *lay, std::vector<u
         uint32_t rows = std::min(rps, h - y0);
         if (packed) {
             const uint64_t nb = t.val(e_cnt, s);
-            if (offs[s] + nb > len) return fail("tiff: strip " + std::to_string(s) + " out of range");
+            if (offs[s] > len || nb > len - offs[s]) return fail("tiff: strip " + std::to_string(s) + " out of range");
             const uint64_t unit = (uint64_t)tw * (planar == 2 ? 1 : spp) * (bps / 8) * th;
             if (tiled && comp == 1 && nb < unit) return fail("tiff: tile byte count too small");
             offs[need + s] = nb;
             continue;
         }
-        if (offs[s] + row * rows > len) return fail("tiff: strip " + std::to_string(s) + " out of range");
+        if (offs[s] > len || (uint64_t)row * rows > len - offs[s])
+            return fail("tiff: strip " + std::to_string(s) + " out of range");
         if (e_cnt && t.val(e_cnt, s) < row * rows) return fail("tiff: strip byte count too small");
     }
     lay->width = (int32_t)w;
@@ -201,6 +279,7 @@ void default_recipe(jp2hip_recipe *r, int conversion) {
     r->format = JP2HIP_FORMAT_JPX;
     r->comment = 1;
     r->slope_skip = 1;
+    r->flush_period = 1024;
 }
 
 // Slope prediction's rate target (bytes; 0 = prediction off) -- the same
@@ -210,15 +289,56 @@ int64_t skip_target_of(const jp2hip_recipe &rc, int w, int h) {
     return (int64_t)std::floor(rc.rate_bpp * (double)w * (double)h / 8.0);
 }
 
-// Safety net of the prediction (oracle predict_and_code): planes were
-// skipped, yet all coded bytes together stay below the target.
-void undershoot_terms(const jp2hip::GpuEncoder &g, int64_t &coded, int64_t &skipped) {
-    coded = 0;
-    skipped = 0;
-    const std::vector<int32_t> &len = g.block_lengths();
-    const std::vector<uint8_t> &pm = g.block_pmin();
-    for (size_t b = 0; b < len.size(); b++) coded += len[b];
-    for (size_t b = 0; b < pm.size(); b++) skipped |= pm[b] > 0;
+// A caller-supplied layout (jp2hip_encode_device*) is checked against the
+// source buffer before any kernel reads it: the strips that rows [row0, row1)
+// touch must lie inside src_len (uncompressed), tiles must hold a whole tile
+// (uncompressed tiled), and compressed strips are checked in
+// unpack_if_compressed.
+bool validate_layout(const jp2hip_layout *lay, size_t src_len, int row0, int row1, std::string &err) {
+    if (lay->width <= 0 || lay->height <= 0 || lay->components < 1 || lay->components > 4 ||
+        (lay->bits != 8 && lay->bits != 16) || (lay->planar != 1 && lay->planar != 2) || lay->rows_per_strip <= 0 ||
+        lay->nstrips <= 0 || !lay->strip_offsets) {
+        err = "layout: bad geometry or strip table";
+        return false;
+    }
+    const uint64_t spp_row = lay->planar == 2 ? 1 : (uint64_t)lay->components;
+    const uint64_t px = spp_row * (uint64_t)(lay->bits / 8);
+    const int planes = lay->planar == 2 ? lay->components : 1;
+    if (lay->tile_width > 0 || lay->tile_height > 0) {
+        if (lay->tile_width <= 0 || lay->tile_height <= 0 || !lay->strip_bytes) {
+            err = "layout: tiles need tile_width, tile_height and strip_bytes";
+            return false;
+        }
+        const int64_t across = (lay->width + lay->tile_width - 1) / lay->tile_width;
+        const int64_t need = across * ((lay->height + lay->tile_height - 1) / lay->tile_height) * planes;
+        if (need > lay->nstrips) { err = "layout: too few tiles"; return false; }
+        const uint64_t unit = (uint64_t)lay->tile_width * lay->tile_height * px;
+        for (int64_t i = 0; i < need; i++) {
+            const uint64_t o = lay->strip_offsets[i], n = lay->strip_bytes[i];
+            if (o > src_len || n > src_len - o || (lay->compression <= 1 && n < unit)) {
+                err = "layout: tile " + std::to_string(i) + " lies outside the source buffer or is short";
+                return false;
+            }
+        }
+        return true;
+    }
+    if (lay->compression > 1) return true;  // checked with the strip byte counts in unpack_if_compressed
+    const int64_t per_plane = (lay->height + (int64_t)lay->rows_per_strip - 1) / lay->rows_per_strip;
+    if (per_plane * planes > lay->nstrips) { err = "layout: too few strips"; return false; }
+    const uint64_t row_bytes = (uint64_t)lay->width * px;
+    const int64_t s0 = std::max(0, row0) / lay->rows_per_strip;
+    const int64_t s1 = std::min<int64_t>(per_plane, ((int64_t)std::min(row1, lay->height) + lay->rows_per_strip - 1) /
+                                                        lay->rows_per_strip);
+    for (int p = 0; p < planes; p++)
+        for (int64_t s = s0; s < s1; s++) {
+            const uint64_t o = lay->strip_offsets[(size_t)(p * per_plane + s)];
+            const uint64_t rows = (uint64_t)std::min<int64_t>(lay->rows_per_strip, lay->height - s * lay->rows_per_strip);
+            if (o > src_len || rows * row_bytes > src_len - o) {
+                err = "layout: strip " + std::to_string(p * per_plane + s) + " lies outside the source buffer";
+                return false;
+            }
+        }
+    return true;
 }
 
 // LZW / Deflate / PackBits strips are decoded on the GPU into the context's staging
@@ -248,8 +368,44 @@ bool unpack_if_compressed(jp2hip_ctx *ctx, const void *&d_src, size_t src_len, c
     return true;
 }
 
+// Kdu-Layer-Info byte counts: the code-stream through each layer.
+void layer_end_of(const jp2hip::Plan &P, int64_t tp_hdr_bytes, const int64_t *layer_bytes, int64_t *layer_end) {
+    std::vector<uint8_t> mh;
+    jp2hip::main_header(P, mh, nullptr, nullptr);
+    int64_t acc = (int64_t)mh.size() + tp_hdr_bytes;
+    for (int l = 0; l < P.rc.layers; l++) {
+        acc += layer_bytes[l];
+        layer_end[l] = acc;
+    }
+}
+
+void fill_stats(jp2hip_stats *stats, const jp2hip::StageTimes &st, double t_start, double h2d_ms, int64_t nb,
+                const jp2hip::T2Summary &sum, int64_t out_bytes, int iters) {
+    if (!stats) return;
+    std::memset(stats, 0, sizeof *stats);
+    stats->total_ms = now_ms() - t_start;
+    stats->h2d_ms = h2d_ms;
+    stats->ingest_ms = st.ingest;
+    stats->dwt_ms = st.dwt;
+    stats->quant_ms = st.quant;
+    stats->t1_ms = st.t1_cm + st.t1_mq;
+    stats->t1_cm_ms = st.t1_cm;
+    stats->t1_mq_ms = st.t1_mq;
+    stats->pcrd_ms = st.pcrd;
+    stats->d2h_ms = st.d2h;
+    stats->t2_ms = st.t2;
+    stats->codeblocks = nb;
+    stats->t1_bytes = sum.t1_bytes;
+    stats->coded_passes = sum.coded_passes;
+    stats->out_bytes = out_bytes;
+    stats->rate_iterations = iters;
+}
+
 // The whole encode with the source already in device memory.  On success
-// *out is a malloc'd buffer holding the complete file.
+// *out is a malloc'd buffer holding the complete file.  Everything up to the
+// code-stream bytes runs on the GPU (tier-2 included, t2_device.hip); the host picks
+// the rate-control budgets from one small summary per pass and writes the
+// file and main headers.
 int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *lay,
                 int conversion, const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
                 jp2hip_stats *stats, double t_start, double h2d_ms) {
@@ -264,118 +420,89 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     std::string err;
     jp2hip_layout ulay;
     std::vector<uint64_t> uoffs;
+    if (!validate_layout(lay, src_len, 0, lay->height, err)) return fail(err);
     if (!unpack_if_compressed(ctx, d_src, src_len, lay, ulay, uoffs, err)) return fail(err);
     if (!build_plan(plan, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     const bool prof = ctx->cfg.profile != 0;
     StageTimes st;
-    const int64_t skip_target = skip_target_of(rc, plan.w, plan.h);
+    int64_t skip_target = skip_target_of(rc, plan.w, plan.h);
     if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, skip_target)) return fail(err);
-    if (skip_target > 0) {
-        int64_t coded, skipped;
-        undershoot_terms(ctx->gpu, coded, skipped);
-        if (skipped && coded < skip_target && !ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, 0))
-            return fail(err);
-    }
-    const int nb = (int)plan.blocks.size();
+    T2Tables tabs;
+    t2_tables(plan, 0, plan.ntx * plan.nty, 0, tabs);
+    if (!ctx->gpu.t2_load(plan, tabs, err)) return fail(err);
     const int L = rc.layers;
-    const std::vector<int32_t> &len = ctx->gpu.block_lengths();
-    std::vector<uint8_t> h_nl;
-    std::vector<int32_t> h_lrate;
-    std::vector<int64_t> budgets((size_t)L, 0);
-    T2Input in;
-    in.plan = &plan;
-    in.P = ctx->gpu.block_planes().data();
-    in.data = nullptr;
-    in.data_off = nullptr;
-    in.threads = ctx->threads;
-    T2State &t2 = ctx->t2;
-    double t2ms = 0;
+    std::vector<uint8_t> mh;
+    main_header(plan, mh, nullptr, nullptr);
+    T2Summary sum;
+    std::memset(&sum, 0, sizeof sum);
     int iters = 0;
     int64_t cs_bytes = 0;
     if (rc.rate_bpp <= 0.0) {
         // lossless: layer l keeps every pass whose slope clears total >> (L-1-l)
-        int64_t total = 0;
-        for (int b = 0; b < nb; b++) total += len[b];
-        for (int l = 0; l < L; l++) budgets[l] = total >> (L - 1 - l);
-        if (!ctx->gpu.select(plan, budgets, h_nl, h_lrate, prof, st, err)) return fail(err);
+        if (!ctx->gpu.select_lossless(plan, err) || !ctx->gpu.t2_size(plan, true, prof, st, sum, err))
+            return fail(err);
+        if (sum.err) return fail("tier-1 output capacity exceeded");
         iters = 1;
-        in.nl = h_nl.data();
-        in.lrate = h_lrate.data();
-        const double t0 = now_ms();
-        cs_bytes = t2_headers(in, t2);
-        t2ms += now_ms() - t0;
+        cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
     } else {
         const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
         int64_t budget = target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
+        std::vector<int64_t> budgets((size_t)L, 0);
         for (int it = 0; it < 8; it++) {
             if (budget < 0) budget = 0;
             for (int l = 0; l < L; l++) budgets[l] = budget >> (L - 1 - l);
-            if (!ctx->gpu.select(plan, budgets, h_nl, h_lrate, prof, st, err)) return fail(err);
+            if (!ctx->gpu.select(plan, budgets, err) || !ctx->gpu.t2_size(plan, true, prof, st, sum, err))
+                return fail(err);
+            if (sum.err) return fail("tier-1 output capacity exceeded");
+            if (it == 0 && skip_target > 0 && sum.skipped && sum.t1_bytes < skip_target) {
+                // slope prediction's safety net (oracle predict_and_code):
+                // planes were skipped, yet every coded byte fits -> code all
+                skip_target = 0;
+                if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, 0)) return fail(err);
+                it = -1;
+                budget = target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
+                iters = 0;
+                continue;
+            }
             iters++;
-            in.nl = h_nl.data();
-            in.lrate = h_lrate.data();
-            const double t0 = now_ms();
-            cs_bytes = t2_headers(in, t2);
-            t2ms += now_ms() - t0;
+            cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
             if (cs_bytes <= target) break;
             // exponential back-off + 1/16 of the overshoot + 64 B, as the oracle
             budget -= ((cs_bytes - target) << it) + ((cs_bytes - target) >> 4) + 64;
         }
     }
-    // t2 now describes the final layer table; fetch the bytes it includes
-    std::vector<int32_t> final_len((size_t)nb);
-    std::vector<uint64_t> offs((size_t)nb);
-    uint64_t total = 0;
-    for (int b = 0; b < nb; b++) {
-        final_len[b] = h_lrate[(size_t)b * L + (L - 1)];
-        offs[b] = total;
-        total += (uint64_t)final_len[b];
-    }
-    const uint8_t *data = nullptr;
-    const double tg = now_ms();
-    if (!ctx->gpu.gather(plan, final_len, offs, total, &data, prof, st, err)) return fail(err);
-    const double gather_ms = now_ms() - tg;
-    in.data = data;
-    in.data_off = offs.data();
-    const double t0 = now_ms();
+    // Kdu-Layer-Info: the final selection's slope keys (lossless: the last
+    // layer takes every pass) and the code-stream bytes through each layer
+    std::vector<uint64_t> K(sum.kc, sum.kc + L);
+    if (rc.rate_bpp <= 0.0) K[L - 1] = 0;
+    std::vector<int64_t> layer_end((size_t)L);
+    layer_end_of(plan, sum.tp_hdr_bytes, sum.layer_bytes, layer_end.data());
+    main_header(plan, mh, K.data(), layer_end.data());
     const size_t fh = file_header_bytes(plan);
     const size_t n = fh + (size_t)cs_bytes;
-    uint8_t *buf = (uint8_t *)std::malloc(n);
-    if (!buf) return fail("out of memory");
+    uint8_t *buf = out_alloc(n);
+    if (!buf) return fail("out of (pinned) host memory");
     write_file_header(plan, (uint64_t)cs_bytes, buf);
-    t2_emit(in, t2, buf + fh);
-    t2ms += now_ms() - t0;
+    std::memcpy(buf + fh, mh.data(), mh.size());
+    if (!ctx->gpu.t2_emit(plan, 0, (uint64_t)sum.part_bytes, buf + fh + mh.size(), prof, st, err) ||
+        !ctx->gpu.collect_profile(st, err)) {
+        out_free(buf);
+        return fail(err);
+    }
+    buf[n - 2] = 0xFF;
+    buf[n - 1] = 0xD9;
     *out = buf;
     *out_len = n;
-    if (stats) {
-        std::memset(stats, 0, sizeof *stats);
-        stats->total_ms = now_ms() - t_start;
-        stats->h2d_ms = h2d_ms;
-        stats->ingest_ms = st.ingest;
-        stats->dwt_ms = st.dwt;
-        stats->quant_ms = st.quant;
-        stats->t1_ms = st.t1_cm + st.t1_mq;
-        stats->t1_cm_ms = st.t1_cm;
-        stats->t1_mq_ms = st.t1_mq;
-        stats->pcrd_ms = st.pcrd;
-        stats->d2h_ms = prof ? st.d2h : gather_ms;
-        stats->t2_ms = t2ms;
-        stats->codeblocks = nb;
-        int64_t tb = 0, tp = 0;
-        ctx->gpu.t1_total_bytes(tb, tp);
-        stats->t1_bytes = tb;
-        stats->coded_passes = tp;
-        stats->out_bytes = (int64_t)n;
-        stats->rate_iterations = iters;
-    }
+    fill_stats(stats, st, t_start, h2d_ms, (int64_t)plan.blocks.size(), sum, (int64_t)n, iters);
     return 0;
 }
 
 // Tile-split encode (jp2hip.h, jp2hip_encode_device_split; split.cpp has the
-// exchange rule).  Rank `rank` runs the device pipeline on its band of tile
-// rows only; budgets, thresholds and tier-2 sizes are agreed through
-// sp->allreduce_sum so the parts concatenate to the single-GPU file.
-int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *lay, int conversion,
+// exchange rule).  Rank `rank` runs the device pipeline -- tier-2 included --
+// on its band of tile rows only; budgets, thresholds and tier-2 sizes are
+// agreed through sp->allreduce_sum so the parts concatenate to the
+// single-GPU file.
+int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip_layout *lay, int conversion,
                       const jp2hip_recipe *recipe, const jp2hip_split *sp, uint8_t **out, size_t *out_len,
                       uint64_t *file_offset, uint64_t *file_len, jp2hip_stats *stats, double t_start) {
     using namespace jp2hip;
@@ -398,18 +525,21 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
         return fail("split: compressed or tiled TIFFs are not supported; rewrite as uncompressed strips first");
     if (!build_plan(full, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     int tr0, tr1;
-    split_tile_rows(full.nty, rank, world, tr0, tr1);
+    split_tile_rows(full.nty, rc.tile_h, full.h, rc.flush_period, rank, world, tr0, tr1);
     Plan sub;
     make_subplan(full, tr0, tr1, sub);
     const bool have = sub.ntc > 0;
+    // only this rank's rows are read, so only their strips must be in d_src
+    // (a rank that fails here still joins every exchange below)
+    bool ok = !have || validate_layout(lay, src_len, sub.row0, sub.row0 + sub.band_h, err);
     const bool prof = ctx->cfg.profile != 0;
     StageTimes st;
     std::vector<uint64_t> keys;
     std::vector<int64_t> cum;
     // slope prediction over the whole image: the plane histogram is summed
-    // over ranks (one all-reduce of kSlopeBins + 1 int64, the last entry a
-    // failure flag, so a rank that failed earlier still joins the exchange)
-    const int64_t skip_target = skip_target_of(rc, full.w, full.h);
+    // over ranks (one all-reduce of kSlopeBins + 1 int64, the last a failure
+    // flag, so a rank that failed earlier still joins the exchange)
+    int64_t skip_target = skip_target_of(rc, full.w, full.h);
     bool hist_done = false;
     GpuEncoder::HistReduce reduce = [&](std::vector<int64_t> &h) {
         hist_done = true;
@@ -419,50 +549,31 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
         std::copy(v.begin(), v.end() - 1, h.begin());
         return true;
     };
-    bool ok = !have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, skip_target, &reduce);
+    ok = ok && (!have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, skip_target, &reduce));
     if (skip_target > 0 && !hist_done) {  // no blocks here, or failed before the exchange
         std::vector<int64_t> v((size_t)kSlopeBins + 1, 0);
         v.back() = ok ? 0 : 1;
         if (!allreduce(v.data(), (int)v.size())) return fail("split: all-reduce failed");
         if (ok && v.back()) { ok = false; err = "split: another rank failed"; }
     }
-    if (skip_target > 0) {  // the prediction's safety net, decided globally
-        int64_t v[3] = {0, 0, ok ? 0 : 1};
-        if (ok && have) undershoot_terms(ctx->gpu, v[0], v[1]);
-        if (!allreduce(v, 3)) return fail("split: all-reduce failed");
-        if (ok && v[2]) { ok = false; err = "split: another rank failed"; }
-        if (ok && v[1] && v[0] < skip_target && have)
-            ok = ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, 0);
-    }
-    ok = ok && (!have || ctx->gpu.segments(keys, cum, err));
-    {
-        int64_t flag = ok ? 0 : 1;
-        if (!allreduce(&flag, 1)) return fail("split: all-reduce failed");
-        if (!ok) return fail(err);
-        if (flag) return fail("split: another rank failed");
+    T2Tables tabs;
+    const int tile0 = sub.tile0, tile1 = sub.tile0 + full.ntx * (tr1 - tr0);
+    if (ok && have) {
+        t2_tables(full, tile0, tile1, sub.block0, tabs);
+        ok = ctx->gpu.t2_load(sub, tabs, err);
     }
     const int L = rc.layers;
-    const size_t nbf = full.blocks.size(), nbl = sub.blocks.size(), b0 = (size_t)sub.block0;
-    std::vector<uint8_t> P_full(nbf, 0), nl_full(nbf * L, 0), h_nl;
-    std::vector<int32_t> lrate_full(nbf * L, 0), h_lrate;
-    if (have) std::copy(ctx->gpu.block_planes().begin(), ctx->gpu.block_planes().begin() + nbl, P_full.begin() + b0);
-    T2Input in;
-    in.plan = &full;
-    in.P = P_full.data();
-    in.nl = nl_full.data();
-    in.lrate = lrate_full.data();
-    in.data = nullptr;
-    in.data_off = nullptr;
-    in.threads = ctx->threads;
-    in.tile0 = sub.tile0;
-    in.tile1 = sub.tile0 + full.ntx * (tr1 - tr0);
-    T2State &t2 = ctx->t2;
     std::vector<int64_t> budgets((size_t)L, 0);
     std::vector<uint64_t> K((size_t)L);
-    double t2ms = 0;
     int iters = 0;
     int64_t cs_bytes = 0;
-    // one selection + header pass for `budgets`; returns false on failure
+    T2Summary sum;
+    std::memset(&sum, 0, sizeof sum);
+    int64_t g_tp_hdr = 0;                          // whole-image sums of the last pass
+    std::vector<int64_t> g_layer((size_t)L, 0);    // (Kdu-Layer-Info)
+    std::vector<uint8_t> mh;
+    main_header(full, mh, nullptr, nullptr);
+    // one selection + tier-2 sizing pass for `budgets`; false on failure
     auto round = [&]() -> bool {
         if (jp2hip_split_thresholds(keys.data(), cum.data(), (int64_t)keys.size(), budgets.data(), L, sp,
                                     K.data()) != 0) {
@@ -470,103 +581,107 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, const jp2hip_layout *l
             return false;
         }
         bool rok = true;
-        if (have) {
-            rok = ctx->gpu.select_keys(sub, K, h_nl, h_lrate, prof, st, err);
-            if (rok) {
-                std::copy(h_nl.begin(), h_nl.end(), nl_full.begin() + b0 * L);
-                std::copy(h_lrate.begin(), h_lrate.end(), lrate_full.begin() + b0 * L);
-            }
+        if (have) rok = ctx->gpu.select_keys(sub, K, err) && ctx->gpu.t2_size(sub, false, prof, st, sum, err);
+        if (rok && have && sum.err) { rok = false; err = "tier-1 output capacity exceeded"; }
+        // [0] part bytes, [1] failure flag, [2] tile-part header bytes,
+        // [3..] packet bytes per layer (Kdu-Layer-Info)
+        std::vector<int64_t> v((size_t)L + 3, 0);
+        v[1] = rok ? 0 : 1;
+        if (rok && have) {
+            v[0] = sum.part_bytes;
+            v[2] = sum.tp_hdr_bytes;
+            for (int l = 0; l < L; l++) v[3 + l] = sum.layer_bytes[l];
         }
-        const double t0 = now_ms();
-        int64_t v[2] = {0, rok ? 0 : 1};
-        if (rok) v[0] = t2_headers(in, t2) - (int64_t)t2.main.size() - 2;
-        t2ms += now_ms() - t0;
-        if (!allreduce(v, 2)) { err = "split: all-reduce failed"; return false; }
+        if (!allreduce(v.data(), (int)v.size())) { err = "split: all-reduce failed"; return false; }
         if (v[1]) { if (rok) err = "split: another rank failed"; return false; }
-        cs_bytes = (int64_t)t2.main.size() + 2 + v[0];
+        cs_bytes = (int64_t)mh.size() + 2 + v[0];
+        g_tp_hdr = v[2];
+        g_layer.assign(v.begin() + 3, v.end());
         iters++;
         return true;
     };
-    if (rc.rate_bpp <= 0.0) {
-        int64_t total = 0;
-        if (have)
-            for (size_t b = 0; b < nbl; b++) total += ctx->gpu.block_lengths()[b];
-        if (!allreduce(&total, 1)) return fail("split: all-reduce failed");
-        for (int l = 0; l < L; l++) budgets[l] = total >> (L - 1 - l);
-        if (!round()) return fail(err);
-    } else {
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if (attempt == 1) {  // the prediction's safety net, decided globally (below)
+            keys.clear();
+            cum.clear();
+            ok = !have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, 0);
+            skip_target = 0;
+            iters = 0;
+        }
+        ok = ok && (!have || ctx->gpu.segments(keys, cum, err));
+        {
+            int64_t flag = ok ? 0 : 1;
+            if (!allreduce(&flag, 1)) return fail("split: all-reduce failed");
+            if (!ok) return fail(err);
+            if (flag) return fail("split: another rank failed");
+        }
+        if (rc.rate_bpp <= 0.0) {
+            int64_t total = 0;
+            if (have && !ctx->gpu.t1_totals(sub, total, err)) ok = false;
+            int64_t v[2] = {total, ok ? 0 : 1};
+            if (!allreduce(v, 2)) return fail("split: all-reduce failed");
+            if (!ok) return fail(err);
+            if (v[1]) return fail("split: another rank failed");
+            for (int l = 0; l < L; l++) budgets[l] = v[0] >> (L - 1 - l);
+            if (!round()) return fail(err);
+            break;
+        }
         const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)full.w * (double)full.h / 8.0);
         int64_t budget = target - 12 * full.npackets - 16 * full.ntileparts - 256;
+        bool rerun = false;
         for (int it = 0; it < 8; it++) {
             if (budget < 0) budget = 0;
             for (int l = 0; l < L; l++) budgets[l] = budget >> (L - 1 - l);
             if (!round()) return fail(err);
+            if (it == 0 && skip_target > 0) {
+                int64_t v[2] = {have ? sum.t1_bytes : 0, have ? sum.skipped : 0};
+                if (!allreduce(v, 2)) return fail("split: all-reduce failed");
+                if (v[1] && v[0] < skip_target) { rerun = true; break; }
+            }
             if (cs_bytes <= target) break;
             budget -= ((cs_bytes - target) << it) + ((cs_bytes - target) >> 4) + 64;  // as encode_core
         }
+        if (!rerun) break;
     }
-    // this rank's included bytes
-    std::vector<int32_t> final_len(nbl);
-    std::vector<uint64_t> offs(nbl), offs_full(nbf, 0);
-    uint64_t total = 0;
-    for (size_t b = 0; b < nbl; b++) {
-        final_len[b] = h_lrate[b * L + (L - 1)];
-        offs[b] = total;
-        offs_full[b0 + b] = total;
-        total += (uint64_t)final_len[b];
-    }
-    const uint8_t *data = nullptr;
-    const double tg = now_ms();
-    ok = !have || ctx->gpu.gather(sub, final_len, offs, total, &data, prof, st, err);
-    const double gather_ms = now_ms() - tg;
+    // this rank's part of the file
     const bool with_main = rank == 0, with_eoc = rank == world - 1;
     const size_t fh = with_main ? file_header_bytes(full) : 0;
-    const uint64_t part = ok ? fh + t2_part_bytes(in, t2, with_main, with_eoc) : 0;
+    const uint64_t head = with_main ? fh + mh.size() : 0;
+    const uint64_t part = head + (uint64_t)(have ? sum.part_bytes : 0) + (with_eoc ? 2 : 0);
     std::vector<int64_t> sizes((size_t)world + 1, 0);
     sizes[rank] = (int64_t)part;
-    sizes[world] = ok ? 0 : 1;
     if (!allreduce(sizes.data(), world + 1)) return fail("split: all-reduce failed");
-    if (!ok) return fail(err);
     if (sizes[world]) return fail("split: another rank failed");
     uint64_t off = 0, flen = 0;
     for (int r = 0; r < world; r++) {
         if (r < rank) off += (uint64_t)sizes[r];
         flen += (uint64_t)sizes[r];
     }
-    in.data = data;
-    in.data_off = offs_full.data();
-    const double t0 = now_ms();
-    uint8_t *buf = (uint8_t *)std::malloc(part ? part : 1);
-    if (!buf) return fail("out of memory");
-    if (with_main) write_file_header(full, (uint64_t)cs_bytes, buf);
-    t2_emit_part(in, t2, buf + fh, with_main, with_eoc);
-    t2ms += now_ms() - t0;
+    uint8_t *buf = out_alloc(part ? part : 1);
+    if (!buf) return fail("out of (pinned) host memory");
+    if (with_main) {
+        std::vector<uint64_t> Kcom = K;
+        if (rc.rate_bpp <= 0.0) Kcom[L - 1] = 0;
+        std::vector<int64_t> layer_end((size_t)L);
+        layer_end_of(full, g_tp_hdr, g_layer.data(), layer_end.data());
+        main_header(full, mh, Kcom.data(), layer_end.data());
+        write_file_header(full, (uint64_t)cs_bytes, buf);
+        std::memcpy(buf + fh, mh.data(), mh.size());
+    }
+    if (have && (!ctx->gpu.t2_emit(sub, 0, (uint64_t)sum.part_bytes, buf + head, prof, st, err) ||
+                 !ctx->gpu.collect_profile(st, err))) {
+        out_free(buf);
+        return fail(err);
+    }
+    if (with_eoc) {
+        buf[part - 2] = 0xFF;
+        buf[part - 1] = 0xD9;
+    }
     *out = buf;
     *out_len = part;
     if (file_offset) *file_offset = off;
     if (file_len) *file_len = flen;
-    if (stats) {
-        std::memset(stats, 0, sizeof *stats);
-        stats->total_ms = now_ms() - t_start;
-        stats->ingest_ms = st.ingest;
-        stats->dwt_ms = st.dwt;
-        stats->quant_ms = st.quant;
-        stats->t1_ms = st.t1_cm + st.t1_mq;
-        stats->t1_cm_ms = st.t1_cm;
-        stats->t1_mq_ms = st.t1_mq;
-        stats->pcrd_ms = st.pcrd;
-        stats->d2h_ms = prof ? st.d2h : gather_ms;
-        stats->t2_ms = t2ms;
-        stats->codeblocks = (int64_t)nbl;
-        if (have) {
-            int64_t tb = 0, tp = 0;
-            ctx->gpu.t1_total_bytes(tb, tp);
-            stats->t1_bytes = tb;
-            stats->coded_passes = tp;
-        }
-        stats->out_bytes = (int64_t)flen;
-        stats->rate_iterations = iters;
-    }
+    fill_stats(stats, st, t_start, 0.0, (int64_t)sub.blocks.size(), sum, (int64_t)flen, iters);
     return 0;
 }
 
@@ -587,6 +702,16 @@ int jp2hip_probe(void) {
             return 1;
     }
     return 0;
+}
+
+int jp2hip_device_count(void) {
+    int n = 0, k = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
+    for (int i = 0; i < n; i++) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) k++;
+    }
+    return k;
 }
 
 void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
@@ -688,12 +813,12 @@ int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path, const char *out_p
                       std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000);
     FILE *o = std::fopen(tmp.c_str(), "wb");
     if (!o) {
-        std::free(out);
+        out_free(out);
         return fail(std::string("cannot write output: ") + out_path);
     }
     bool ok = std::fwrite(out, 1, olen, o) == olen;
     ok = (std::fclose(o) == 0) && ok;
-    std::free(out);
+    out_free(out);
     if (!ok || std::rename(tmp.c_str(), out_path) != 0) {
         std::remove(tmp.c_str());
         return fail(std::string("cannot write output: ") + out_path);
@@ -708,13 +833,12 @@ int jp2hip_encode_device_split(jp2hip_ctx *ctx, const void *d_src, size_t src_le
     if (!ctx || !out || !out_len) return fail("null argument");
     *out = nullptr;
     *out_len = 0;
-    (void)src_len;
     double t0 = now_ms();
     std::lock_guard<std::mutex> lk(ctx->mu);
-    return encode_split_core(ctx, d_src, layout, conversion, recipe, split, out, out_len, file_offset, file_len,
-                             stats, t0);
+    return encode_split_core(ctx, d_src, src_len, layout, conversion, recipe, split, out, out_len, file_offset,
+                             file_len, stats, t0);
 }
 
-void jp2hip_free(void *p) { std::free(p); }
+void jp2hip_free(void *p) { out_free(p); }
 
 }  // extern "C"

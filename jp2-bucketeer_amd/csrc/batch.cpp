@@ -202,8 +202,10 @@ struct jp2hip_batch {
             std::memset(&lay, 0, sizeof lay);
             if (offs.size() < 1024) offs.resize(1024);
             int prc = jp2hip_tiff_layout(j.src, j.src_len, &lay, offs.data(), (int32_t)offs.size());
-            if (prc != 0 && lay.height > 0 && (size_t)lay.height > offs.size()) {  // more strips than slots
-                offs.resize(2 * (size_t)lay.height * (size_t)std::max(1, lay.components));  // + byte counts
+            // more strips / tiles than slots: the parse already counted them
+            // (offsets + byte counts for compressed or tiled files)
+            if (prc != 0 && lay.nstrips > 0 && 2 * (size_t)lay.nstrips > offs.size()) {
+                offs.resize(2 * (size_t)lay.nstrips);
                 prc = jp2hip_tiff_layout(j.src, j.src_len, &lay, offs.data(), (int32_t)offs.size());
             }
             if (prc != 0) {

@@ -17,8 +17,10 @@ struct DevBuf {
 };
 
 struct StageTimes {
-    double ingest = 0, dwt = 0, quant = 0, t1_cm = 0, t1_mq = 0, pcrd = 0, d2h = 0;
+    double ingest = 0, dwt = 0, quant = 0, t1_cm = 0, t1_mq = 0, pcrd = 0, d2h = 0, t2 = 0;
 };
+
+struct T2Args;  // t2_device.hip
 
 // tier-1 kernels (t1.hip)
 struct T1CmArgs {
@@ -97,31 +99,36 @@ class GpuEncoder {
                    StageTimes &st, std::string &err, int64_t skip_target = 0,
                    const HistReduce *reduce = nullptr);
     // layer thresholds for the given data budgets -> per-block layer tables
-    bool select(const Plan &plan, const std::vector<int64_t> &budgets, std::vector<uint8_t> &h_nl,
-                std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err);
+    // in HBM (enqueued only; t2_size reads the result)
+    bool select(const Plan &plan, const std::vector<int64_t> &budgets, std::string &err);
+    // lossless "-rate -": budgets total >> (L-1-l) from the tier-1 lengths,
+    // computed on the device
+    bool select_lossless(const Plan &plan, std::string &err);
     // per-block layer tables for explicit slope thresholds K[layer]
     // (tile-split: thresholds agreed across ranks)
-    bool select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::vector<uint8_t> &h_nl,
-                     std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err);
+    bool select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::string &err);
+    // tier-2 on the device (t2_device.hip): tables for the tiles coded, one sizing
+    // pass per layer table (one host wait: the summary), then the code-stream
+    // part (tile-parts, in stream order) written in HBM and copied to host_dst
+    bool t2_load(const Plan &plan, const T2Tables &T, std::string &err);
+    bool t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum, std::string &err);
+    // host_dst must be pinned (hipHostMalloc) memory
+    bool t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
+                 StageTimes &st, std::string &err);
+    // tier-1 totals (one host wait; the tile-split path's lossless budget)
+    bool t1_totals(const Plan &plan, int64_t &bytes, std::string &err);
+    // stage times of the last encode from its events (profile mode; call
+    // after the encode's last host wait)
+    bool collect_profile(StageTimes &st, std::string &err);
     // this encode's hull segments: slope keys (descending) and inclusive byte sums
     bool segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err);
-    // compact the included bytes of every block and download them
-    bool gather(const Plan &plan, const std::vector<int32_t> &final_len,
-                const std::vector<uint64_t> &offsets, uint64_t total, const uint8_t **host_data,
-                bool profile, StageTimes &st, std::string &err);
-
-    bool t1_total_bytes(int64_t &bytes, int64_t &passes) const;
-    const std::vector<int32_t> &block_lengths() const { return h_lengths; }
-    const std::vector<uint8_t> &block_passes() const { return h_npasses; }
-    const std::vector<uint8_t> &block_planes() const { return h_P; }
-    const std::vector<uint8_t> &block_pmin() const { return h_pmin; }
     hipStream_t get_stream() const { return stream; }
 
   private:
     // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
-    bool apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate,
-                          bool profile, StageTimes &st, std::string &err);
+    bool apply_thresholds(const Plan &plan, std::string &err);
+    T2Args t2_args(const Plan &plan) const;
     bool host_wait(std::string &err);
     static constexpr int kNumEvents = 12;
     int device = 0;
@@ -132,11 +139,17 @@ class GpuEncoder {
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
         est, hist, kcut, pmin, mqspan, stage, soff, lzwtab, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
         dbgbuf;
+    // device tier-2 (t2_device.hip)
+    DevBuf hdist;
+    DevBuf t2prec, t2tp, t2tt, t2lblock, t2incl, t2pklen, t2pkoff, t2tplen, t2tphdr, t2tpoff, t2blkdst, t2out, t2sum;
+    int t2_nprec = 0, t2_ntp = 0;
+    T2Summary *h_sum = nullptr;
+    int64_t *h_tot = nullptr;  // pinned: t1_totals / profile read-back
+    bool profiled = false;
     int nseg = 0;
     uint8_t *h_packed = nullptr;
     size_t h_packed_cap = 0;
-    std::vector<int32_t> h_lengths;
-    std::vector<uint8_t> h_npasses, h_P, h_pmin;
+    std::vector<uint8_t> h_P, h_pmin;
     std::vector<int64_t> h_hist;
     std::vector<int2> h_items;
     std::vector<uint64_t> h_slot;

@@ -93,66 +93,57 @@ bool build_plan(Plan &plan, const jp2hip_recipe &rc, int w, int h, int nc, int b
 
 int prec_log2(const jp2hip_recipe &rc, int r, bool vertical);
 
-// Tile rows [tr0, tr1) of rank `rank` out of `world` (contiguous bands).
-void split_tile_rows(int nty, int rank, int world, int &tr0, int &tr1);
+// Tile rows grouped the way "-flush_period P" flushes them
+// (KakaduConverter.java:40; oracle flush_stripes): a stripe ends once the rows
+// pushed reach the next multiple of P, and at the last tile row.  Returns one
+// past the last tile row of each stripe.  P <= 0: one stripe per tile row.
+std::vector<int> flush_stripe_ends(int nty, int tile_h, int h, int period);
+// Tile rows [tr0, tr1) of rank `rank` out of `world`: contiguous runs of
+// whole flush stripes, so each rank's tile-parts are contiguous in the file.
+void split_tile_rows(int nty, int tile_h, int h, int period, int rank, int world, int &tr0, int &tr1);
 // The device part of `full` for tile rows [tr0, tr1): same blocks, offsets
 // rebased to the band (tier-2 keeps using `full` and global block indices).
 void make_subplan(const Plan &full, int tr0, int tr1, Plan &sub);
 
-// Tier-2 inputs: the layer table chosen by PCRD.  `data` holds the included
-// bytes of every block back to back at `data_off[b]` (needed by t2_emit only).
-struct T2Input {
-    const Plan *plan;
-    const uint8_t *P;           // coded bit-planes per block
-    const uint8_t *nl;          // [block][layers] cumulative passes per layer
-    const int32_t *lrate;       // [block][layers] cumulative bytes per layer
-    const uint8_t *data;
-    const uint64_t *data_off;
-    int threads;
-    int tile0 = 0, tile1 = -1;  // tiles to code ([tile0, tile1); -1: all)
+// --------------------------------------------------------------------------
+// Device tier-2 (t2_device.hip).  The host lays out, once per encode, the precincts
+// of the tiles being coded in packet order (tile, resolution, py, px,
+// component; RPCL) and the tile-parts in code-stream order (-flush_period
+// stripes); the kernels code every packet header, size the tile-parts and
+// write the code-stream in HBM.  Packet k of precinct p is packet p * L + k.
+// --------------------------------------------------------------------------
+struct PrecDesc {
+    int32_t first[3];        // first code-block (encode-local index) of each precinct-band
+    uint16_t ncw[3], nch[3]; // code-block grid of each precinct-band
+    int32_t tt_off;          // tag-tree node scratch: (inclusion, zero bit-planes) per band
+    int32_t nsop0;           // SOP sequence number of the precinct's first packet in its tile
+    uint8_t nb, pad0, pad1, pad2;
 };
-
-struct TagNode {
-    int32_t parent, value, low;
-    int32_t known;
+static_assert(sizeof(PrecDesc) == 36, "PrecDesc layout");
+struct TpDesc {
+    int32_t tile, tpsot, tnsot;  // SOT fields (Isot, TPsot, TNsot)
+    int32_t prec0, nprec;        // its precincts in the PrecDesc table
 };
-
-// Per-tile result of the header pass (reused across calls; no reallocation
-// once warm).
-struct T2Tile {
-    std::vector<uint8_t> hdr;        // coded packet headers, back to back
-    std::vector<uint32_t> hdr_end;   // per packet: end offset in hdr
-    std::vector<uint32_t> pk_len;    // per packet: SOP + header + EPH + body bytes
-    std::vector<uint32_t> pk_cend;   // per packet: end index (in triples) into contrib
-    std::vector<uint32_t> contrib;   // (block, first byte, end byte) of each body piece
-    std::vector<int32_t> tp_npk;     // packets per tile-part
-    std::vector<uint64_t> tp_bytes;  // Psot per tile-part
-    std::vector<int32_t> tree;       // tag-tree roots per (c, r, precinct, band)
-    uint64_t bytes = 0;
+struct T2Tables {
+    std::vector<PrecDesc> prec;
+    std::vector<TpDesc> tp;   // code-stream order
+    int64_t tt_nodes = 0;
 };
-struct T2Worker {
-    std::vector<int32_t> lblock;     // indexed by block (a tile touches only its own)
-    std::vector<int8_t> incl;
-    std::vector<TagNode> nodes;
+// Tables for tiles [tile0, tile1) of `P` (blocks rebased by -block0: a
+// tile-split rank's blocks are its sub-plan's).
+void t2_tables(const Plan &P, int tile0, int tile1, int block0, T2Tables &T);
+// What the host reads back after a tier-2 sizing pass (one D2H per pass).
+struct T2Summary {
+    int64_t part_bytes;               // tile-parts of the tiles coded (SOT .. last packet)
+    int64_t tp_hdr_bytes;             // SOT + PLT + SOD of those tile-parts
+    int64_t layer_bytes[kMaxLayers];  // packet bytes per layer
+    uint64_t kc[kMaxLayers];          // Kdu-Layer-Info slope keys (select() only)
+    int64_t t1_bytes, coded_passes;   // tier-1 totals (every coded pass)
+    int32_t skipped, err;             // slope prediction skipped planes; tier-1 overflow
 };
-struct T2State {
-    std::vector<uint8_t> main;       // main header (SOC .. COM)
-    std::vector<T2Tile> tiles;
-    std::vector<T2Worker> workers;
-    int64_t total = 0;               // code-stream bytes, SOC .. EOC
-};
-
-// Header pass: codes every packet header of tiles [in.tile0, in.tile1),
-// returns main header + those tiles + EOC (the code-stream size when the
-// range is every tile).
-int64_t t2_headers(const T2Input &in, T2State &st);
-// Writes the code-stream described by the last t2_headers() into dst
-// (st.total bytes); in.data / in.data_off must be set.
-void t2_emit(const T2Input &in, const T2State &st, uint8_t *dst);
-// Tile-split: bytes of tiles [in.tile0, in.tile1) (+ main header / EOC when
-// asked) as written by t2_emit_part.
-uint64_t t2_part_bytes(const T2Input &in, const T2State &st, bool with_main, bool with_eoc);
-void t2_emit_part(const T2Input &in, const T2State &st, uint8_t *dst, bool with_main, bool with_eoc);
+// Main header (SOC .. COM) for the Kdu-Layer-Info values (nullptr: zeros;
+// the length does not depend on them).
+void main_header(const Plan &P, std::vector<uint8_t> &v, const uint64_t *K, const int64_t *layer_end);
 
 // JP2 / JPX boxes in front of the code-stream (0 bytes for raw J2K).
 size_t file_header_bytes(const Plan &plan);

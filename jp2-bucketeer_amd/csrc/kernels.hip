@@ -148,7 +148,12 @@ __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
     int nbits = 0, width = 9, next = 258;
     uint32_t prev_len = 0;
     bool bad = false;
+    if (n >= 2 && in[0] == 0 && (in[1] & 1)) {  // pre-TIFF 6.0 (LSB-first) LZW, as libtiff detects it
+        atomicOr(a.err, 4);
+        return;
+    }
     for (;;) {
+        if (pos >= cap) break;  // strip complete: trailing codes are ignored (libtiff stops here too)
         if (nbits < width) {  // top up to >= 32 bits with independent byte loads
             if (ip + 4 <= n) {
                 const uint32_t w4 = ((uint32_t)in[ip] << 24) | ((uint32_t)in[ip + 1] << 16) |
@@ -168,7 +173,6 @@ __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
         const uint64_t cur = pos;
         uint32_t len;
         if (code < 256) {
-            if (pos >= cap) { bad = true; break; }
             out[pos++] = (uint8_t)code;
             len = 1;
         } else {
@@ -177,7 +181,11 @@ __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
             if (code < next) { const uint2 e = tab[code]; from = e.x; len = e.y; }
             else if (code == next && prev_len) { from = prev_pos; len = prev_len + 1; kwk = true; }
             else { bad = true; break; }
-            if (pos + len > cap) { bad = true; break; }
+            if (pos + len > cap) {  // the strip ends inside this string: keep what fits
+                for (uint64_t k = 0; pos + k < cap; k++) out[pos + k] = (kwk && k == len - 1) ? out[from] : out[from + k];
+                pos = cap;
+                break;
+            }
             const uint32_t body = kwk ? len - 1 : len;  // source bytes all lie before pos
             uint32_t k = 0;
             for (; k + 8 <= body; k += 8) {
@@ -216,16 +224,19 @@ __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
     bool bad = false;
     while (ip < n && pos < cap) {
         const int c = (int8_t)in[ip++];
+        // a run past the strip's end is cut at cap (libtiff keeps what fits)
         if (c >= 0) {
-            if (ip + c + 1 > n || pos + c + 1 > cap) { bad = true; break; }
-            for (int i = lane; i <= c; i += 64) out[pos + i] = in[ip + i];
+            if (ip + c + 1 > n) { bad = true; break; }
+            const uint64_t m = min((uint64_t)c + 1, cap - pos);
+            for (uint64_t i = lane; i < m; i += 64) out[pos + i] = in[ip + i];
             ip += c + 1;
-            pos += c + 1;
+            pos += m;
         } else if (c != -128) {
-            if (ip >= n || pos + 1 - c > cap) { bad = true; break; }
+            if (ip >= n) { bad = true; break; }
             const uint8_t v = in[ip++];
-            for (int i = lane; i < 1 - c; i += 64) out[pos + i] = v;
-            pos += 1 - c;
+            const uint64_t m = min((uint64_t)(1 - c), cap - pos);
+            for (uint64_t i = lane; i < m; i += 64) out[pos + i] = v;
+            pos += m;
         }
     }
     if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
@@ -389,8 +400,10 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
         if (b.bad) { bad = true; break; }
         if (type == 0) {  // stored: to the byte boundary, LEN, ~LEN, bytes
             b.align();
-            const uint32_t len = b.get(16), nlen = b.get(16);
-            if (b.bad || len != (~nlen & 0xFFFFu) || pos + len > cap) { bad = true; break; }
+            uint32_t len = b.get(16);
+            const uint32_t nlen = b.get(16);
+            if (b.bad || len != (~nlen & 0xFFFFu)) { bad = true; break; }
+            if (pos + len > cap) { len = (uint32_t)(cap - pos); last = true; }  // strip full: stop here
             for (uint32_t i = 0; i < len; i++) {
                 win[(uint32_t)pos & WM] = (uint8_t)b.get(8);
                 if (++pos - flushed >= 4096) flush(flushed + 4096);
@@ -434,7 +447,7 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
             int sy = inf_decode<LB>(b, lfast, lcnt, lsym);
             if (sy < 0) { bad = true; break; }
             if (sy < 256) {
-                if (pos >= cap) { bad = true; break; }
+                if (pos >= cap) { last = true; break; }  // strip full: trailing data ignored
                 win[(uint32_t)pos++ & WM] = (uint8_t)sy;
                 if (pos - flushed >= 4096) flush(flushed + 4096);
                 continue;
@@ -446,7 +459,13 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
             const int d = inf_decode<DB>(b, dfast, dcnt, dsym);
             if (d < 0 || d >= 30) { bad = true; break; }
             const uint32_t dist = dbase[d] + b.get(dextra[d]);
-            if (b.bad || dist > pos || pos + len > cap) { bad = true; break; }
+            if (b.bad || dist > pos) { bad = true; break; }
+            if (pos + len > cap) {  // the strip ends inside this match: keep what fits
+                for (uint32_t k = 0; pos + k < cap; k++) win[(uint32_t)(pos + k) & WM] = win[(uint32_t)(pos - dist + k) & WM];
+                pos = cap;
+                last = true;
+                break;
+            }
             const uint32_t src = (uint32_t)(pos - dist), dst = (uint32_t)pos;
             uint32_t k = 0;
             if (dist >= 8)  // 8 independent LDS reads, then the writes
@@ -739,6 +758,7 @@ struct HullArgs {
     uint8_t *nhull;
     uint8_t *hpass;   // [block][kMaxPasses+1]
     uint64_t *hkey;   // [block][kMaxPasses+1]
+    int64_t *hdist;   // [block][kMaxPasses+1] cumulative distortion at each hull point
 };
 
 __global__ void __launch_bounds__(256) k_hull(HullArgs a) {
@@ -749,30 +769,33 @@ __global__ void __launch_bounds__(256) k_hull(HullArgs a) {
     const int64_t *Dd = a.dists + (size_t)b * kMaxPasses;
     uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
     uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
+    // the hull stack lives in the output arrays themselves (pass index,
+    // slope bits) plus the cumulative distortion of each hull point in hd,
+    // so the lane keeps no per-pass arrays (no scratch memory)
+    int64_t *hd = a.hdist + (size_t)b * (kMaxPasses + 1);
     double wgt = a.weight[b];
-    int64_t D[kMaxPasses + 1];
-    double sl[kMaxPasses + 1];
-    D[0] = 0;
-    for (int n = 1; n <= np; n++) D[n] = D[n - 1] + Dd[n - 1];
     int nh = 1;
     hp[0] = 0;
-    sl[0] = 0.0;
+    hk[0] = 0;
+    hd[0] = 0;
+    int64_t Dn = 0;
     for (int n = 1; n <= np; n++) {
+        Dn += Dd[n - 1];
         for (;;) {
             int hh = hp[nh - 1];
-            int64_t dD = D[n] - D[hh];
+            int64_t dD = Dn - hd[nh - 1];
             int32_t dR = R[n - 1] - (hh ? R[hh - 1] : 0);
             if (dD <= 0) break;
             if (dR <= 0) { nh--; continue; }
             double s = (double)dD * wgt / (double)dR;
-            if (nh >= 2 && s >= sl[nh - 1]) { nh--; continue; }
+            if (nh >= 2 && s >= __longlong_as_double((long long)hk[nh - 1])) { nh--; continue; }
             hp[nh] = (uint8_t)n;
-            sl[nh] = s;
+            hk[nh] = (uint64_t)__double_as_longlong(s);
+            hd[nh] = Dn;
             nh++;
             break;
         }
     }
-    for (int i = 0; i < nh; i++) hk[i] = (uint64_t)__double_as_longlong(sl[i]);
     a.nhull[b] = (uint8_t)nh;
 }
 
@@ -802,9 +825,11 @@ __global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nh
     }
 }
 
-// one thread per layer: threshold key K (UINT64_MAX = nothing fits)
+// one thread per layer: threshold key K (UINT64_MAX = nothing fits), and Kc,
+// the Kdu-Layer-Info slope: one above the first key not taken, 0 if every
+// segment is taken (= the tile-split bisection's K'; oracle select_threshold)
 __global__ void k_thresh(int nseg, int layers, const uint64_t *keys, const int64_t *cum,
-                         const int64_t *budget, uint64_t *K) {
+                         const int64_t *budget, uint64_t *K, uint64_t *Kc) {
     int l = threadIdx.x;
     if (l >= layers) return;
     int64_t bgt = budget[l];
@@ -826,6 +851,7 @@ __global__ void k_thresh(int nseg, int layers, const uint64_t *keys, const int64
         j = l2 - 1;
     }
     K[l] = (j >= 0) ? keys[j] : 0xFFFFFFFFFFFFFFFFull;
+    Kc[l] = (j + 1 < nseg) ? keys[j + 1] + 1 : 0ull;
 }
 
 // last hull index whose key >= K (0 = nothing); hull keys strictly decrease
@@ -863,17 +889,6 @@ __global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
     }
 }
 
-// gather included bytes: one workgroup per block
-__global__ void __launch_bounds__(256) k_compact(const BlockDesc *blocks, const uint8_t *src,
-                                                 const uint64_t *dst_off, const int32_t *len,
-                                                 uint8_t *dst) {
-    int b = blockIdx.x;
-    const uint8_t *s = src + blocks[b].out_off;
-    uint8_t *o = dst + dst_off[b];
-    int n = len[b];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) o[i] = s[i];
-}
-
 // --------------------------------------------------------------------------
 // Device pipeline
 // --------------------------------------------------------------------------
@@ -900,7 +915,9 @@ GpuEncoder::~GpuEncoder() {
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
                      &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
-                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwtab, &untiled};
+                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwtab, &untiled,
+                     &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
+                     &t2blkdst, &t2out, &t2sum, &hdist};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -908,6 +925,8 @@ GpuEncoder::~GpuEncoder() {
     for (int i = 0; i < kNumEvents; i++)
         if (ev[i]) (void)hipEventDestroy(ev[i]);
     if (h_packed) (void)hipHostFree(h_packed);
+    if (h_sum) (void)hipHostFree(h_sum);
+    if (h_tot) (void)hipHostFree(h_tot);
 }
 
 bool GpuEncoder::init(int dev, std::string &err) {
@@ -1023,6 +1042,10 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
     int herr = 0;
     HIPCHECK(hipMemcpyAsync(&herr, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (!host_wait(err)) return false;
+    if (herr & 4) {
+        err = "tiff: old-style (pre-TIFF 6.0, LSB-first) LZW strips are not supported";
+        return false;
+    }
     if (herr) {
         err = "tiff: corrupt compressed strip";
         return false;
@@ -1062,6 +1085,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<uint8_t>(nhull, nb, err)) return false;
     if (!ensure<uint8_t>(hpass, (size_t)nb * (kMaxPasses + 1), err)) return false;
     if (!ensure<uint64_t>(hkey, (size_t)nb * (kMaxPasses + 1), err)) return false;
+    if (!ensure<int64_t>(hdist, (size_t)nb * (kMaxPasses + 1), err)) return false;
     if (!ensure<int64_t>(budget, kMaxLayers, err)) return false;
     if (!ensure<uint8_t>(nl, (size_t)nb * plan.rc.layers, err)) return false;
     if (!ensure<int32_t>(lrate, (size_t)nb * plan.rc.layers, err)) return false;
@@ -1272,6 +1296,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ha.nhull = (uint8_t *)nhull.ptr;
     ha.hpass = (uint8_t *)hpass.ptr;
     ha.hkey = (uint64_t *)hkey.ptr;
+    ha.hdist = (int64_t *)hdist.ptr;
     if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + 255) / 256), dim3(256), 0, stream, ha);
     HIPCHECK(hipGetLastError());
     // hull segments of all blocks, sorted by slope key (descending), sizes prefix-summed
@@ -1293,7 +1318,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     nseg = tail[0] + tail[1];
     if (!ensure<uint64_t>(segkey, std::max(nseg, 1), err) || !ensure<uint64_t>(segkey2, std::max(nseg, 1), err) ||
         !ensure<int64_t>(segval, std::max(nseg, 1), err) || !ensure<int64_t>(segval2, std::max(nseg, 1), err) ||
-        !ensure<int64_t>(segcum, std::max(nseg, 1), err) || !ensure<uint64_t>(thr, kMaxLayers, err))
+        !ensure<int64_t>(segcum, std::max(nseg, 1), err) || !ensure<uint64_t>(thr, 2 * kMaxLayers, err))
         return false;
     if (nb) hipLaunchKernelGGL(k_seg_emit, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
                                (const uint8_t *)nhull.ptr, (const uint8_t *)hpass.ptr,
@@ -1312,22 +1337,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         HIPCHECK(hipcub::DeviceScan::InclusiveSum(cubtmp.ptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
     }
     HIPCHECK(hipEventRecord(ev[5], stream));
-    // totals needed on the host for the budgets
-    h_lengths.resize(nb);
-    h_npasses.resize(nb);
-    h_P.resize(nb);
-    HIPCHECK(hipMemcpyAsync(h_P.data(), P.ptr, nb, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(h_lengths.data(), lengths.ptr, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(h_npasses.data(), npasses.ptr, nb, hipMemcpyDeviceToHost, stream));
-    int herr = 0;
-    unsigned long long span[2] = {0, 0};
-    HIPCHECK(hipMemcpyAsync(&herr, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(span, mqspan.ptr, sizeof span, hipMemcpyDeviceToHost, stream));
-    if (!host_wait(err)) return false;
-    if (herr) {
-        err = "tier-1 output capacity exceeded";
-        return false;
-    }
+    profiled = profile;
     if (dd) {
         if (!dump(dd, "blocks.bin", blocks, sizeof(BlockDesc) * nb, err)) return false;
         if (!dump(dd, "sm.bin", sm, plan.sm_words * 4, err)) return false;
@@ -1342,43 +1352,77 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!dump(dd, "bp.bin", bp, plan.bp_words * 8, err)) return false;
         if (!dump(dd, "mqdbg.bin", dbgbuf, (size_t)nb * 4 * 8, err)) return false;
     }
-    if (profile) {
-        float t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[0], ev[1])); st.ingest = t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[1], ev[2])); st.dwt = t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[2], ev[3])); st.quant = t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[10], ev[11])); st.t1_cm = t;
-        // k_t1_mq's own execution span (100 MHz wall clock, see t1.hip)
-        st.t1_mq = nb && span[1] > span[0] ? (double)(span[1] - span[0]) * 1e-5 : 0.0;
-        HIPCHECK(hipEventElapsedTime(&t, ev[4], ev[5])); st.pcrd = t;
-    }
+    // no host wait: tier-1 totals and the overflow flag reach the host with
+    // the first tier-2 summary (t2_size), stage times via collect_profile()
     return true;
 }
 
-bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets,
-                        std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate, bool profile,
-                        StageTimes &st, std::string &err) {
+// Stage times from the events of the last encode (all complete once the
+// encode's final host wait returned).
+bool GpuEncoder::collect_profile(StageTimes &st, std::string &err) {
+    if (!profiled || !h_tot) return true;
+    const uint64_t span[2] = {(uint64_t)h_tot[2], (uint64_t)h_tot[3]};  // read back by t2_emit
+    float t;
+    HIPCHECK(hipEventElapsedTime(&t, ev[0], ev[1])); st.ingest = t;
+    HIPCHECK(hipEventElapsedTime(&t, ev[1], ev[2])); st.dwt = t;
+    HIPCHECK(hipEventElapsedTime(&t, ev[2], ev[3])); st.quant = t;
+    HIPCHECK(hipEventElapsedTime(&t, ev[10], ev[11])); st.t1_cm = t;
+    // k_t1_mq's own execution span (100 MHz wall clock, see t1.hip)
+    st.t1_mq = span[1] > span[0] ? (double)(span[1] - span[0]) * 1e-5 : 0.0;
+    HIPCHECK(hipEventElapsedTime(&t, ev[4], ev[5])); st.pcrd += t;
+    return true;
+}
+
+bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     const int L = plan.rc.layers;
     HIPCHECK(hipMemcpyAsync(budget.ptr, budgets.data(), sizeof(int64_t) * L, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipEventRecord(ev[6], stream));
     hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
-                       (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr);
+                       (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
+                       (uint64_t *)thr.ptr + kMaxLayers);
     HIPCHECK(hipGetLastError());
-    return apply_thresholds(plan, h_nl, h_lrate, profile, st, err);
+    return apply_thresholds(plan, err);
 }
 
-bool GpuEncoder::select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::vector<uint8_t> &h_nl,
-                             std::vector<int32_t> &h_lrate, bool profile, StageTimes &st, std::string &err) {
+// lossless "-rate -": layer l's budget is total >> (L-1-l), total = every
+// coded byte (api.cpp encode_core restates the rule for the split path)
+__global__ void __launch_bounds__(256) k_budget_lossless(int nblocks, const int32_t *lengths, int layers,
+                                                         int64_t *budget) {
+    __shared__ int64_t part[256];
+    int64_t s = 0;
+    for (int b = threadIdx.x; b < nblocks; b += 256) s += lengths[b];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t tot = 0;
+        for (int i = 0; i < 256; i++) tot += part[i];
+        for (int l = 0; l < layers; l++) budget[l] = tot >> (layers - 1 - l);
+    }
+}
+
+bool GpuEncoder::select_lossless(const Plan &plan, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    const int L = plan.rc.layers, nb = (int)plan.blocks.size();
+    HIPCHECK(hipEventRecord(ev[6], stream));
+    hipLaunchKernelGGL(k_budget_lossless, dim3(1), dim3(256), 0, stream, nb, (const int32_t *)lengths.ptr, L,
+                       (int64_t *)budget.ptr);
+    hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
+                       (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
+                       (uint64_t *)thr.ptr + kMaxLayers);
+    HIPCHECK(hipGetLastError());
+    return apply_thresholds(plan, err);
+}
+
+bool GpuEncoder::select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     HIPCHECK(hipMemcpyAsync(thr.ptr, K.data(), sizeof(uint64_t) * plan.rc.layers, hipMemcpyHostToDevice, stream));
     HIPCHECK(hipEventRecord(ev[6], stream));
-    return apply_thresholds(plan, h_nl, h_lrate, profile, st, err);
+    return apply_thresholds(plan, err);
 }
 
 // per-block layer tables for the thresholds in `thr` (ev[6] already recorded)
-bool GpuEncoder::apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, std::vector<int32_t> &h_lrate,
-                                  bool profile, StageTimes &st, std::string &err) {
+bool GpuEncoder::apply_thresholds(const Plan &plan, std::string &err) {
     const int nb = (int)plan.blocks.size();
     const int L = plan.rc.layers;
     ApplyArgs aa;
@@ -1396,19 +1440,33 @@ bool GpuEncoder::apply_thresholds(const Plan &plan, std::vector<uint8_t> &h_nl, 
     if (nb) hipLaunchKernelGGL(k_apply, dim3((nb + 255) / 256), dim3(256), 0, stream, aa);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[7], stream));
-    h_nl.resize((size_t)nb * L);
-    h_lrate.resize((size_t)nb * L);
-    if (nb) {
-        HIPCHECK(hipMemcpyAsync(h_nl.data(), nl.ptr, h_nl.size(), hipMemcpyDeviceToHost, stream));
-        HIPCHECK(hipMemcpyAsync(h_lrate.data(), lrate.ptr, sizeof(int32_t) * h_lrate.size(), hipMemcpyDeviceToHost,
-                                stream));
+    return true;
+}
+
+// tier-1 byte total (tile-split lossless budget); one host wait
+__global__ void __launch_bounds__(256) k_sum_lengths(int nblocks, const int32_t *lengths, int64_t *out) {
+    __shared__ int64_t part[256];
+    int64_t s = 0;
+    for (int b = threadIdx.x; b < nblocks; b += 256) s += lengths[b];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t tot = 0;
+        for (int i = 0; i < 256; i++) tot += part[i];
+        *out = tot;
     }
+}
+
+bool GpuEncoder::t1_totals(const Plan &plan, int64_t &bytes, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    if (!ensure<int64_t>(hist, kSlopeBins, err)) return false;
+    if (!h_tot) HIPCHECK(hipHostMalloc((void **)&h_tot, 4 * sizeof(int64_t), hipHostMallocDefault));
+    hipLaunchKernelGGL(k_sum_lengths, dim3(1), dim3(256), 0, stream, (int)plan.blocks.size(),
+                       (const int32_t *)lengths.ptr, (int64_t *)hist.ptr);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(h_tot, hist.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     if (!host_wait(err)) return false;
-    if (profile) {
-        float t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[7]));
-        st.pcrd += t;
-    }
+    bytes = h_tot[0];
     return true;
 }
 
@@ -1421,51 +1479,6 @@ bool GpuEncoder::segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum
         HIPCHECK(hipMemcpyAsync(cum.data(), segcum.ptr, sizeof(int64_t) * nseg, hipMemcpyDeviceToHost, stream));
     }
     if (!host_wait(err)) return false;
-    return true;
-}
-
-bool GpuEncoder::gather(const Plan &plan, const std::vector<int32_t> &final_len,
-                        const std::vector<uint64_t> &offsets, uint64_t total, const uint8_t **host_data,
-                        bool profile, StageTimes &st, std::string &err) {
-    HIPCHECK(hipSetDevice(device));
-    const int nb = (int)plan.blocks.size();
-    if (!ensure<uint64_t>(dstoff, nb, err)) return false;
-    if (!ensure<uint8_t>(packed, total, err)) return false;
-    if (!ensure<int32_t>(lengths, nb, err)) return false;
-    if (h_packed_cap < total) {
-        if (h_packed) (void)hipHostFree(h_packed);
-        h_packed = nullptr;
-        h_packed_cap = 0;
-        size_t cap = total + total / 4 + 4096;
-        HIPCHECK(hipHostMalloc((void **)&h_packed, cap, hipHostMallocDefault));
-        h_packed_cap = cap;
-    }
-    HIPCHECK(hipEventRecord(ev[8], stream));
-    HIPCHECK(hipMemcpyAsync(dstoff.ptr, offsets.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(lengths.ptr, final_len.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, stream));
-    if (nb) hipLaunchKernelGGL(k_compact, dim3(nb), dim3(256), 0, stream, (const BlockDesc *)blocks.ptr,
-                               (const uint8_t *)t1out.ptr, (const uint64_t *)dstoff.ptr,
-                               (const int32_t *)lengths.ptr, (uint8_t *)packed.ptr);
-    HIPCHECK(hipGetLastError());
-    if (total) HIPCHECK(hipMemcpyAsync(h_packed, packed.ptr, total, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipEventRecord(ev[9], stream));
-    if (!host_wait(err)) return false;
-    if (profile) {
-        float t;
-        HIPCHECK(hipEventElapsedTime(&t, ev[8], ev[9]));
-        st.d2h += t;
-    }
-    *host_data = h_packed;
-    return true;
-}
-
-bool GpuEncoder::t1_total_bytes(int64_t &bytes, int64_t &passes) const {
-    bytes = 0;
-    passes = 0;
-    for (size_t i = 0; i < h_lengths.size(); i++) {
-        bytes += h_lengths[i];
-        passes += h_npasses[i];
-    }
     return true;
 }
 

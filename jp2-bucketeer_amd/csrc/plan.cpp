@@ -281,9 +281,26 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
     return true;
 }
 
-void split_tile_rows(int nty, int rank, int world, int &tr0, int &tr1) {
-    tr0 = (int)((int64_t)nty * rank / world);
-    tr1 = (int)((int64_t)nty * (rank + 1) / world);
+std::vector<int> flush_stripe_ends(int nty, int tile_h, int h, int period) {
+    std::vector<int> ends;
+    int64_t next = period;
+    for (int ty = 0; ty < nty; ty++) {
+        const int64_t bottom = std::min<int64_t>((int64_t)(ty + 1) * tile_h, h);
+        if (period <= 0 || bottom >= next || ty == nty - 1) {
+            ends.push_back(ty + 1);
+            if (period > 0)
+                while (next <= bottom) next += period;
+        }
+    }
+    return ends;
+}
+
+void split_tile_rows(int nty, int tile_h, int h, int period, int rank, int world, int &tr0, int &tr1) {
+    const std::vector<int> ends = flush_stripe_ends(nty, tile_h, h, period);
+    const int64_t ns = (int64_t)ends.size();
+    const int s0 = (int)(ns * rank / world), s1 = (int)(ns * (rank + 1) / world);
+    tr0 = s0 > 0 ? ends[s0 - 1] : 0;
+    tr1 = s1 > 0 ? ends[s1 - 1] : 0;
 }
 
 void make_subplan(const Plan &full, int tr0, int tr1, Plan &S) {

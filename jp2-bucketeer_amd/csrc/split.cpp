@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "jp2hip.h"
+#include "jp2hip_internal.h"
 
 namespace {
 
@@ -38,13 +39,13 @@ int64_t bytes_at_least(const uint64_t *keys, const int64_t *cum, int64_t n, uint
 
 extern "C" {
 
-void jp2hip_split_rows(int32_t height, int32_t tile_h, int32_t rank, int32_t world, int32_t *row0,
-                       int32_t *row1) {
-    const int32_t nty = tile_h > 0 ? (height + tile_h - 1) / tile_h : 0;
-    const int32_t tr0 = world > 0 ? (int32_t)((int64_t)nty * rank / world) : 0;
-    const int32_t tr1 = world > 0 ? (int32_t)((int64_t)nty * (rank + 1) / world) : 0;
-    if (row0) *row0 = std::min(height, tr0 * tile_h);
-    if (row1) *row1 = std::min(height, tr1 * tile_h);
+void jp2hip_split_rows(int32_t height, int32_t tile_h, int32_t flush_period, int32_t rank, int32_t world,
+                       int32_t *row0, int32_t *row1) {
+    int tr0 = 0, tr1 = 0;
+    if (tile_h > 0 && height > 0 && world > 0 && rank >= 0 && rank < world)
+        jp2hip::split_tile_rows((height + tile_h - 1) / tile_h, tile_h, height, flush_period, rank, world, tr0, tr1);
+    if (row0) *row0 = (int32_t)std::min<int64_t>(height, (int64_t)tr0 * tile_h);
+    if (row1) *row1 = (int32_t)std::min<int64_t>(height, (int64_t)tr1 * tile_h);
 }
 
 int jp2hip_split_thresholds(const uint64_t *keys, const int64_t *cum, int64_t nseg, const int64_t *budgets,

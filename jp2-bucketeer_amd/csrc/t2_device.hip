@@ -1,0 +1,608 @@
+// t2_device.hip -- tier-2 on the GPU (ISO/IEC 15444-1 Annex B.9-B.10, A.4, A.7.3):
+// packet headers, tile-part sizes and the code-stream itself, written in HBM.
+//
+// Structure produced for the Bucketeer recipe (KakaduConverter.java:38-44):
+// RPCL packets, SOP before and EPH after every packet header, one tile-part
+// per resolution (ORGtparts=R) with a PLT marker (ORGgen_plt=yes), tile-parts
+// in -flush_period stripe order (t2_tables, test.jpx).  The byte layout is
+// the oracle's (oracle/jp2_oracle.c encode_packet / write_codestream).
+//
+// Parallel structure.  A precinct's L packets share state (tag trees, each
+// block's Lblock and inclusion layer), so one lane codes one precinct's
+// packets in order; precincts are independent (C2: 2 880 per image, C5:
+// 51 153).  Sizing and emission run the same coder (template EMIT):
+//   k_t2_code<false>  header bytes + packet lengths        (every rate pass)
+//   k_t2_tparts       Psot / PLT bytes per tile-part       (every rate pass)
+//   k_t2_total        stream offsets, sums for the host    (every rate pass)
+//   k_t2_tp_emit      SOT + PLT + SOD, packet offsets      (final pass)
+//   k_t2_code<true>   SOP + header + EPH, body offsets     (final pass)
+//   k_t2_copy         code-block bytes into the bodies     (final pass)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device_common.h"
+#include "gpu_encoder.h"
+
+namespace jp2hip {
+
+#define HIPCHECK(x)                                                                    \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            err = std::string(#x) + ": " + hipGetErrorString(e_);                      \
+            return false;                                                              \
+        }                                                                              \
+    } while (0)
+
+struct T2Args {
+    const PrecDesc *prec;
+    int nprec;
+    const TpDesc *tps;
+    int ntp;
+    const BlockDesc *blocks;
+    const uint8_t *P;       // coded planes per block
+    const uint8_t *nl;      // [block][L] cumulative passes
+    const int32_t *lrate;   // [block][L] cumulative bytes
+    int L, sop, eph, plt;
+    uint32_t *tt;           // tag-tree nodes: value | low << 8 | known << 16
+    int8_t *lblock, *incl;  // per block coding state
+    uint32_t *pk_len;       // [nprec * L] SOP + header + EPH + body
+    uint32_t *tp_len;       // [ntp] Psot
+    uint32_t *tp_hdr;       // [ntp] SOT + PLT + SOD
+    uint64_t *tp_off;       // [ntp] offset of the tile-part in the part
+    uint64_t *pk_off;       // [nprec * L] offset of the packet (its SOP) in `out`
+    uint64_t *blkdst;       // [block][L] offset of the block's layer-l bytes in `out`
+    uint8_t *out;           // the part: tile-parts from byte `base`
+    uint64_t base;
+};
+
+// Packet-header bit writer (B.10.1): MSB first, a byte after 0xFF carries 7
+// bits; a header never ends in 0xFF (t2.cpp Bits, oracle bw_*).
+template <bool EMIT>
+struct DevBits {
+    uint8_t *p;
+    uint32_t nbytes;
+    uint64_t acc;
+    int n, cap;
+    __device__ __forceinline__ void init(uint8_t *dst) { p = dst; nbytes = 0; acc = 0; n = 0; cap = 8; }
+    __device__ __forceinline__ void put(uint32_t val, int nb) {
+        acc = (acc << nb) | val;
+        n += nb;
+        while (n >= cap) {
+            n -= cap;
+            const uint32_t byte = (uint32_t)(acc >> n) & ((1u << cap) - 1u);
+            if (EMIT) p[nbytes] = (uint8_t)byte;
+            nbytes++;
+            cap = (byte == 0xFF) ? 7 : 8;
+        }
+    }
+    __device__ __forceinline__ void bit(int b) { put((uint32_t)(b & 1), 1); }
+    __device__ __forceinline__ void flush() {
+        if (n) {
+            const uint32_t byte = (uint32_t)(acc << (cap - n)) & ((1u << cap) - 1u);
+            if (EMIT) p[nbytes] = (uint8_t)byte;
+            nbytes++;
+        } else if (cap == 7) {
+            if (EMIT) p[nbytes] = 0;
+            nbytes++;
+        }
+        cap = 8;
+        n = 0;
+        acc = 0;
+    }
+};
+
+// Tag trees (B.10.2).  A tree over a w x h leaf grid is stored level by
+// level (raster inside a level, level sizes ceil(w / 2^k) x ceil(h / 2^k)),
+// each node one word: value | low << 8 | known << 16.  Geometry is recomputed
+// from (w, h) on every walk, so a lane keeps no arrays (no scratch memory).
+__device__ __forceinline__ int tree_size(int w, int h) {
+    int n = 0;
+    for (;;) {
+        n += w * h;
+        if (w == 1 && h == 1) return n;
+        w = (w + 1) >> 1;
+        h = (h + 1) >> 1;
+    }
+}
+
+__device__ __forceinline__ void tree_set(uint32_t *nd, int w, int h, int leaf, int v) {
+    int x = leaf % w, y = leaf / w, base = 0;
+    for (;;) {
+        uint32_t &e = nd[base + y * w + x];
+        if ((int)(e & 0xFFu) <= v) return;
+        e = (e & ~0xFFu) | (uint32_t)v;
+        if (w == 1 && h == 1) return;
+        base += w * h;
+        w = (w + 1) >> 1;
+        h = (h + 1) >> 1;
+        x >>= 1;
+        y >>= 1;
+    }
+}
+
+// Codes leaf `leaf` against `threshold`, root first (t2.cpp / oracle tt_encode).
+template <bool EMIT>
+__device__ __forceinline__ void tree_encode(uint32_t *nd, int w, int h, int leaf, int threshold, DevBits<EMIT> &bw) {
+    const int lx = leaf % w, ly = leaf / w;
+    int nlev = 1;
+    for (int cw = w, ch = h; cw != 1 || ch != 1; cw = (cw + 1) >> 1, ch = (ch + 1) >> 1) nlev++;
+    int low = 0;
+    for (int k = nlev - 1; k >= 0; k--) {
+        int base = 0, cw = w, ch = h;
+        for (int j = 0; j < k; j++) {
+            base += cw * ch;
+            cw = (cw + 1) >> 1;
+            ch = (ch + 1) >> 1;
+        }
+        uint32_t &e = nd[base + (ly >> k) * cw + (lx >> k)];
+        const int value = (int)(e & 0xFFu);
+        int nlow = (int)((e >> 8) & 0xFFu);
+        bool known = (e >> 16) & 1u;
+        if (low > nlow) nlow = low;
+        else low = nlow;
+        while (low < threshold) {
+            if (low >= value) {
+                if (!known) {
+                    bw.bit(1);
+                    known = true;
+                }
+                break;
+            }
+            bw.bit(0);
+            low++;
+        }
+        e = (uint32_t)value | ((uint32_t)low << 8) | (known ? (1u << 16) : 0u);
+    }
+}
+
+__device__ __forceinline__ int dev_floor_log2(int v) { return 31 - __clz(v); }
+
+// One precinct's L packets (oracle encode_packet).  Tag-tree nodes live in
+// the lane's LDS slot when they fit (the recipe's precincts: at most 2 x 2
+// blocks per band, 30 nodes), else in the global scratch.
+constexpr int kLdsNodes = 48;
+
+template <bool EMIT>
+__global__ void __launch_bounds__(64) k_t2_code(T2Args a) {
+    __shared__ uint32_t lds_nodes[64 * kLdsNodes];
+    const int pi = blockIdx.x * 64 + threadIdx.x;
+    if (pi >= a.nprec) return;
+    const PrecDesc d = a.prec[pi];
+    const int L = a.L;
+    int nodes = 0;
+#pragma unroll
+    for (int bi = 0; bi < 3; bi++)
+        if (bi < d.nb && d.ncw[bi] && d.nch[bi]) nodes += 2 * tree_size(d.ncw[bi], d.nch[bi]);
+    uint32_t *tt = nodes <= kLdsNodes ? lds_nodes + threadIdx.x * kLdsNodes : a.tt + d.tt_off;
+    for (int i = 0; i < nodes; i++) tt[i] = 0xFFu;  // value 255 = unset, low 0, not known
+    // node offsets of the (inclusion, zero bit-plane) trees of each band
+    int toff[3];
+    {
+        int o = 0;
+#pragma unroll
+        for (int bi = 0; bi < 3; bi++) {
+            toff[bi] = o;
+            if (bi < d.nb && d.ncw[bi] && d.nch[bi]) o += 2 * tree_size(d.ncw[bi], d.nch[bi]);
+        }
+    }
+#pragma unroll
+    for (int bi = 0; bi < 3; bi++) {
+        const int w = bi < d.nb ? d.ncw[bi] : 0, h = bi < d.nb ? d.nch[bi] : 0;
+        if (!w || !h) continue;
+        uint32_t *ti = tt + toff[bi], *tz = ti + tree_size(w, h);
+        for (int k = 0; k < w * h; k++) {
+            const int b = d.first[bi] + k;
+            a.lblock[b] = 3;
+            a.incl[b] = -1;
+            const uint8_t *nb = a.nl + (size_t)b * L;
+            int first = L;
+            for (int l = 0; l < L; l++)
+                if (nb[l] > 0) { first = l; break; }
+            tree_set(ti, w, h, k, first);
+            tree_set(tz, w, h, k, a.blocks[b].Mb - a.P[b]);
+        }
+    }
+    const uint32_t fixed = (a.sop ? 6u : 0u) + (a.eph ? 2u : 0u);
+    for (int l = 0; l < L; l++) {
+        const size_t pk = (size_t)pi * L + l;
+        bool nonempty = false;
+#pragma unroll
+        for (int bi = 0; bi < 3; bi++) {
+            const int nk = bi < d.nb ? d.ncw[bi] * d.nch[bi] : 0;
+            for (int k = 0; k < nk && !nonempty; k++) {
+                const uint8_t *nb = a.nl + (size_t)(d.first[bi] + k) * L;
+                if (nb[l] > (l ? nb[l - 1] : 0)) nonempty = true;
+            }
+        }
+        uint8_t *o = nullptr;
+        if (EMIT) {
+            o = a.out + a.pk_off[pk];
+            if (a.sop) {
+                const uint32_t ns = (uint32_t)(d.nsop0 + l) & 0xFFFFu;
+                o[0] = 0xFF; o[1] = 0x91; o[2] = 0; o[3] = 4; o[4] = (uint8_t)(ns >> 8); o[5] = (uint8_t)ns;
+                o += 6;
+            }
+        }
+        DevBits<EMIT> w;
+        w.init(o);
+        w.bit(nonempty ? 1 : 0);
+        uint32_t body = 0;
+        if (nonempty) {
+#pragma unroll
+            for (int bi = 0; bi < 3; bi++) {
+                const int cw = bi < d.nb ? d.ncw[bi] : 0, ch = bi < d.nb ? d.nch[bi] : 0;
+                if (!cw || !ch) continue;
+                uint32_t *ti = tt + toff[bi], *tz = ti + tree_size(cw, ch);
+                for (int k = 0; k < cw * ch; k++) {
+                    const int b = d.first[bi] + k;
+                    const uint8_t *nb = a.nl + (size_t)b * L;
+                    const int n = nb[l] - (l ? nb[l - 1] : 0);
+                    const bool first_time = a.incl[b] < 0;
+                    if (first_time) tree_encode(ti, cw, ch, k, l + 1, w);
+                    else w.bit(n > 0 ? 1 : 0);
+                    if (n <= 0) continue;
+                    if (first_time) {
+                        tree_encode(tz, cw, ch, k, 1 << 20, w);
+                        a.incl[b] = (int8_t)l;
+                    }
+                    // number of passes, Table B.4
+                    if (n == 1) w.bit(0);
+                    else if (n == 2) w.put(2u, 2);
+                    else if (n <= 5) w.put((3u << 2) | (uint32_t)(n - 3), 4);
+                    else if (n <= 36) w.put((15u << 5) | (uint32_t)(n - 6), 9);
+                    else w.put((511u << 7) | (uint32_t)(n - 37), 16);
+                    const int32_t *lr = a.lrate + (size_t)b * L;
+                    const int r0 = l ? lr[l - 1] : 0;
+                    const int len = lr[l] - r0;
+                    int lb = a.lblock[b];
+                    int nbits = lb + dev_floor_log2(n);
+                    while (len >= (1 << nbits)) { w.bit(1); lb++; nbits++; }
+                    a.lblock[b] = (int8_t)lb;
+                    w.bit(0);
+                    w.put((uint32_t)len, nbits);
+                    if (EMIT) a.blkdst[(size_t)b * L + l] = body;  // relative; the header length is added below
+                    body += (uint32_t)len;
+                }
+            }
+        }
+        w.flush();
+        if (EMIT) {
+            o += w.nbytes;
+            if (a.eph) { o[0] = 0xFF; o[1] = 0x92; o += 2; }
+            // body pieces start here, in block order
+            const uint64_t at = (uint64_t)(o - a.out);
+            if (nonempty)
+#pragma unroll
+                for (int bi = 0; bi < 3; bi++) {
+                    const int nk = bi < d.nb ? d.ncw[bi] * d.nch[bi] : 0;
+                    for (int k = 0; k < nk; k++) {
+                        const int b = d.first[bi] + k;
+                        const uint8_t *nb = a.nl + (size_t)b * L;
+                        if (nb[l] > (l ? nb[l - 1] : 0)) a.blkdst[(size_t)b * L + l] += at;
+                    }
+                }
+        } else {
+            a.pk_len[pk] = fixed + w.nbytes + body;
+        }
+    }
+}
+
+__device__ __forceinline__ int varint_len(uint32_t v) {
+    int k = 1;
+    while (v >>= 7) k++;
+    return k;
+}
+
+// Psot and SOT + PLT + SOD bytes of each tile-part (thread per tile-part)
+__global__ void __launch_bounds__(64) k_t2_tparts(T2Args a) {
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= a.ntp) return;
+    const TpDesc d = a.tps[t];
+    const size_t p0 = (size_t)d.prec0 * a.L, p1 = (size_t)(d.prec0 + d.nprec) * a.L;
+    uint64_t body = 0, plt = 0, seg = 0;
+    for (size_t i = p0; i < p1; i++) {
+        const uint32_t len = a.pk_len[i];
+        body += len;
+        if (a.plt) {
+            const uint64_t k = (uint64_t)varint_len(len);
+            if (i == p0 || seg + k > 65532) {
+                if (i != p0) plt += 5 + seg;
+                seg = 0;
+            }
+            seg += k;
+        }
+    }
+    if (a.plt && p1 > p0) plt += 5 + seg;
+    a.tp_hdr[t] = (uint32_t)(14 + plt);
+    a.tp_len[t] = (uint32_t)(14 + plt + body);
+}
+
+// One workgroup: tile-part offsets in code-stream order, and the sums the
+// host needs (part size, header bytes, bytes per layer, tier-1 totals).
+__global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
+                                                  const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
+                                                  const uint64_t *kc, T2Summary *sum) {
+    __shared__ uint64_t part[256];
+    __shared__ int64_t lay[256][kMaxLayers > 8 ? 8 : kMaxLayers];
+    const int tid = threadIdx.x;
+    const int chunk = (a.ntp + 255) / 256;
+    const int t0 = min(a.ntp, tid * chunk), t1 = min(a.ntp, t0 + chunk);
+    uint64_t s = 0, hdr = 0;
+    for (int t = t0; t < t1; t++) s += a.tp_len[t];
+    part[tid] = s;
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan of the 256 chunk sums
+        uint64_t acc = 0;
+        for (int i = 0; i < 256; i++) {
+            const uint64_t v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+        sum->part_bytes = (int64_t)acc;
+    }
+    __syncthreads();
+    uint64_t o = part[tid];
+    for (int t = t0; t < t1; t++) {
+        a.tp_off[t] = o;
+        o += a.tp_len[t];
+        hdr += a.tp_hdr[t];
+    }
+    // per-layer packet bytes (layers in groups of 8 through shared memory)
+    const size_t npk = (size_t)a.nprec * a.L;
+    for (int l0 = 0; l0 < a.L; l0 += 8) {
+        int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (size_t i = tid; i < npk; i += 256) {
+            const int l = (int)(i % a.L);
+            if (l >= l0 && l < l0 + 8) v[l - l0] += a.pk_len[i];
+        }
+        for (int k = 0; k < 8; k++) lay[tid][k] = v[k];
+        __syncthreads();
+        if (tid < 8 && l0 + tid < a.L) {
+            int64_t acc = 0;
+            for (int i = 0; i < 256; i++) acc += lay[i][tid];
+            sum->layer_bytes[l0 + tid] = acc;
+        }
+        __syncthreads();
+    }
+    // tier-1 totals
+    int64_t tb = 0, tp = 0;
+    int skipped = 0;
+    for (int b = tid; b < nblocks; b += 256) {
+        tb += lengths[b];
+        tp += npasses[b];
+        skipped |= pmin[b] > 0;
+    }
+    part[tid] = (uint64_t)tb;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t acc = 0;
+        for (int i = 0; i < 256; i++) acc += part[i];
+        sum->t1_bytes = (int64_t)acc;
+    }
+    __syncthreads();
+    part[tid] = (uint64_t)tp | ((uint64_t)skipped << 63);
+    lay[tid][0] = (int64_t)hdr;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t acc = 0;
+        int64_t h = 0;
+        int sk = 0;
+        for (int i = 0; i < 256; i++) {
+            acc += part[i] & ~(1ull << 63);
+            sk |= (int)(part[i] >> 63);
+            h += lay[i][0];
+        }
+        sum->coded_passes = (int64_t)acc;
+        sum->skipped = sk;
+        sum->tp_hdr_bytes = h;
+        sum->err = *t1err;
+        for (int l = 0; l < a.L; l++) sum->kc[l] = kc ? kc[l] : 0ull;
+    }
+}
+
+// SOT + PLT + SOD of each tile-part, and where each of its packets starts
+__global__ void __launch_bounds__(64) k_t2_tp_emit(T2Args a) {
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= a.ntp) return;
+    const TpDesc d = a.tps[t];
+    uint8_t *p = a.out + a.base + a.tp_off[t];
+    const uint32_t psot = a.tp_len[t];
+    p[0] = 0xFF; p[1] = 0x90; p[2] = 0; p[3] = 10;
+    p[4] = (uint8_t)(d.tile >> 8); p[5] = (uint8_t)d.tile;
+    p[6] = (uint8_t)(psot >> 24); p[7] = (uint8_t)(psot >> 16); p[8] = (uint8_t)(psot >> 8); p[9] = (uint8_t)psot;
+    p[10] = (uint8_t)d.tpsot;
+    p[11] = (uint8_t)d.tnsot;
+    p += 12;
+    const size_t p0 = (size_t)d.prec0 * a.L, p1 = (size_t)(d.prec0 + d.nprec) * a.L;
+    if (a.plt) {  // PLT segments (A.7.3): lengths as 7-bit groups, <= 65532 bytes each
+        size_t i = p0;
+        int z = 0;
+        while (i < p1) {
+            uint8_t *hdr = p;
+            p += 5;
+            uint32_t seg = 0;
+            while (i < p1) {
+                const uint32_t len = a.pk_len[i];
+                const int k = varint_len(len);
+                if (seg + (uint32_t)k > 65532) break;
+                for (int j = k - 1; j >= 0; j--) *p++ = (uint8_t)(((len >> (7 * j)) & 0x7F) | (j ? 0x80 : 0));
+                seg += (uint32_t)k;
+                i++;
+            }
+            hdr[0] = 0xFF; hdr[1] = 0x58;
+            hdr[2] = (uint8_t)((3 + seg) >> 8); hdr[3] = (uint8_t)(3 + seg);
+            hdr[4] = (uint8_t)z++;
+        }
+    }
+    p[0] = 0xFF; p[1] = 0x93;
+    p += 2;
+    uint64_t o = (uint64_t)(p - a.out);
+    for (size_t i = p0; i < p1; i++) {
+        a.pk_off[i] = o;
+        o += a.pk_len[i];
+    }
+}
+
+// code-block bytes into the packet bodies: one wave per block, its layer
+// pieces in turn; bytes move in 16-byte vector loads/stores where source and
+// destination are both aligned, else one byte per lane
+__global__ void __launch_bounds__(256) k_t2_copy(T2Args a, int nblocks, const uint8_t *t1out) {
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= nblocks) return;
+    const int L = a.L;
+    const uint8_t *nb = a.nl + (size_t)b * L;
+    const int32_t *lr = a.lrate + (size_t)b * L;
+    const uint8_t *src0 = t1out + a.blocks[b].out_off;
+    for (int l = 0; l < L; l++) {
+        if (nb[l] <= (l ? nb[l - 1] : 0)) continue;
+        const int r0 = l ? lr[l - 1] : 0, n = lr[l] - r0;
+        const uint8_t *s = src0 + r0;
+        uint8_t *d = a.out + a.blkdst[(size_t)b * L + l];
+        const int head = (int)((16 - ((uintptr_t)d & 15)) & 15);
+        if ((((uintptr_t)s ^ (uintptr_t)d) & 15) == 0 && n >= head + 16) {
+            if (lane < head) d[lane] = s[lane];
+            const int nv = (n - head) >> 4;
+            const uint4 *sv = (const uint4 *)(s + head);
+            uint4 *dv = (uint4 *)(d + head);
+            for (int i = lane; i < nv; i += 64) dv[i] = sv[i];
+            for (int i = head + (nv << 4) + lane; i < n; i += 64) d[i] = s[i];
+        } else {
+            for (int i = lane; i < n; i += 64) d[i] = s[i];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Host side (GpuEncoder)
+// --------------------------------------------------------------------------
+template <typename T>
+static bool ensure_t2(DevBuf &b, size_t count, std::string &err) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return true;
+    if (b.ptr) (void)hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+    const size_t alloc = bytes + bytes / 8;
+    const hipError_t e = hipMalloc(&b.ptr, alloc);
+    if (e != hipSuccess) {
+        err = std::string("hipMalloc(") + std::to_string(alloc) + "): " + hipGetErrorString(e);
+        return false;
+    }
+    b.bytes = alloc;
+    return true;
+}
+
+T2Args GpuEncoder::t2_args(const Plan &plan) const {
+    T2Args a;
+    std::memset(&a, 0, sizeof a);
+    a.prec = (const PrecDesc *)t2prec.ptr;
+    a.nprec = t2_nprec;
+    a.tps = (const TpDesc *)t2tp.ptr;
+    a.ntp = t2_ntp;
+    a.blocks = (const BlockDesc *)blocks.ptr;
+    a.P = (const uint8_t *)P.ptr;
+    a.nl = (const uint8_t *)nl.ptr;
+    a.lrate = (const int32_t *)lrate.ptr;
+    a.L = plan.rc.layers;
+    a.sop = plan.rc.sop;
+    a.eph = plan.rc.eph;
+    a.plt = plan.rc.plt;
+    a.tt = (uint32_t *)t2tt.ptr;
+    a.lblock = (int8_t *)t2lblock.ptr;
+    a.incl = (int8_t *)t2incl.ptr;
+    a.pk_len = (uint32_t *)t2pklen.ptr;
+    a.tp_len = (uint32_t *)t2tplen.ptr;
+    a.tp_hdr = (uint32_t *)t2tphdr.ptr;
+    a.tp_off = (uint64_t *)t2tpoff.ptr;
+    a.pk_off = (uint64_t *)t2pkoff.ptr;
+    a.blkdst = (uint64_t *)t2blkdst.ptr;
+    a.out = (uint8_t *)t2out.ptr;
+    return a;
+}
+
+bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    const int nb = (int)plan.blocks.size();
+    const int L = plan.rc.layers;
+    t2_nprec = (int)T.prec.size();
+    t2_ntp = (int)T.tp.size();
+    const size_t npk = (size_t)t2_nprec * L;
+    if (!ensure_t2<PrecDesc>(t2prec, T.prec.size(), err) || !ensure_t2<TpDesc>(t2tp, T.tp.size(), err) ||
+        !ensure_t2<uint32_t>(t2tt, (size_t)T.tt_nodes, err) || !ensure_t2<int8_t>(t2lblock, nb, err) ||
+        !ensure_t2<int8_t>(t2incl, nb, err) || !ensure_t2<uint32_t>(t2pklen, npk, err) ||
+        !ensure_t2<uint64_t>(t2pkoff, npk, err) || !ensure_t2<uint32_t>(t2tplen, T.tp.size(), err) ||
+        !ensure_t2<uint32_t>(t2tphdr, T.tp.size(), err) || !ensure_t2<uint64_t>(t2tpoff, T.tp.size(), err) ||
+        !ensure_t2<uint64_t>(t2blkdst, (size_t)nb * L, err) || !ensure_t2<T2Summary>(t2sum, 1, err))
+        return false;
+    if (!h_sum) HIPCHECK(hipHostMalloc((void **)&h_sum, sizeof(T2Summary), hipHostMallocDefault));
+    if (!h_tot) HIPCHECK(hipHostMalloc((void **)&h_tot, 4 * sizeof(int64_t), hipHostMallocDefault));
+    if (t2_nprec) HIPCHECK(hipMemcpyAsync(t2prec.ptr, T.prec.data(), sizeof(PrecDesc) * T.prec.size(),
+                                          hipMemcpyHostToDevice, stream));
+    if (t2_ntp) HIPCHECK(hipMemcpyAsync(t2tp.ptr, T.tp.data(), sizeof(TpDesc) * T.tp.size(), hipMemcpyHostToDevice,
+                                        stream));
+    return true;
+}
+
+bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,
+                         std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    const int nb = (int)plan.blocks.size();
+    T2Args a = t2_args(plan);
+    HIPCHECK(hipEventRecord(ev[8], stream));
+    if (t2_nprec) hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
+    if (t2_ntp) hipLaunchKernelGGL(k_t2_tparts, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
+                       (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
+                       with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
+                       (T2Summary *)t2sum.ptr);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(h_sum, t2sum.ptr, sizeof(T2Summary), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipEventRecord(ev[9], stream));
+    if (!host_wait(err)) return false;
+    sum = *h_sum;
+    if (profile) {
+        float t;
+        HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[7]));
+        st.pcrd += t;
+        HIPCHECK(hipEventElapsedTime(&t, ev[8], ev[9]));
+        st.t2 += t;
+    }
+    return true;
+}
+
+bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
+                         StageTimes &st, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    const int nb = (int)plan.blocks.size();
+    if (!ensure_t2<uint8_t>(t2out, base + part_bytes, err)) return false;
+    T2Args a = t2_args(plan);
+    a.base = base;
+    HIPCHECK(hipEventRecord(ev[8], stream));
+    if (t2_ntp) hipLaunchKernelGGL(k_t2_tp_emit, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
+    if (t2_nprec) hipLaunchKernelGGL(k_t2_code<true>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
+    if (nb) hipLaunchKernelGGL(k_t2_copy, dim3((nb + 3) / 4), dim3(256), 0, stream, a, nb, (const uint8_t *)t1out.ptr);
+    HIPCHECK(hipGetLastError());
+    // host_dst is pinned (api.cpp out_alloc): an async D2H on this context's
+    // stream (a copy into pageable memory goes through the runtime's shared
+    // staging path, which serialises the contexts)
+    if (part_bytes)
+        HIPCHECK(hipMemcpyAsync(host_dst, (const uint8_t *)t2out.ptr + base, part_bytes, hipMemcpyDeviceToHost, stream));
+    if (profiled)  // k_t1_mq's execution span, for collect_profile()
+        HIPCHECK(hipMemcpyAsync(h_tot + 2, mqspan.ptr, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipEventRecord(ev[9], stream));
+    if (!host_wait(err)) return false;
+    if (profile) {
+        float t;
+        HIPCHECK(hipEventElapsedTime(&t, ev[8], ev[9]));
+        st.d2h += t;
+    }
+    return true;
+}
+
+}  // namespace jp2hip

@@ -35,7 +35,8 @@ class Recipe(Structure):
                 ("progression", c_int32), ("sop", c_int32), ("eph", c_int32), ("plt", c_int32),
                 ("tparts_r", c_int32), ("guard_bits", c_int32), ("reversible", c_int32),
                 ("mct", c_int32), ("qstep", c_double), ("rate_bpp", c_double),
-                ("format", c_int32), ("comment", c_int32), ("slope_skip", c_int32)]
+                ("format", c_int32), ("comment", c_int32), ("slope_skip", c_int32),
+                ("flush_period", c_int32)]
 
 
 class Layout(Structure):
@@ -61,7 +62,7 @@ class Stats(Structure):
 
 
 # every symbol include/jp2hip.h declares
-EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_recipe_init",
+EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_device_count", "jp2hip_recipe_init",
            "jp2hip_create", "jp2hip_destroy", "jp2hip_encode_file", "jp2hip_encode_tiff",
            "jp2hip_tiff_layout", "jp2hip_encode_device", "jp2hip_free",
            # batch path (csrc/batch.cpp; bound in jp2hip.batch)
@@ -93,6 +94,7 @@ def lib():
     L.jp2hip_version.restype = c_char_p
     L.jp2hip_last_error.restype = c_char_p
     L.jp2hip_probe.restype = c_int
+    L.jp2hip_device_count.restype = c_int
     L.jp2hip_recipe_init.argtypes = [POINTER(Recipe), c_int]
     L.jp2hip_create.argtypes = [POINTER(c_void_p), POINTER(Config)]
     L.jp2hip_destroy.argtypes = [c_void_p]
@@ -106,7 +108,7 @@ def lib():
                                        POINTER(Recipe), POINTER(POINTER(c_uint8)),
                                        POINTER(c_size_t), POINTER(Stats)]
     L.jp2hip_free.argtypes = [c_void_p]
-    L.jp2hip_split_rows.argtypes = [c_int32, c_int32, c_int32, c_int32, POINTER(c_int32),
+    L.jp2hip_split_rows.argtypes = [c_int32, c_int32, c_int32, c_int32, c_int32, POINTER(c_int32),
                                     POINTER(c_int32)]
     L.jp2hip_split_rows.restype = None
     L.jp2hip_encode_device_split.argtypes = [c_void_p, c_void_p, c_size_t, POINTER(Layout), c_int,
@@ -130,6 +132,11 @@ def version() -> str:
 
 def probe() -> bool:
     return bool(lib().jp2hip_probe())
+
+
+def device_count() -> int:
+    """gfx950 devices visible to libjp2hip (0 without a GPU)."""
+    return int(lib().jp2hip_device_count())
 
 
 def recipe(conversion: int, **overrides) -> Recipe:

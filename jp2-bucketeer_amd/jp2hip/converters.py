@@ -97,7 +97,8 @@ class OpenJPEGConverter(Converter):
 
 
 class GpuConverter(Converter):
-    """MI355X converter: libjp2hip in-process, one context per visible GPU.
+    """MI355X converter: libjp2hip in-process, a pool of contexts (images in
+    flight) on every visible gfx950 device.
 
     Safe for concurrent callers (the reference runs one ImageWorkerVerticle
     thread, MainVerticle.java:229-231; raising that count gives each call its
@@ -106,17 +107,39 @@ class GpuConverter(Converter):
 
     WORKING_DIR_NAME = "jp2hip"
 
-    def __init__(self, devices: list[int] | None = None, host_threads: int = 0):
+    def __init__(self, devices: list[int] | None = None, host_threads: int = 0, per_gpu: int = 1):
         self.tmp_dir = Path(tempfile.gettempdir()) / self.WORKING_DIR_NAME
+        self._pool, self._free = [], []
+        self._cv = threading.Condition()
+        self.unavailable = None  # reason every convert() fails with (GPU absent / init failed)
         try:
             self.tmp_dir.mkdir(parents=True, exist_ok=True)
         except OSError as e:  # KakaduConverter.java:48-52 throws BUCKETEER_163 here
             raise IOError(BUCKETEER_002.format(self.tmp_dir)) from e
         if devices is None:
-            devices = [0]
-        self._pool = [_lib.Encoder(d, host_threads) for d in devices]
+            devices = list(range(_lib.device_count()))
+        try:
+            self._pool = [_lib.Encoder(d, host_threads) for _ in range(max(1, per_gpu)) for d in devices]
+        except _lib.Jp2hipError as e:
+            for enc in self._pool:
+                enc.close()
+            self._pool = []
+            raise IOError(BUCKETEER_001.format(f"(GPU converter init: {e})")) from e
+        if not self._pool:
+            raise IOError(BUCKETEER_001.format("(no gfx950 device)"))
         self._free = list(self._pool)
-        self._cv = threading.Condition()
+
+    @classmethod
+    def unavailable_converter(cls, reason: str) -> "GpuConverter":
+        """A GpuConverter whose convert() raises IOError(BUCKETEER_001 ...):
+        what ConverterFactory hands out when the GPU cannot be used and Kakadu
+        is absent, so ImageWorkerVerticle's IOException handler (:106) answers
+        the event-bus message instead of an unchecked exception escaping it."""
+        c = cls.__new__(cls)
+        c.tmp_dir = Path(tempfile.gettempdir()) / cls.WORKING_DIR_NAME
+        c._pool, c._free, c._cv = [], [], threading.Condition()
+        c.unavailable = reason
+        return c
 
     def _acquire(self):
         with self._cv:
@@ -130,6 +153,8 @@ class GpuConverter(Converter):
             self._cv.notify()
 
     def convert(self, image_id, tiff, conversion):
+        if self.unavailable is not None:
+            raise IOError(BUCKETEER_001.format(image_id) + f": {self.unavailable}")
         tiff = Path(tiff)
         jpx = self.tmp_dir / _jpx_name(image_id)
         if not os.access(jpx.parent, os.W_OK):
@@ -160,8 +185,14 @@ class ConverterFactory:
         with cls._lock:
             if klass is None:
                 if cls._converter is None:
+                    gpu = None
                     if cls.check_system_gpu():
-                        cls._converter = GpuConverter()
+                        try:
+                            gpu = GpuConverter()
+                        except IOError:
+                            gpu = None
+                    if gpu is not None:
+                        cls._converter = gpu
                     elif cls.check_system_kakadu():
                         cls._converter = KakaduConverter()
                     else:
@@ -174,10 +205,21 @@ class ConverterFactory:
             elif klass is OpenJPEGConverter:
                 cls._converter = OpenJPEGConverter()
             elif klass is GpuConverter:
-                if not cls.check_system_gpu():
-                    raise IOError(BUCKETEER_001.format("(no gfx950 device)"))
-                if not isinstance(cls._converter, GpuConverter):
-                    cls._converter = GpuConverter()
+                # never raises: GPU if usable, else Kakadu if present, else a
+                # converter whose convert() raises IOError (the caller's
+                # handler, ImageWorkerVerticle.java:106, catches only that)
+                if not (isinstance(cls._converter, GpuConverter) and cls._converter.unavailable is None):
+                    reason = "no gfx950 device"
+                    conv = None
+                    if cls.check_system_gpu():
+                        try:
+                            conv = GpuConverter()
+                        except IOError as e:
+                            reason = str(e)
+                    if conv is None:
+                        conv = KakaduConverter() if cls.check_system_kakadu() else \
+                            GpuConverter.unavailable_converter(reason)
+                    cls._converter = conv
             else:
                 raise ValueError(BUCKETEER_032)
             return cls._converter

@@ -80,6 +80,7 @@ void oracle_recipe_init(oracle_recipe *r, int lossless) {
     r->format = 2;
     r->comment = 1;
     r->slope_skip = 1;
+    r->flush_period = 1024;
 }
 
 /* precinct exponent for resolution r (0 = lowest) given Kakadu ordering */
@@ -868,6 +869,7 @@ typedef struct {
     int nall, capall;
     double compw[4];
     int skip;            /* slope prediction active (rate-driven + slope_skip) */
+    uint64_t K[32];      /* Kdu-Layer-Info slope keys per layer (0 = every pass) */
 } encoder;
 
 static void add_block(encoder *E, cblk *b) {
@@ -1197,8 +1199,11 @@ static int seg_cmp(const void *a, const void *b) {
 static uint64_t slope_key(double s) { uint64_t k; memcpy(&k, &s, 8); return k; }
 
 /* threshold key: smallest key K such that sum of dR over segments with
- * key >= K is <= budget (all segments of equal key taken together). */
-static uint64_t select_threshold(const seg *S, int ns, int64_t budget) {
+ * key >= K is <= budget (all segments of equal key taken together).
+ * *Kc (the Kdu-Layer-Info slope): the smallest key k with that sum <= budget,
+ * i.e. one above the first key not taken (0 if every segment is taken) --
+ * the value a tile-split encode's bisection finds, so both agree. */
+static uint64_t select_threshold(const seg *S, int ns, int64_t budget, uint64_t *Kc) {
     int64_t acc = 0;
     uint64_t K = UINT64_MAX;
     int i = 0;
@@ -1211,6 +1216,7 @@ static uint64_t select_threshold(const seg *S, int ns, int64_t budget) {
         K = S[i].key;
         i = j;
     }
+    *Kc = i < ns ? S[i].key + 1 : 0;
     return K;
 }
 
@@ -1318,7 +1324,26 @@ static void encode_packet(encoder *E, precinct *pr, int layer, bytes *out, int n
     }
 }
 
-static void write_main_header(encoder *E, bytes *o) {
+/* COM markers in Kakadu's layout (test.jpx): a
+ * version string, then "Kdu-Layer-Info" with one line per quality layer:
+ * log2 of the layer's slope threshold (squared error of samples normalised
+ * to unit range, summed over the image, per byte) and the code-stream bytes
+ * through that layer.  -192.0 marks "every pass" (the lossless last layer). */
+#define JP2HIP_COM_VERSION "jp2hip-v0.2.0"
+#define KDU_LAYER_HDR "Kdu-Layer-Info: log_2{Delta-D(squared-error)/Delta-L(bytes)}, L(bytes)\n"
+
+static double layer_log_slope(uint64_t K, int bits) {
+    if (K == 0) return -192.0;
+    if (K >= 0x7FF0000000000000ull) return 192.0; /* nothing included */
+    double s;
+    memcpy(&s, &K, 8);
+    double v = log2(s) - 2.0 * bits;
+    return v < -192.0 ? -192.0 : (v > 192.0 ? 192.0 : v);
+}
+
+static int layer_info_len(int layers) { return (int)strlen(KDU_LAYER_HDR) + 17 * layers; }
+
+static void write_main_header(encoder *E, bytes *o, const int64_t *layer_end) {
     const oracle_recipe *rc = E->rc;
     int L = rc->levels, nc = E->nc;
     bput16(o, 0xFF4F);
@@ -1359,12 +1384,34 @@ static void write_main_header(encoder *E, bytes *o) {
         else bput16(o, (q.eps << 11) | q.mu);
     }
     if (rc->comment) {
-        static const char msg[] = "jp2hip";
+        const char *ver = JP2HIP_COM_VERSION;
         bput16(o, 0xFF64);
-        bput16(o, 4 + (int)strlen(msg));
+        bput16(o, 4 + (int)strlen(ver));
+        bput16(o, 1); /* Rcom: Latin-1 text */
+        bput(o, ver, strlen(ver));
+        bput16(o, 0xFF64);
+        bput16(o, 4 + layer_info_len(rc->layers));
         bput16(o, 1);
-        bput(o, msg, strlen(msg));
+        bput(o, KDU_LAYER_HDR, strlen(KDU_LAYER_HDR));
+        for (int l = 0; l < rc->layers; l++) {
+            char line[64];
+            int n = snprintf(line, sizeof line, "%6.1f, %8.1e\n", layer_log_slope(E->K[l], E->bits),
+                             (double)(layer_end ? layer_end[l] : 0));
+            if (n != 17) { /* never for |slope| <= 192 and < 1e100 bytes */
+                memset(line, ' ', 16);
+                line[16] = '\n';
+            }
+            bput(o, line, 17);
+        }
     }
+}
+
+static size_t main_header_len(encoder *E) {
+    bytes h = {0, 0, 0};
+    write_main_header(E, &h, NULL);
+    size_t n = h.n;
+    free(h.d);
+    return n;
 }
 
 static void write_plt(bytes *o, const uint32_t *lens, int n) {
@@ -1390,20 +1437,50 @@ static void write_plt(bytes *o, const uint32_t *lens, int n) {
     }
 }
 
+/* Tile rows grouped the way "-flush_period P" flushes them
+ * (KakaduConverter.java:40): tile rows are pushed top to bottom, and a flush
+ * happens once the rows pushed reach the next multiple of P (and at the end
+ * of the image); each flush writes the tile-parts of the tile rows it
+ * completes.  ends[i] = one past the last tile row of stripe i.  P <= 0: one
+ * stripe per tile row.  For test.jpx (2000 rows, 512-row tiles, P = 1024):
+ * stripes {0, 1} and {2, 3}. */
+static int flush_stripes(int nty, int tile_h, int h, int period, int *ends) {
+    int n = 0;
+    int64_t next = period;
+    for (int ty = 0; ty < nty; ty++) {
+        int64_t bottom = (int64_t)(ty + 1) * tile_h;
+        if (bottom > h) bottom = h;
+        if (period <= 0 || bottom >= next || ty == nty - 1) {
+            ends[n++] = ty + 1;
+            if (period > 0)
+                while (next <= bottom) next += period;
+        }
+    }
+    return n;
+}
+
+/* Packets of every tile in RPCL order, one tile-part per resolution with
+ * ORGtparts=R (TNsot = 0 except on a tile's last tile-part, which carries the
+ * count, as test.jpx does), written stripe by stripe: within a flush stripe,
+ * resolution 0 of every tile, then resolution 1, ... (test.jpx: tiles 0-7
+ * res 0, tiles 0-7 res 1, ..., then tiles 8-15). */
 static void write_codestream(encoder *E, bytes *o) {
     const oracle_recipe *rc = E->rc;
-    int L = rc->levels;
+    int L = rc->levels, NL = rc->layers, ntiles = E->ntx * E->nty;
     reset_t2(E);
-    write_main_header(E, o);
-    for (int t = 0; t < E->ntx * E->nty; t++) {
+    bytes *tp = (bytes *)calloc((size_t)ntiles * (L + 1), sizeof(bytes));
+    int *ntp = (int *)calloc((size_t)ntiles, sizeof(int));
+    int64_t layer_bytes[32];
+    int64_t tp_hdr_bytes = 0;
+    memset(layer_bytes, 0, sizeof layer_bytes);
+    for (int t = 0; t < ntiles; t++) {
         tileinfo *T = &E->tiles[t];
-        int ntp = 0;
+        int nres = 0;
         for (int r = 0; r <= L; r++) {
             reslevel *rl = &T->tc[0].res[r];
-            if (rl->npx * rl->npy > 0) ntp++;
+            if (rl->npx * rl->npy > 0) nres++;
         }
-        int tp = 0, nsop = 0;
-        /* RPCL; with tparts_r each resolution is one tile-part */
+        int nsop = 0;
         bytes pk = {0, 0, 0};
         uint32_t *plens = NULL;
         int npk = 0, cappk = 0;
@@ -1413,7 +1490,7 @@ static void write_codestream(encoder *E, bytes *o) {
             for (int py = 0; py < r0->npy; py++)
                 for (int px = 0; px < r0->npx; px++)
                     for (int c = 0; c < E->nc; c++)
-                        for (int l = 0; l < rc->layers; l++) {
+                        for (int l = 0; l < NL; l++) {
                             precinct *pr = &T->tc[c].res[r].prec[py * r0->npx + px];
                             size_t before = pk.n;
                             encode_packet(E, pr, l, &pk, nsop++);
@@ -1422,20 +1499,23 @@ static void write_codestream(encoder *E, bytes *o) {
                                 plens = (uint32_t *)realloc(plens, sizeof(uint32_t) * (size_t)cappk);
                             }
                             plens[npk++] = (uint32_t)(pk.n - before);
+                            layer_bytes[l] += (int64_t)(pk.n - before);
                         }
             if (rc->tparts_r || r == L) {
-                size_t sot = o->n;
-                bput16(o, 0xFF90);
-                bput16(o, 10);
-                bput16(o, t);
-                bput32(o, 0);
-                bput8(o, tp);
-                bput8(o, rc->tparts_r ? ntp : 1);
-                if (rc->plt) write_plt(o, plens, npk);
-                bput16(o, 0xFF93);
-                bput(o, pk.d, pk.n);
-                bset32(o, sot + 6, (uint32_t)(o->n - sot));
-                tp++;
+                bytes *o2 = &tp[(size_t)t * (L + 1) + ntp[t]];
+                int k = ntp[t]++;
+                bput16(o2, 0xFF90);
+                bput16(o2, 10);
+                bput16(o2, t);
+                bput32(o2, 0);
+                bput8(o2, k);
+                /* TNsot: known (and written) on the tile's last tile-part */
+                bput8(o2, rc->tparts_r ? (k == nres - 1 ? nres : 0) : 1);
+                if (rc->plt) write_plt(o2, plens, npk);
+                bput16(o2, 0xFF93);
+                tp_hdr_bytes += (int64_t)o2->n;
+                bput(o2, pk.d, pk.n);
+                bset32(o2, 6, (uint32_t)o2->n);
                 pk.n = 0;
                 npk = 0;
             }
@@ -1443,6 +1523,23 @@ static void write_codestream(encoder *E, bytes *o) {
         free(pk.d);
         free(plens);
     }
+    /* Kdu-Layer-Info byte counts: the code-stream through each layer */
+    int64_t layer_end[32];
+    int64_t acc = (int64_t)main_header_len(E) + tp_hdr_bytes;
+    for (int l = 0; l < NL; l++) { acc += layer_bytes[l]; layer_end[l] = acc; }
+    write_main_header(E, o, layer_end);
+    int *ends = (int *)malloc(sizeof(int) * (size_t)(E->nty > 0 ? E->nty : 1));
+    int ns = flush_stripes(E->nty, rc->tile_h, E->h, rc->flush_period, ends);
+    for (int s = 0, ty0 = 0; s < ns; ty0 = ends[s++]) {
+        int t0 = ty0 * E->ntx, t1 = ends[s] * E->ntx;
+        for (int k = 0; k <= L; k++)
+            for (int t = t0; t < t1; t++)
+                if (k < ntp[t]) bput(o, tp[(size_t)t * (L + 1) + k].d, tp[(size_t)t * (L + 1) + k].n);
+    }
+    for (int i = 0; i < ntiles * (L + 1); i++) free(tp[i].d);
+    free(tp);
+    free(ntp);
+    free(ends);
     bput16(o, 0xFFD9);
 }
 
@@ -1597,7 +1694,9 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
     bytes cs = {0, 0, 0};
     if (rc->rate_bpp <= 0.0) {
         for (int l = 0; l < NL; l++) {
-            uint64_t K = (l == NL - 1) ? 0 : select_threshold(S, ns, total >> (NL - 1 - l));
+            uint64_t Kc = 0;
+            uint64_t K = (l == NL - 1) ? 0 : select_threshold(S, ns, total >> (NL - 1 - l), &Kc);
+            E.K[l] = Kc;
             for (int i = 0; i < E.nall; i++) {
                 cblk *b = E.all[i];
                 b->nl[l] = (l == NL - 1) ? b->npasses : passes_for_key(b, K);
@@ -1610,7 +1709,9 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         for (int it = 0; it < 8; it++) {
             if (budget < 0) budget = 0;
             for (int l = 0; l < NL; l++) {
-                uint64_t K = select_threshold(S, ns, budget >> (NL - 1 - l));
+                uint64_t Kc;
+                uint64_t K = select_threshold(S, ns, budget >> (NL - 1 - l), &Kc);
+                E.K[l] = Kc;
                 for (int i = 0; i < E.nall; i++) E.all[i]->nl[l] = passes_for_key(E.all[i], K);
             }
             cs.n = 0;

@@ -48,6 +48,10 @@ typedef struct oracle_recipe {
     int32_t slope_skip;        /* rate-driven only: skip bit-planes whose    */
                                /* predicted slope is far below the target's  */
                                /* (Kakadu-style slope prediction); 0 = off   */
+    int32_t flush_period;      /* -flush_period 1024: tile-parts are written */
+                               /* per stripe of tile rows that completes a   */
+                               /* flush (res 0 of every tile in the stripe,  */
+                               /* then res 1, ...); <= 0: tile by tile       */
 } oracle_recipe;
 
 /* Fill the Bucketeer recipe: lossless != 0 -> LOSSLESS_OPTIONS, else LOSSY. */

@@ -39,3 +39,16 @@ def encoder():
     enc = jp2hip.Encoder(0)
     yield enc
     enc.close()
+
+
+def golden_image(name, testjpx_pixels):
+    """Source pixels of a tests/golden/golden.json "lossy" case, by name."""
+    import imaging as im
+    table = {
+        "synth_rgb8_1024x1536": lambda: im.synth_rgb8(1024, 1536, seed=1234),
+        "testjpx_rgb_crop_1024": lambda: testjpx_pixels[:1024, :1024, :3].copy(),
+        "synth_gray16_1024": lambda: im.synth_u16(1024, 1024, comps=1, seed=5),
+        "c2_synth_rgb8_6000x4000": lambda: im.synth_rgb8(4000, 6000, seed=1234),
+        "c2_testjpx_tiled_6000x4000": lambda: im.testjpx_tiled(testjpx_pixels),
+    }
+    return table[name]()

@@ -21,16 +21,22 @@ def _rt():
 class DeviceBytes:
     """`data` copied into device memory of `device`; .ptr / .nbytes; free()."""
 
-    def __init__(self, data: bytes, device: int = 0):
+    def __init__(self, data, device: int = 0):
+        """`data`: bytes, or a C-contiguous numpy array (copied without an
+        intermediate bytes object)."""
         rt = _rt()
         if rt.hipSetDevice(device) != 0:
             raise RuntimeError("hipSetDevice failed")
-        self.nbytes = max(1, len(data))
+        if hasattr(data, "ctypes"):
+            n, src = int(data.nbytes), ctypes.c_void_p(data.ctypes.data)
+        else:
+            n, src = len(data), data
+        self.nbytes = max(1, n)
         p = ctypes.c_void_p()
         if rt.hipMalloc(ctypes.byref(p), self.nbytes) != 0:
             raise RuntimeError("hipMalloc failed")
         self.ptr = p.value
-        if data and rt.hipMemcpy(self.ptr, data, len(data), 1) != 0:  # hipMemcpyHostToDevice
+        if n and rt.hipMemcpy(self.ptr, src, n, 1) != 0:  # hipMemcpyHostToDevice
             self.free()
             raise RuntimeError("hipMemcpy failed")
 

@@ -66,7 +66,8 @@ def main():
         "siz": seg["ff51"].hex(), "cod": seg["ff52"].hex(), "qcd": seg["ff5c"].hex(),
         "sop": im.count_marker(tj, b"\xff\x91"),
         "tileparts": len(im.tile_parts(tj)),
-        "tp_order": [[t[0], t[2]] for t in im.tile_parts(tj)][:16],
+        # every tile-part: (Isot, TPsot, TNsot), in code-stream order
+        "tp_order": [[t[0], t[2], t[3]] for t in im.tile_parts(tj)],
         "min_size_assert": 30000,   # KakaduConverterTest.java:107
     }
     # lossy yardsticks: opj at exactly the oracle's output size
@@ -77,17 +78,33 @@ def main():
         ("synth_rgb8_1024x1536", im.synth_rgb8(1024, 1536, seed=1234), 8, 6),
         ("testjpx_rgb_crop_1024", pix[:1024, :1024, :3].copy(), 8, 6),
         ("synth_gray16_1024", im.synth_u16(1024, 1024, comps=1, seed=5), 16, 7),
+        # full-size C2 (BASELINE.json configs[1]) in both SURVEY.md 8(d)
+        # content classes; the oracle file's SHA-256 pins the GPU output
+        ("c2_synth_rgb8_6000x4000", im.synth_rgb8(4000, 6000, seed=1234), 8, 6),
+        ("c2_testjpx_tiled_6000x4000", im.testjpx_tiled(pix), 8, 6),
     ]:
         rc = ol.recipe(False, levels=lv, format=0)
         cs = ol.encode(img, rc)
         dec = im.decode_opj(cs, ".j2k")
         ps = im.psnr(img, dec, bits)
         n_opj, ps_opj = opj_psnr_at(img, bits, len(cs), lv)
+        import hashlib
         cases.append({"name": name, "bits": bits, "levels": lv, "oracle_bytes": len(cs),
+                      "oracle_sha256": hashlib.sha256(cs).hexdigest(),
                       "oracle_psnr": round(ps, 4), "opj_bytes": n_opj, "opj_psnr": round(ps_opj, 4),
                       "bpp": round(8.0 * len(cs) / (img.shape[0] * img.shape[1]), 5)})
         print(cases[-1])
     g["lossy"] = cases
+    # lossless at full C4 size (BASELINE.json configs[3]: one 5000x7000 RGB8
+    # batch image, seed 0, JPX as the batch writes it): the oracle file's
+    # SHA-256 pins the GPU batch output without running the oracle there
+    img = im.synth_rgb8(7000, 5000, seed=0)
+    cs = ol.encode(img, ol.recipe(True))
+    assert np.array_equal(im.decode_pillow(cs), img)
+    import hashlib
+    g["lossless"] = [{"name": "c4_synth_rgb8_5000x7000_seed0_jpx", "oracle_bytes": len(cs),
+                      "oracle_sha256": hashlib.sha256(cs).hexdigest()}]
+    print(g["lossless"])
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(g, f, indent=1)
     print(json.dumps(g["testjpx"], indent=1))

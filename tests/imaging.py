@@ -40,6 +40,15 @@ def synth_rgb8(h, w, seed=1234, noise=6.0):
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
+def testjpx_tiled(pix: np.ndarray, h=4000, w=6000) -> np.ndarray:
+    """SURVEY.md 8(d)'s second C2 content class: the RGB channels of the
+    test.jpx pixels (a real scan), mirror-tiled to h x w."""
+    rgb = np.ascontiguousarray(pix[..., :3])
+    H, W = rgb.shape[:2]
+    return np.ascontiguousarray(np.pad(rgb, ((0, max(0, h - H)), (0, max(0, w - W)), (0, 0)),
+                                       mode="symmetric")[:h, :w])
+
+
 def synth_u16(h, w, comps=3, seed=2):
     """C3/C5-style 16-bit content scaled to [0, 65535] plus N(0, 400)."""
     rng = np.random.default_rng(seed)
@@ -157,8 +166,9 @@ def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=Fals
     return hdr + ifd + bytes(extra) + b"".join(strips)
 
 
-def decode_opj(data: bytes, ext=".jpx") -> np.ndarray:
-    """Decode with opj_decompress (exact for 16-bit RGB, unlike Pillow)."""
+def decode_opj(data: bytes, ext=".jpx", area=None) -> np.ndarray:
+    """Decode with opj_decompress (exact for 16-bit RGB, unlike Pillow);
+    area = (x0, y0, x1, y1) decodes only that window (-d)."""
     tool = opj("opj_decompress")
     if tool is None:
         raise RuntimeError("opj_decompress not available")
@@ -167,7 +177,10 @@ def decode_opj(data: bytes, ext=".jpx") -> np.ndarray:
         dst = os.path.join(d, "out.tif")
         with open(src, "wb") as f:
             f.write(data)
-        r = subprocess.run([tool, "-i", src, "-o", dst], capture_output=True)
+        cmd = [tool, "-i", src, "-o", dst]
+        if area is not None:
+            cmd += ["-d", ",".join(str(int(v)) for v in area)]
+        r = subprocess.run(cmd, capture_output=True)
         if r.returncode != 0:
             raise RuntimeError(r.stderr.decode() + r.stdout.decode())
         return read_tiff(open(dst, "rb").read())
@@ -262,6 +275,27 @@ def tile_parts(cs: bytes):
             break
         p += psot
     return out
+
+
+def tiff_set_tag(data: bytes, tag: int, value: int) -> bytes:
+    """Classic or BigTIFF (either byte order): overwrite the first (inline)
+    value of IFD entry `tag` -- malformed-file fixtures for the parser tests."""
+    b = bytearray(data)
+    e = "<" if b[:2] == b"II" else ">"
+    big = struct.unpack(e + "H", b[2:4])[0] == 43
+    ifd = struct.unpack(e + "Q", b[8:16])[0] if big else struct.unpack(e + "I", b[4:8])[0]
+    n = struct.unpack(e + ("Q" if big else "H"), b[ifd:ifd + (8 if big else 2)])[0]
+    base, size = ifd + (8 if big else 2), (20 if big else 12)
+    for i in range(n):
+        p = base + i * size
+        t, typ = struct.unpack(e + "HH", b[p:p + 4])
+        if t != tag:
+            continue
+        v = p + (12 if big else 8)
+        fmt = {3: "H", 4: "I", 16: "Q"}[typ]
+        b[v:v + struct.calcsize(fmt)] = struct.pack(e + fmt, value)
+        return bytes(b)
+    raise KeyError(tag)
 
 
 def tiff_bytes_compressed(img: np.ndarray, compression: str, predictor: bool = False, rows_per_strip: int = 16) -> bytes:

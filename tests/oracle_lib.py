@@ -22,7 +22,8 @@ class OracleRecipe(Structure):
                 ("progression", c_int32), ("sop", c_int32), ("eph", c_int32), ("plt", c_int32),
                 ("tparts_r", c_int32), ("guard_bits", c_int32), ("reversible", c_int32),
                 ("mct", c_int32), ("qstep", c_double), ("rate_bpp", c_double),
-                ("format", c_int32), ("comment", c_int32), ("slope_skip", c_int32)]
+                ("format", c_int32), ("comment", c_int32), ("slope_skip", c_int32),
+                ("flush_period", c_int32)]
 
 
 _L = None

@@ -105,6 +105,35 @@ def test_tiff_layout_rejects_unsupported_compression():
         jp2hip.tiff_layout(bytes(data))
 
 
+def test_tiff_layout_rows_per_strip_zero_is_one_strip():
+    """RowsPerStrip = 0 (invalid) reads as one strip, as libtiff does, instead
+    of dividing by zero (one bad upload must not kill the JVM)."""
+    img = im.synth_rgb8(40, 30, seed=1)
+    data = im.tiff_set_tag(im.tiff_bytes(img, rows_per_strip=64), 278, 0)
+    lay, offs = jp2hip.tiff_layout(data)
+    assert lay.rows_per_strip == 40 and lay.nstrips == 1
+
+
+def test_tiff_layout_rejects_wrapped_bigtiff_offset():
+    """A LONG8 strip offset near 2^64 must not wrap the bounds check."""
+    img = im.synth_rgb8(16, 16, seed=2)
+    data = im.tiff_set_tag(im.bigtiff_bytes(img, rows_per_strip=16), 273, (1 << 64) - 8)
+    with pytest.raises(jp2hip.Jp2hipError, match="out of range"):
+        jp2hip.tiff_layout(data)
+
+
+@pytest.mark.parametrize("photo,nc,msg", [(0, 1, "WhiteIsZero"), (3, 1, "Photometric"), (5, 4, "Photometric"),
+                                          (6, 3, "Photometric"), (2, 1, "RGB needs"), (1, 3, "BlackIsZero")])
+def test_tiff_layout_rejects_unsupported_photometric(photo, nc, msg):
+    """Only BlackIsZero gray (+alpha) and RGB (+alpha) are encoded; palette,
+    CMYK, YCbCr and WhiteIsZero fail with a message."""
+    img = im.synth_rgb8(8, 8)
+    img = img[..., 0].copy() if nc == 1 else (np.dstack([img, img[..., :1]]) if nc == 4 else img)
+    data = im.tiff_set_tag(im.tiff_bytes(img), 262, photo)
+    with pytest.raises(jp2hip.Jp2hipError, match=msg):
+        jp2hip.tiff_layout(data)
+
+
 @pytest.mark.parametrize("comp,code,pred", [("tiff_lzw", 5, False), ("tiff_lzw", 5, True), ("packbits", 32773, False),
                                             ("tiff_adobe_deflate", 8, False), ("tiff_adobe_deflate", 8, True),
                                             ("tiff_deflate", 32946, False)])
@@ -179,8 +208,14 @@ def test_factory_without_gpu_or_kakadu(monkeypatch):
     assert ConverterFactory.get_converter(OpenJPEGConverter).convert("x", "y.tif", Conversion.LOSSLESS) is None
     with pytest.raises(KakaduNotFoundError):
         ConverterFactory.get_converter(KakaduConverter)
-    with pytest.raises(IOError):
-        ConverterFactory.get_converter(GpuConverter)
+    # the GPU branch never raises (ImageWorkerVerticle.java:106 catches only
+    # IOException/InterruptedException): without a GPU or Kakadu it hands out
+    # a converter whose convert() raises IOError with the BUCKETEER-001 text
+    conv = ConverterFactory.get_converter(GpuConverter)
+    assert isinstance(conv, GpuConverter) and conv.unavailable
+    with pytest.raises(IOError, match="Failed to convert TIFF to JP2: img1"):
+        conv.convert("img1", "y.tif", Conversion.LOSSLESS)
+    assert jp2hip.device_count() == 0
     with pytest.raises(ValueError):
         ConverterFactory.get_converter(str)
     ConverterFactory.reset()

@@ -118,3 +118,45 @@ def test_batch_upload_failure_is_reported_and_file_kept(tmp_path):
         res = q.drain()
     assert res[0]["job"] == 5 and res[0]["status"] == jb.UPLOAD_FAILED
     assert (tmp_path / "a.jpx").exists()  # S3BucketVerticle only deletes after success
+
+
+@pytest.mark.gpu
+def test_batch_compressed_tiff_with_many_strips(tmp_path):
+    """An LZW TIFF with 600 one-row strips needs 1200 offset slots (offsets +
+    byte counts); the reader sizes its retry from the strip count."""
+    import oracle_lib as ol
+    img = im.synth_rgb8(600, 96, seed=21)
+    p = tmp_path / "many.tif"
+    p.write_bytes(im.tiff_bytes_compressed(img, "tiff_lzw", rows_per_strip=1))
+    with jb.BatchQueue(contexts=1) as q:
+        q.submit(1, "ark:/x/many", p, tmp_path / "many.jpx")
+        res = q.drain()
+    assert res[0]["status"] == jb.OK, res[0]["message"]
+    assert res[0]["pixels"] == 600 * 96
+
+
+@pytest.mark.gpu
+def test_batch_c4_full_size_image_identical_to_oracle(tmp_path, golden):
+    """C4 at its configured size: one 5000x7000 RGB8 TIFF through the native
+    batch queue (read, lossless encode, JPX write, stub upload) -- the file
+    is the oracle's, byte for byte (golden SHA-256 from make_golden.py)."""
+    import hashlib
+    g = golden["lossless"][0]
+    img = im.synth_rgb8(7000, 5000, seed=0)
+    p = tmp_path / "c4.tif"
+    p.write_bytes(im.tiff_bytes(img, rows_per_strip=64))
+    got = {}
+
+    def upload(image_id, path):
+        with open(path, "rb") as f:
+            got[image_id] = f.read()
+        return True
+
+    with jb.BatchQueue(contexts=2, upload=upload) as q:
+        q.submit(1, "ark:/99999/synth00000", p, tmp_path / "c4.jpx")
+        res = q.drain()
+    assert res[0]["status"] == jb.OK, res[0]["message"]
+    data = got["ark:/99999/synth00000"]
+    assert len(data) == g["oracle_bytes"]
+    assert hashlib.sha256(data).hexdigest() == g["oracle_sha256"]
+    assert not (tmp_path / "c4.jpx").exists()

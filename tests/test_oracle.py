@@ -38,28 +38,64 @@ def test_oracle_lossless_reproduces_testjpx_main_header(testjpx_pixels, golden):
     assert im.count_marker(cs, b"\xff\x91") == g["sop"]
     tps = im.tile_parts(cs)
     assert len(tps) == g["tileparts"]
-    # ORGtparts=R: 7 tile-parts per tile, TPsot = resolution
-    assert [t[2] for t in tps[:7]] == list(range(7))
+    # ORGtparts=R + -flush_period 1024: Kakadu's order in test.jpx -- tiles
+    # 0-7 res 0, tiles 0-7 res 1, ..., res 6, then tiles 8-15 -- with TNsot
+    # written only on each tile's last tile-part
+    assert [[t[0], t[2], t[3]] for t in tps] == g["tp_order"]
     assert len(cs) > g["min_size_assert"]
     assert abs(len(cs) - g["size"]) / g["size"] < 0.02   # Kakadu: 303,886 B
     assert np.array_equal(im.decode_pillow(cs), testjpx_pixels)
 
 
-@pytest.mark.parametrize("case", [0, 1, 2])
+def test_oracle_com_markers_follow_kakadu_layout(testjpx_pixels, testjpx_bytes):
+    """test.jpx's main header ends in two COMs: a version string and
+    Kdu-Layer-Info (one "%6.1f, %8.1e" line per layer, -192.0 on the lossless
+    last layer, bytes through that layer).  The oracle writes the same
+    layout (its own version string; slopes in its own units)."""
+    def coms(cs):
+        seg, p = [], cs.find(b"\xff\x64")
+        while cs[p:p + 2] == b"\xff\x64":
+            n = int.from_bytes(cs[p + 2:p + 4], "big")
+            seg.append(cs[p + 4:p + 2 + n])
+            p += 2 + n
+        return seg
+    ref = coms(testjpx_bytes)
+    cs = ol.encode(testjpx_pixels, ol.recipe(True, format=0))
+    got = coms(cs)
+    assert len(got) == len(ref) == 2
+    assert got[0][:2] == ref[0][:2] == b"\x00\x01"
+    hdr = b"Kdu-Layer-Info: log_2{Delta-D(squared-error)/Delta-L(bytes)}, L(bytes)\n"
+    for seg in (ref[1], got[1]):
+        assert seg[:2] == b"\x00\x01" and seg[2:2 + len(hdr)] == hdr
+        lines = seg[2 + len(hdr):].decode().splitlines()
+        assert len(lines) == 6 and all(len(x) == 16 for x in lines)
+        assert lines[-1].startswith("-192.0,")
+        nbytes = [float(x.split(",")[1]) for x in lines]
+        assert nbytes == sorted(nbytes)
+    assert len(got[1]) == len(ref[1])
+    last = float(got[1].decode("latin-1").splitlines()[-1].split(",")[1])
+    assert abs(last - len(cs)) / len(cs) < 0.05
+
+
+@pytest.mark.parametrize("case", range(5))
 def test_oracle_lossy_within_0p1db_of_opj(case, golden, testjpx_pixels):
+    """The lossy yardstick (north_star): PSNR within 0.1 dB of opj_compress at
+    the same bytes -- 1024-class crops and full-size C2 in both SURVEY.md 8(d)
+    content classes (synthetic scan, test.jpx pixels mirror-tiled)."""
+    import hashlib
+    from conftest import golden_image
     c = golden["lossy"][case]
-    if c["name"].startswith("synth_rgb8"):
-        img = im.synth_rgb8(1024, 1536, seed=1234)
-    elif c["name"].startswith("testjpx"):
-        img = testjpx_pixels[:1024, :1024, :3].copy()
-    else:
-        img = im.synth_u16(1024, 1024, comps=1, seed=5)
+    img = golden_image(c["name"], testjpx_pixels)
     cs = ol.encode(img, ol.recipe(False, levels=c["levels"], format=0))
     assert len(cs) == c["oracle_bytes"]            # deterministic
+    assert hashlib.sha256(cs).hexdigest() == c["oracle_sha256"]
     dec = im.decode_opj(cs, ".j2k") if c["bits"] == 16 else im.decode_pillow(cs)
     ps = im.psnr(img, dec, c["bits"])
     assert abs(ps - c["oracle_psnr"]) < 1e-3
-    assert abs(c["opj_bytes"] - len(cs)) / len(cs) < 0.01
+    if c["bpp"] > 2.9:  # on the rate target: opj was asked for the same bytes
+        assert abs(c["opj_bytes"] - len(cs)) / len(cs) < 0.01
+    else:  # every pass fits under 3 bpp: opj's output is no larger than ours
+        assert c["opj_bytes"] <= len(cs) * 1.01
     assert ps >= c["opj_psnr"] - 0.1
 
 

@@ -59,18 +59,24 @@ def _rank_arrays(keys, dr):
 
 
 def test_split_rows_cover_every_row_once():
-    for h, th in ((30000, 512), (1, 512), (1000, 512), (2048, 512), (700, 256)):
+    """Bands are whole -flush_period stripes (so each rank's tile-parts are one
+    contiguous run of the file) and balanced to within one stripe."""
+    for h, th, fp in ((30000, 512, 1024), (1, 512, 1024), (1000, 512, 1024), (2048, 512, 1024),
+                      (700, 256, 1024), (30000, 512, 0), (5000, 768, 1024), (8000, 1024, 1024)):
         nty = (h + th - 1) // th
+        stripe = max(1, fp // th) if fp > 0 else 1
         for world in (1, 2, 3, 4, 7, 8, 64):
-            bands = [js.split_rows(h, th, r, world) for r in range(world)]
+            bands = [js.split_rows(h, th, r, world, fp) for r in range(world)]
             assert bands[0][0] == 0 and bands[-1][1] == h
             for (a0, a1), (b0, b1) in zip(bands, bands[1:]):
                 assert a1 == b0 and a0 <= a1
             for r0, r1 in bands:
                 assert r0 % th == 0
                 assert r1 == h or r1 % th == 0
+                if fp > 0 and r1 < h:
+                    assert r1 % fp == 0 or (r1 // fp) > ((r1 - th) // fp), (h, th, fp, r1)  # ends a flush
             sizes = [-(-(r1 - r0) // th) if r1 > r0 else 0 for r0, r1 in bands]
-            assert max(sizes) - min(sizes) <= 1 or nty < world
+            assert max(sizes) - min(sizes) <= 2 * stripe or nty < world * stripe
 
 
 def test_thresholds_world1_match_oracle_rule():
@@ -198,7 +204,7 @@ def _encode_world(tif, conv, rc, world, band_only=False):
             enc = jp2hip.Encoder(0)
             try:
                 if band_only:
-                    r0, r1 = js.split_rows(lay.height, rc.tile_h, r, world)
+                    r0, r1 = js.split_rows(lay.height, rc.tile_h, r, world, rc.flush_period)
                     buf, blay, keep = js.band_strips(tif, lay, offs, r0, r1)
                     src, use = (buf or b"\0"), blay
                 else:
@@ -315,3 +321,65 @@ def test_split_write_parts_to_one_file(encoder, tmp_path):
     os.replace(tmp, tmp_path / "x.jpx")
     assert (tmp_path / "x.jpx").read_bytes() == data
     assert np.array_equal(im.decode_pillow(data), img)
+
+
+@pytest.mark.gpu
+def test_split_c5_full_size(encoder):
+    """C5 at its configured size: 40000x30000 Gray16, lossy 3 bpp, 7 levels,
+    512^2 tiles (1.2 GP, 4 661 tiles, 350 701 code-blocks).  The tile-split
+    encode at world 1 and world 2 (ranks as threads on cuda:0) equals the
+    single-GPU encode, stays within rate, and decodes (opj_decompress on
+    three 1024^2 windows) at the expected PSNR."""
+    from concurrent.futures import ThreadPoolExecutor
+    from devmem import DeviceBytes
+    w, h, rps = 40000, 30000, 64
+    buf = np.empty((h, w), "<u2")
+
+    def fill(g):
+        buf[g:min(h, g + 512)] = im.synth_gray16_rows(g, min(h, g + 512), w, seed=5, band=512)
+
+    with ThreadPoolExecutor(16) as ex:
+        list(ex.map(fill, range(0, h, 512)))
+    nstrips = (h + rps - 1) // rps
+    from ctypes import POINTER, c_uint64, cast
+    offs = (c_uint64 * nstrips)(*[s * rps * w * 2 for s in range(nstrips)])
+    from jp2hip._lib import Layout
+    lay = Layout(w, h, 1, 16, 1, 0, rps, nstrips, cast(offs, POINTER(c_uint64)))
+    rc = jp2hip.recipe(jp2hip.LOSSY, levels=7)
+    d = DeviceBytes(buf)
+    try:
+        single, st = encoder.encode_device(d.ptr, d.nbytes, lay, jp2hip.LOSSY, rc)
+        assert st.codeblocks == 350701
+        cs = im.codestream(single)
+        assert len(cs) <= 3.0 * w * h / 8
+        assert len(im.tile_parts(cs)) == 4661 * 8
+        for world in (1, 2):
+            g = js.ThreadGroup(world)
+            parts, errs = [None] * world, []
+
+            def work(r):
+                try:
+                    e = jp2hip.Encoder(0)
+                    try:
+                        parts[r] = e.encode_device_split(d.ptr, d.nbytes, lay, jp2hip.LOSSY, g.member(r).split(), rc)
+                    finally:
+                        e.close()
+                except Exception as ex:
+                    errs.append(ex)
+                    g.abort()
+
+            th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=600)
+            assert not errs, errs
+            assert b"".join(p[0] for p in parts) == single, world
+    finally:
+        d.free()
+    # decoded windows (opj_decompress -d) against the source rows
+    for (x0, y0) in ((0, 0), (19456, 14336), (38976, 28976)):
+        x1, y1 = min(w, x0 + 1024), min(h, y0 + 1024)
+        dec = im.decode_opj(single, ".jpx", area=(x0, y0, x1, y1))
+        assert dec.shape[:2] == (y1 - y0, x1 - x0)
+        assert im.psnr(buf[y0:y1, x0:x1], dec.reshape(y1 - y0, x1 - x0), 16) > 40
