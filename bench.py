@@ -75,9 +75,37 @@ def barrier(world):
         dist.barrier()
 
 
-def cpu_baseline_oracle(img, budget_s=12.0):
-    """The oracle (plain C, 1 thread) on a bounded crop of the same workload:
-    whole 1024x2048 encodes until ~budget_s seconds of CPU work."""
+def host_cpu():
+    """(cores this process may use, CPU model) of the host the bench runs on:
+    the affinity mask, capped by the cgroup CPU quota (a GPU box's share of a
+    large host) and OMP_NUM_THREADS when the pool sets it."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            cores = min(cores, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return cores, model
+
+
+def cpu_oracle_not_a_reference(img, budget_s=8.0):
+    """This repo's own C restatement (oracle/jp2_oracle.c, 1 thread) on a
+    1024x2048 crop -- NOT a reference converter, reported for scale only."""
     import oracle_lib as ol
     crop = np.ascontiguousarray(img[:1024, :2048])
     rc = ol.recipe(False)
@@ -89,9 +117,46 @@ def cpu_baseline_oracle(img, budget_s=12.0):
         if time.perf_counter() - t0 > budget_s or n >= 32:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(n * crop.shape[0] * crop.shape[1] / 1e6 / dt, 4), "unit": "MP/s",
-            "cores": 1, "kind": "port", "seconds": round(dt, 2),
-            "sample": f"{n}x encode of a 1024x2048 crop of the C2 image, lossy 9/7 3 bpp, oracle/jp2_oracle.c single thread"}
+    return {"value": round(n * crop.shape[0] * crop.shape[1] / 1e6 / dt, 4), "unit": "MP/s", "cores": 1,
+            "kind": "not a reference (this repo's C restatement, oracle/jp2_oracle.c)", "seconds": round(dt, 2),
+            "sample": f"{n}x encode of a 1024x2048 crop of the C2 image, lossy 9/7 3 bpp, 1 thread"}
+
+
+def cpu_reference_opj(img):
+    """north_star's CPU reference converter: kdu_compress is proprietary and
+    absent, so opj_compress (OpenJPEG 2.4.0) with the
+    Appendix A mapping of the recipe.  BASELINE.md steps 1-3: the full C2
+    image (6000x4000 RGB8, lossy 3 bpp) encoded by `nproc` concurrent
+    single-image processes (OpenJPEG's encoder does not scale with -threads),
+    on the host cores of this same run; value = images x 24 MP / wall time."""
+    import imaging as im
+    tool = im.opj("opj_compress")
+    if tool is None:
+        return None
+    cores, model = host_cpu()
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "c2.tif")
+        with open(src, "wb") as f:
+            f.write(im.tiff_bytes(img))
+        # -r: rate ratios of the 6 layers, the last = 24 bpp raw / 3 bpp
+        cmd = [tool, "-i", src, "-I", "-n", "7", "-t", "512,512", "-b", "64,64", "-p", "RPCL", "-SOP",
+               "-EPH", "-PLT", "-TP", "R", "-c",
+               "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]",
+               "-r", "256,128,64,32,16,8"]
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen(cmd + ["-o", os.path.join(d, f"o{i}.j2k")], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL) for i in range(cores)]
+        ok = all(p.wait() == 0 for p in ps)
+        dt = time.perf_counter() - t0
+        nbytes = os.path.getsize(os.path.join(d, "o0.j2k")) if ok else 0
+    if not ok:
+        return None
+    mp = cores * img.shape[0] * img.shape[1] / 1e6
+    return {"value": round(mp / dt, 3), "unit": "MP/s", "cores": cores, "kind": "reference",
+            "tool": "opj_compress 2.4.0 (north_star's stand-in for the proprietary kdu_compress)",
+            "cpu_model": model, "seconds": round(dt, 2), "bytes_per_image": nbytes,
+            "sample": f"{cores} concurrent processes, each one full 6000x4000 RGB8 C2 image, lossy 3 bpp, "
+                      "Appendix A recipe"}
 
 
 def pmc_traffic(kernel):
@@ -130,33 +195,6 @@ def sq_counters(kernel):
     return keep
 
 
-def cpu_converter_opj(img, nproc):
-    """north_star's CPU reference converter: opj_compress (Kakadu is absent),
-    `nproc` concurrent single-image processes with the Appendix A recipe."""
-    import imaging as im
-    tool = im.opj("opj_compress")
-    if tool is None:
-        return None
-    crop = np.ascontiguousarray(img[:2048, :2048])
-    with tempfile.TemporaryDirectory() as d:
-        src = os.path.join(d, "in.tif")
-        open(src, "wb").write(im.tiff_bytes(crop))
-        cmd = [tool, "-i", src, "-I", "-n", "7", "-t", "512,512", "-b", "64,64", "-p", "RPCL", "-SOP",
-               "-EPH", "-PLT", "-TP", "R", "-c",
-               "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]",
-               "-r", "256,128,64,32,16,8"]
-        t0 = time.perf_counter()
-        ps = [subprocess.Popen(cmd + ["-o", os.path.join(d, f"o{i}.j2k")], stdout=subprocess.DEVNULL,
-                               stderr=subprocess.DEVNULL) for i in range(nproc)]
-        ok = all(p.wait() == 0 for p in ps)
-        dt = time.perf_counter() - t0
-    if not ok:
-        return None
-    mp = nproc * crop.shape[0] * crop.shape[1] / 1e6
-    return {"tool": "opj_compress 2.4.0", "value": round(mp / dt, 3), "unit": "MP/s", "processes": nproc,
-            "sample": "2048x2048 crop of the C2 image per process, lossy 3 bpp, Appendix A recipe"}
-
-
 def run(args):
     import threading
 
@@ -172,10 +210,16 @@ def run(args):
     tif = im.tiff_bytes(img, rows_per_strip=64)
     lay, offs = jp2hip.tiff_layout(tif)
     d_src = torch.frombuffer(bytearray(tif), dtype=torch.uint8).to(device)
+    # the same TIFF in pinned host memory, for the PCIe-inclusive variant
+    h_src = torch.frombuffer(bytearray(tif), dtype=torch.uint8).pin_memory()
     torch.cuda.synchronize()
     # `inflight` independent images per GPU, each on its own libjp2hip
-    # context (own HIP stream and buffers): the batch path's per-GPU queue
-    nf = max(1, args.inflight)
+    # context (own HIP stream and buffers): the batch path's per-GPU queue.
+    # Steps are spread evenly over the contexts (no context does an extra
+    # image after the others have drained).
+    nf = max(1, min(args.inflight, args.steps))
+    rounds = -(-args.steps // nf)
+    nf = -(-args.steps // rounds)
     host_threads = max(2, 16 // nf)
     encs = [jp2hip.Encoder(local, host_threads=host_threads, profile=True) for _ in range(nf)]
     rc = jp2hip.recipe(jp2hip.LOSSY)
@@ -188,67 +232,76 @@ def run(args):
             all_stats.append(st.as_dict())
     # single-image latency (one context, nothing else in flight)
     lat, alone = [], []
-    for _ in range(2):
+    for _ in range(3):
         t = time.perf_counter()
         _, st = encs[0].encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
         lat.append(time.perf_counter() - t)
         all_stats.append(st.as_dict())
         alone.append(st.as_dict())
-    barrier(world)
-    torch.cuda.synchronize()
-    stages = [[] for _ in range(nf)]
-    outs = [None] * nf
-    errors = []
 
-    def worker(k):
-        try:
-            for step in range(k, args.steps, nf):
-                out, st = encs[k].encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
-                stages[k].append(st.as_dict())
-                outs[k] = out
-        except Exception as ex:  # surfaced after the timed region
-            errors.append(ex)
+    def timed(encode):
+        """K steps over the contexts from a shared counter; (seconds, stats)."""
+        stages, errors = [], []
+        nxt = [0]
+        mu = threading.Lock()
 
-    t0 = time.perf_counter()
-    th = [threading.Thread(target=worker, args=(k,)) for k in range(nf)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    torch.cuda.synchronize()
-    barrier(world)
-    dt = time.perf_counter() - t0
-    if errors:
-        raise errors[0]
+        def worker(k):
+            try:
+                while True:
+                    with mu:
+                        step = nxt[0]
+                        nxt[0] += 1
+                    if step >= args.steps:
+                        return
+                    _, st = encode(encs[k])
+                    with mu:
+                        stages.append(st.as_dict())
+            except Exception as ex:  # surfaced after the timed region
+                errors.append(ex)
+
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(nf)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        barrier(world)
+        dt = time.perf_counter() - t0
+        if errors:
+            raise errors[0]
+        return dt, stages
+
+    # the contract's value: TIFF resident in HBM -> JPX bytes in host memory
+    dt, stages = timed(lambda e: e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc))
     dt_max = barrier_max(world, dt, device)
     mp = img.shape[0] * img.shape[1] / 1e6
     value = world * mp * args.steps / dt_max
+    # PCIe-inclusive: TIFF bytes in pinned host memory -> jp2hip_encode_tiff
+    # (header parse, H2D of the 72 MB file, encode) -> JPX bytes in host memory
+    dt_h, _ = timed(lambda e: e.encode_tiff_ptr(h_src.data_ptr(), h_src.numel(), jp2hip.LOSSY, rc))
+    dt_h_max = barrier_max(world, dt_h, device)
     res = None
     if rank == 0:
-        flat = [s for ss in stages for s in ss]
+        flat = stages
         avg = {k: float(np.mean([s[k] for s in flat])) for k in flat[0]}
         every = flat + all_stats
         avg_all = {k: float(np.mean([s[k] for s in every])) for k in every[0]}
-        # candidate dominant kernels: k_t1_mq's time is its own execution span
-        # (wall clock read inside the kernel, as rocprofv3 measures it); the
-        # others are HIP-event stage intervals.  PCRD is not a candidate: its
-        # interval holds host round trips (segment count, thresholds).
-        kern = {"k_t1_mq": avg_all["t1_mq_ms"], "k_t1_cm": avg_all["t1_cm_ms"], "k_dwt": avg_all["dwt_ms"],
-                "k_quant": avg_all["quant_ms"], "k_ingest": avg_all["ingest_ms"]}
         # the dominant kernel by rocprofv3 kernel time (~50 % of all kernel
-        # time, profiles/r01/c2_kernel_stats_final*.csv); the stage intervals of
-        # the other kernels include waiting behind other images under load
+        # time, profiles/r02/c2_kernel_stats*.csv): k_t1_mq, whose time is its
+        # own execution span (wall clock read inside the kernel, as rocprofv3
+        # measures it)
         dom = "k_t1_mq"
         C, L = 3, 6
         npx = img.shape[0] * img.shape[1]
-        # algorithmic bytes per launch (DESIGN.md "Roofline"):
-        #   tier-1 reads one int32 coefficient per sample and writes the MQ bytes
-        #   DWT per SURVEY.md 8(d) B_dwt
-        t1_alg = 4 * C * npx + avg["t1_bytes"]
+        # algorithmic bytes per k_t1_mq launch: it reads one decision-stream
+        # byte per MQ decision and writes the MQ code bytes (the per-pass
+        # counts / distortions it also reads are < 1 %)
+        mq_alg = avg_all["mq_decisions"] + avg_all["t1_bytes"]
+        ach = mq_alg / (avg_all["t1_mq_ms"] * 1e-3) / 1e9
         dwt_alg = dwt_bytes_per_px(C, 1, L) * npx
-        alg = {"k_t1_mq": t1_alg, "k_t1_cm": t1_alg, "k_dwt": dwt_alg, "k_quant": 4 * C * npx * 2,
-               "k_ingest": (C + 4 * C) * npx, "k_pcrd": 0}
-        ach = alg[dom] / (kern[dom] * 1e-3) / 1e9
         dwt_alone = float(np.mean([x["dwt_ms"] for x in alone]))
         traffic, traffic_src = pmc_traffic(dom)
         # SURVEY.md 8(d) full path: B_path = B_dwt + 4C + 3*bpp/8 per pixel
@@ -263,24 +316,33 @@ def run(args):
             "config": {"workload": "C2: 6000x4000 RGB8 TIFF -> JPX, lossy 9/7 3 bpp, Kakadu recipe "
                                    "(6 levels, 6 layers, 512^2 tiles, 64^2 blocks, RPCL, SOP/EPH/PLT, TP=R)",
                        "image": "6000x4000x3 u8", "images_in_flight_per_gpu": nf,
+                       "timed_span": "TIFF resident in HBM -> JPX bytes in host memory (jp2hip_encode_device)",
                        "parallelism": f"replicas x{world}", "out_bytes": int(avg["out_bytes"]),
                        "bpp": round(8 * avg["out_bytes"] / npx, 4),
                        "single_image_latency_ms": round(1e3 * min(lat), 3)},
+            # the same steps with the TIFF in pinned host memory and the H2D
+            # inside the timed span (PCIe-inclusive rate)
+            "value_pcie_inclusive": {"value": round(world * mp * args.steps / dt_h_max, 3), "unit": "MP/s",
+                                     "ms_per_step": round(dt_h_max * 1e3 / args.steps, 3),
+                                     "timed_span": "TIFF bytes in pinned host memory -> jp2hip_encode_tiff (parse, "
+                                                   "H2D, encode) -> JPX bytes in host memory"},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(ach * 1e9 / HBM_PEAK, 5),
                          "traffic": round(traffic) if traffic is not None else None,
                          "traffic_source": traffic_src,
-                         "alg_bytes_per_launch": int(alg[dom]),
-                         "avg_launch_ms": round(kern[dom], 4), "launches_averaged": len(every),
-                         "note": "tier-1 is a serial MQ dependency chain per code-block: latency-bound, "
-                                 "the byte roofline is reported as SURVEY.md 8(d) asks"},
+                         "alg_bytes_per_launch": int(mq_alg),
+                         "alg_bytes_def": "decision-stream bytes read (1 per MQ decision) + MQ code bytes written",
+                         "avg_launch_ms": round(avg_all["t1_mq_ms"], 4), "launches_averaged": len(every),
+                         "mq_decisions_per_launch": int(avg_all["mq_decisions"]),
+                         "note": "tier-1 MQ is a serial dependency chain per code-block: latency-bound; "
+                                 "its byte roofline is tiny by nature (SURVEY.md 8(d))"},
             "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
                               "achieved": round(b_path * px_per_s_gpu / 1e9, 2), "peak": HBM_PEAK / 1e9,
                               "unit": "GB/s", "frac": round(b_path * px_per_s_gpu / HBM_PEAK, 5)},
             # DWT stage time from HIP events on the context's stream: under
-            # load (12 images in flight, the event span includes waiting for
-            # CUs other images hold) and alone (one image on the GPU)
+            # load (the event span includes waiting for CUs other images
+            # hold) and alone (one image on the GPU)
             "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                              "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                              "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
@@ -294,7 +356,7 @@ def run(args):
                                                         "t1_mq_ms", "pcrd_ms", "d2h_ms", "t2_ms",
                                                         "total_ms")},
             "t1": {"codeblocks": int(avg["codeblocks"]), "coded_passes": int(avg["coded_passes"]),
-                   "mq_bytes": int(avg["t1_bytes"])},
+                   "mq_bytes": int(avg["t1_bytes"]), "mq_decisions": int(avg["mq_decisions"])},
         }
     return res, img, world, rank, encs[0]
 
@@ -508,9 +570,8 @@ def main():
         if not args.no_lossless:
             res["lossless_c3"] = lossless_c3(enc)
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline_oracle(img)
-            nproc = min(16, os.cpu_count() or 1)
-            res["cpu_converter"] = cpu_converter_opj(img, nproc)
+            res["cpu_baseline"] = cpu_reference_opj(img)
+            res["cpu_not_a_reference"] = cpu_oracle_not_a_reference(img)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

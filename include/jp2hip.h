@@ -123,6 +123,7 @@ typedef struct jp2hip_stats {
     int32_t reserved;
     double t1_cm_ms;      /* tier-1 context-modelling kernel (part of t1_ms)  */
     double t1_mq_ms;      /* tier-1 MQ-coder kernel (part of t1_ms)           */
+    int64_t mq_decisions; /* MQ-coded decisions (one decision-stream byte each) */
 } jp2hip_stats;
 
 const char *jp2hip_version(void);

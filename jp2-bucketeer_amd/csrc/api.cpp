@@ -399,6 +399,7 @@ void fill_stats(jp2hip_stats *stats, const jp2hip::StageTimes &st, double t_star
     stats->coded_passes = sum.coded_passes;
     stats->out_bytes = out_bytes;
     stats->rate_iterations = iters;
+    stats->mq_decisions = sum.decisions;
 }
 
 // The whole encode with the source already in device memory.  On success

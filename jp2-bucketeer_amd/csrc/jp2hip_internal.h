@@ -139,6 +139,7 @@ struct T2Summary {
     int64_t layer_bytes[kMaxLayers];  // packet bytes per layer
     uint64_t kc[kMaxLayers];          // Kdu-Layer-Info slope keys (select() only)
     int64_t t1_bytes, coded_passes;   // tier-1 totals (every coded pass)
+    int64_t decisions;                // MQ-coded decisions
     int32_t skipped, err;             // slope prediction skipped planes; tier-1 overflow
 };
 // Main header (SOC .. COM) for the Kdu-Layer-Info values (nullptr: zeros;

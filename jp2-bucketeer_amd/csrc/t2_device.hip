@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(64) k_t2_tparts(T2Args a) {
 // host needs (part size, header bytes, bytes per layer, tier-1 totals).
 __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
                                                   const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
-                                                  const uint64_t *kc, T2Summary *sum) {
+                                                  const uint64_t *kc, const uint32_t *ndec_key, T2Summary *sum) {
     __shared__ uint64_t part[256];
     __shared__ int64_t lay[256][kMaxLayers > 8 ? 8 : kMaxLayers];
     const int tid = threadIdx.x;
@@ -369,14 +369,16 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
         }
         __syncthreads();
     }
-    // tier-1 totals
-    int64_t tb = 0, tp = 0;
+    // tier-1 totals (ndec_key: ~decisions per block, the MQ lane-order keys)
+    int64_t tb = 0, tp = 0, nd = 0;
     int skipped = 0;
     for (int b = tid; b < nblocks; b += 256) {
         tb += lengths[b];
         tp += npasses[b];
+        nd += ~ndec_key[b];
         skipped |= pmin[b] > 0;
     }
+    lay[tid][1] = nd;
     part[tid] = (uint64_t)tb;
     __syncthreads();
     if (tid == 0) {
@@ -390,13 +392,15 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
     __syncthreads();
     if (tid == 0) {
         uint64_t acc = 0;
-        int64_t h = 0;
+        int64_t h = 0, dsum = 0;
         int sk = 0;
         for (int i = 0; i < 256; i++) {
             acc += part[i] & ~(1ull << 63);
             sk |= (int)(part[i] >> 63);
             h += lay[i][0];
+            dsum += lay[i][1];
         }
+        sum->decisions = dsum;
         sum->coded_passes = (int64_t)acc;
         sum->skipped = sk;
         sum->tp_hdr_bytes = h;
@@ -560,7 +564,7 @@ bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTime
     hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
                        (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
                        with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
-                       (T2Summary *)t2sum.ptr);
+                       (const uint32_t *)ordkey2.ptr, (T2Summary *)t2sum.ptr);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpyAsync(h_sum, t2sum.ptr, sizeof(T2Summary), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipEventRecord(ev[9], stream));

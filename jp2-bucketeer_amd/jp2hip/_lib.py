@@ -55,7 +55,7 @@ class Stats(Structure):
                 ("pcrd_ms", c_double), ("d2h_ms", c_double), ("t2_ms", c_double),
                 ("codeblocks", c_int64), ("coded_passes", c_int64), ("t1_bytes", c_int64),
                 ("out_bytes", c_int64), ("rate_iterations", c_int32), ("reserved", c_int32),
-                ("t1_cm_ms", c_double), ("t1_mq_ms", c_double)]
+                ("t1_cm_ms", c_double), ("t1_mq_ms", c_double), ("mq_decisions", c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
@@ -203,6 +203,19 @@ class Encoder:
         st = Stats()
         buf = ctypes.create_string_buffer(data, len(data))
         rc = lib().jp2hip_encode_tiff(self._h, buf, len(data), conversion,
+                                      byref(rcp) if rcp is not None else None,
+                                      byref(out), byref(n), byref(st))
+        if rc != 0:
+            raise Jp2hipError(last_error())
+        return self._take(out, n), st
+
+    def encode_tiff_ptr(self, h_ptr: int, nbytes: int, conversion: int, rcp: Recipe | None = None):
+        """encode_tiff on TIFF bytes already in host memory at h_ptr (pinned
+        memory makes the H2D a plain DMA)."""
+        out = POINTER(c_uint8)()
+        n = c_size_t()
+        st = Stats()
+        rc = lib().jp2hip_encode_tiff(self._h, c_void_p(h_ptr), nbytes, conversion,
                                       byref(rcp) if rcp is not None else None,
                                       byref(out), byref(n), byref(st))
         if rc != 0:
