@@ -68,7 +68,7 @@ __device__ __forceinline__ void lift_update(void *buf, int idx, int lidx, int ri
 
 // Vertical lifting of staged rows [ya, yb) (global row numbers, signal
 // length H), W columns, row stride ld, rows stored from LDS row 0 = ya.
-template <bool REV>
+template <bool REV, int NT>
 __device__ __forceinline__ void lift_vertical(void *lds, int ya, int yb, int H, int W, int ld) {
     if (H < 2) return;
     const int nsteps = REV ? 2 : 4;
@@ -77,7 +77,7 @@ __device__ __forceinline__ void lift_vertical(void *lds, int ya, int yb, int H, 
         const int par = (s & 1) ? 0 : 1;  // odd rows first
         const int y0 = ya + ((ya & 1) != par ? 1 : 0);
         const int nr = (yb - y0 + 1) / 2;
-        for (int it = tid; it < nr * W; it += kDwtThreads) {
+        for (int it = tid; it < nr * W; it += NT) {
             const int k = it / W, x = it - k * W;
             const int y = y0 + 2 * k;
             int l = y > 0 ? y - 1 : y + 1;
@@ -91,7 +91,7 @@ __device__ __forceinline__ void lift_vertical(void *lds, int ya, int yb, int H, 
 
 // Horizontal lifting of `nrows` full rows of length W starting at LDS row
 // `row0`, row stride ld.
-template <bool REV>
+template <bool REV, int NT>
 __device__ __forceinline__ void lift_horizontal(void *lds, int row0, int nrows, int W, int ld) {
     if (W < 2) return;
     const int nsteps = REV ? 2 : 4;
@@ -99,7 +99,7 @@ __device__ __forceinline__ void lift_horizontal(void *lds, int row0, int nrows, 
     for (int s = 0; s < nsteps; s++) {
         const int par = (s & 1) ? 0 : 1;
         const int cnt = par ? W / 2 : (W + 1) / 2;
-        for (int it = tid; it < nrows * cnt; it += kDwtThreads) {
+        for (int it = tid; it < nrows * cnt; it += NT) {
             const int k = it / cnt, j = it - k * cnt;
             const int x = par + 2 * j;
             const int l = x > 0 ? x - 1 : x + 1;
@@ -180,6 +180,9 @@ __device__ __forceinline__ int32_t band_load(const DwtBandArgs &a, int tc, int y
 template <bool REV, int NR>
 __device__ __forceinline__ void lift_regs(int32_t (&v)[NR], int y0, int H) {
     const int nsteps = REV ? 2 : 4;
+    // a window wholly inside [0, H) needs no boundary selects (wave-uniform
+    // for the vertical pass; per item for the horizontal one)
+    const bool interior = y0 >= 0 && y0 + NR <= H;
 #pragma unroll
     for (int s = 0; s < nsteps; s++) {
         const int par = (s & 1) ? 0 : 1;
@@ -187,8 +190,8 @@ __device__ __forceinline__ void lift_regs(int32_t (&v)[NR], int y0, int H) {
         for (int i = par; i < NR; i += 2) {
             const int y = y0 + i;
             const int im = i > 0 ? i - 1 : i + 1, ip = i + 1 < NR ? i + 1 : i - 1;
-            const int32_t l = (y == 0) ? v[ip] : v[im];
-            const int32_t r = (y + 1 < H) ? v[ip] : v[im];
+            const int32_t l = (!interior && y == 0) ? v[ip] : v[im];
+            const int32_t r = (interior || y + 1 < H) ? v[ip] : v[im];
             if (REV) {
                 if (s == 0) v[i] -= (l + r) >> 1;
                 else v[i] += (l + r + 2) >> 2;
@@ -206,6 +209,58 @@ __device__ __forceinline__ void lift_regs(int32_t (&v)[NR], int y0, int H) {
 // tile-component: vertical lifting in registers (thread = column, window of
 // RB + 2*halo rows), the RB kept rows through LDS for horizontal lifting,
 // then the de-interleaved write.
+// Horizontal lifting (in LDS, thread = sample, row loop uniform), then
+// scaling and the de-interleaved write -- consecutive threads store
+// consecutive words, whole 256-byte runs per wave-instruction -- of NROWS
+// staged rows (LDS row r at lds + kPadL + r * ld).  rows(r, lrow, hrow)
+// names row r's output rows (false: row r was not staged).  A register
+// variant (16-sample segments, 16-byte stores) measured slower: its stores
+// scatter over many lines per wave-instruction.
+constexpr int kPadL = 4;   // LDS words in front of row 0 (the first segment's left halo)
+// LDS row stride for W samples: a multiple of 4 words (16-byte reads), = 4
+// mod 64 so consecutive rows start on different banks
+__host__ __device__ constexpr int lds_row_stride(int W) { return ((W + 63) & ~63) + 4; }
+constexpr int kPadR = 24;  // LDS words after the last row (the last segment's right halo)
+
+template <bool REV, int NROWS, typename RowFn>
+__device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn rows) {
+    const int tid = threadIdx.x;
+    int32_t *base = lds + kPadL;
+    if (W > 1) {
+        const int nsteps = REV ? 2 : 4;
+        for (int s = 0; s < nsteps; s++) {
+            const int par = (s & 1) ? 0 : 1;
+            const int cnt = par ? W / 2 : (W + 1) / 2;
+            for (int r = 0; r < NROWS; r++) {
+                int32_t *lr, *hr;
+                if (!rows(r, lr, hr)) continue;
+                int32_t *row = base + r * ld;
+                for (int j = tid; j < cnt; j += kDwtThreads) {
+                    const int x = par + 2 * j;
+                    const int l = x > 0 ? x - 1 : x + 1;
+                    const int rr = x + 1 < W ? x + 1 : x - 1;
+                    lift_update<REV>(row, x, l, rr, s);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // scale + de-interleave: consecutive threads write consecutive words
+    const int nlh = (W + 1) / 2;
+    for (int r = 0; r < NROWS; r++) {
+        int32_t *lrow, *hrow;
+        if (!rows(r, lrow, hrow)) continue;
+        const int32_t *row = base + r * ld;
+        for (int j = tid; j < W; j += kDwtThreads) {
+            const bool lo = j < nlh;
+            const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
+            int32_t v = row[x];
+            if (!REV && W > 1) v = __float_as_int(__int_as_float(v) * (lo ? INVK97 : K97));
+            (lo ? lrow : hrow)[j] = v;
+        }
+    }
+}
+
 template <bool REV, bool INGEST, int RB>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     extern __shared__ int32_t lds[];
@@ -219,7 +274,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     const int nkeep = min(RB, H - r0);
     const int y0 = r0 - kDwtHalo;
     const int tid = threadIdx.x;
-    const int ld = W;
+    const int ld = lds_row_stride(W);
     // ---- vertical: one column per thread, in registers ----
     for (int x = tid; x < W; x += kDwtThreads) {
         int32_t v[NR];
@@ -238,44 +293,129 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < RB; i++)
-            if (i < nkeep) lds[i * ld + x] = v[kDwtHalo + i];
+            if (i < nkeep) lds[kPadL + i * ld + x] = v[kDwtHalo + i];
     }
     __syncthreads();
-    // ---- horizontal lifting of the kept rows ----
-    if (W > 1) {
-        const int nsteps = REV ? 2 : 4;
-        for (int s = 0; s < nsteps; s++) {
-            const int par = (s & 1) ? 0 : 1;
-            const int cnt = par ? W / 2 : (W + 1) / 2;
-            for (int k = 0; k < nkeep; k++) {
-                const int base = k * ld;
-                for (int j = tid; j < cnt; j += kDwtThreads) {
-                    const int x = par + 2 * j;
-                    const int l = x > 0 ? x - 1 : x + 1;
-                    const int r = x + 1 < W ? x + 1 : x - 1;
-                    lift_update<REV>(lds, base + x, base + l, base + r, s);
-                }
-            }
-            __syncthreads();
-        }
-    }
-    // ---- scale + de-interleave + write ----
-    const int nlv = (H + 1) / 2, nlh = (W + 1) / 2;
+    // ---- horizontal lifting, scaling and de-interleaved write ----
+    const int nlv = (H + 1) / 2;
     int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
     int32_t *ll = a.ll ? (int32_t *)a.ll + (size_t)tc * a.ll_tc : nullptr;
-    for (int k = 0; k < nkeep; k++) {
+    hlift_write<REV, RB>(lds, W, ld, [&](int k, int32_t *&lrow, int32_t *&hrow) -> bool {
+        if (k >= nkeep) return false;
         const int y = r0 + k;
         const bool ylo = (y & 1) == 0;
-        int32_t *drow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
-        int32_t *lrow = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : drow;
-        for (int j = tid; j < W; j += kDwtThreads) {
-            const bool lo = j < nlh;
-            const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
-            int32_t v = lds[k * ld + x];
-            if (!REV && W > 1) v = __float_as_int(__int_as_float(v) * (lo ? INVK97 : K97));
-            (lo ? lrow : drow)[j] = v;
+        hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
+        lrow = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : hrow;
+        return true;
+    });
+}
+
+// Level 1 with ingest, every component of a tile at once: a workgroup owns
+// RB output rows of one tile; thread = column.  Each TIFF pixel of the band
+// (+ halo) is read once for all its components -- the colour transform needs
+// all three anyway -- instead of once per tile-component workgroup; the
+// vertical lifting of each component runs in registers, the kept rows of all
+// components go through LDS for the horizontal lifting, and the
+// de-interleaved write puts HL/LH/HH in their final Mallat place and LL in the
+// next level's scratch.  Same expressions as band_load / lift_regs /
+// k_dwt_band (bit-exact with the oracle).
+template <bool REV, int NC, int RB>
+__global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
+    extern __shared__ int32_t lds[];
+    constexpr int NR = RB + 2 * kDwtHalo;
+    const int t = blockIdx.y;          // tile (part-local)
+    const int tc0 = t * NC;
+    const int W = a.tc_w[tc0], H = a.tc_h[tc0];
+    const int r0 = blockIdx.x * RB;
+    if (r0 >= H) return;
+    const int nkeep = min(RB, H - r0);
+    const int y0 = r0 - kDwtHalo;
+    const int tid = threadIdx.x;
+    const int ld = lds_row_stride(W);
+    const int32_t off = 1 << (a.bits - 1);
+    const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : NC) * (a.bits >> 3);
+    const int gx0 = (t % a.ntx) * a.tile_w, gy0 = a.row0 + (t / a.ntx) * a.tile_h;
+    const bool mct = a.mct && NC >= 3;
+    // byte offset of each window row (per component plane when planar):
+    // wave-uniform, computed once per workgroup instead of per column
+    uint64_t rowoff[NC][NR];
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        const int y = min(max(y0 + i, 0), H - 1);
+        const int gy = gy0 + y;
+        const int strip = gy / a.rps;
+        const size_t ly = (size_t)(gy - strip * a.rps) * row_bytes;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+            rowoff[c][i] = a.strip_off[a.planar == 2 ? (size_t)c * a.spp_strips + strip : (size_t)strip] + ly;
+    }
+    const int bps = a.bits >> 3;
+    for (int x = tid; x < W; x += kDwtThreads) {
+        int32_t v[NC][NR];
+        const int gx = gx0 + x;
+        const size_t xo = a.planar == 2 ? (size_t)gx * bps : (size_t)gx * NC * bps;
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const int y = y0 + i;
+            int32_t smp[NC];
+            if (y >= 0 && y < H) {
+#pragma unroll
+                for (int c = 0; c < NC; c++) {
+                    const uint8_t *p8 = a.tif + (a.planar == 2 ? rowoff[c][i] : rowoff[0][i] + (size_t)c * bps) + xo;
+                    if (a.bits == 8) smp[c] = (int32_t)p8[0];
+                    else smp[c] = a.big_endian ? (((int32_t)p8[0] << 8) | p8[1]) : (p8[0] | ((int32_t)p8[1] << 8));
+                    smp[c] -= off;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < NC; c++) smp[c] = 0;
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) v[c][i] = REV ? smp[c] : __float_as_int((float)smp[c]);
+            if constexpr (NC >= 3) if (mct) {
+                if (REV) {
+                    v[0][i] = (smp[0] + 2 * smp[1] + smp[2]) >> 2;
+                    v[1][i] = smp[2] - smp[1];
+                    v[2][i] = smp[0] - smp[1];
+                } else {
+                    const float R = (float)smp[0], G = (float)smp[1], B = (float)smp[2];
+                    float f0 = 0.299f * R; f0 = f0 + 0.587f * G; f0 = f0 + 0.114f * B;
+                    float f1 = -0.16875f * R; f1 = f1 - 0.33126f * G; f1 = f1 + 0.5f * B;
+                    float f2 = 0.5f * R; f2 = f2 - 0.41869f * G; f2 = f2 - 0.08131f * B;
+                    v[0][i] = __float_as_int(f0);
+                    v[1][i] = __float_as_int(f1);
+                    v[2][i] = __float_as_int(f2);
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (H > 1) {
+                lift_regs<REV, NR>(v[c], y0, H);
+                if (!REV) {
+#pragma unroll
+                    for (int i = kDwtHalo; i < kDwtHalo + RB; i++)
+                        v[c][i] = __float_as_int(__int_as_float(v[c][i]) * ((i & 1) ? K97 : INVK97));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < RB; i++)
+                if (i < nkeep) lds[kPadL + (c * RB + i) * ld + x] = v[c][kDwtHalo + i];
         }
     }
+    __syncthreads();
+    // ---- horizontal lifting, scaling and de-interleaved write ----
+    const int nlv = (H + 1) / 2;
+    hlift_write<REV, NC * RB>(lds, W, ld, [&](int r, int32_t *&lrow, int32_t *&hrow) -> bool {
+        const int c = r / RB, k = r - c * RB;
+        if (k >= nkeep) return false;
+        const int tc = tc0 + c, y = r0 + k;
+        const bool ylo = (y & 1) == 0;
+        int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
+        hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
+        lrow = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride : hrow;
+        return true;
+    });
 }
 
 struct DwtTailArgs {
@@ -289,73 +429,97 @@ struct DwtTailArgs {
     int level, levels;
 };
 
-// Levels level..levels of one tile-component, entirely in LDS.
+// Levels level..levels of one tile-component, entirely in LDS.  1024 threads
+// as 8 rows x 128 columns (no index divisions; a tail level is <= 128 x 128
+// for the recipe's tiles).  Each level works in place on the previous
+// level's LL, which stays where it was computed -- element (i, j) of level
+// k's input at LDS (i << k) * ld + (j << k) -- so no compaction pass.
+constexpr int kTailThreads = 1024;
+constexpr int kTailCols = 128, kTailRows = kTailThreads / kTailCols;
 template <bool REV>
-__global__ void __launch_bounds__(kDwtThreads) k_dwt_tail(DwtTailArgs a) {
+__device__ __forceinline__ void tail_lift(int32_t *x, int idx, int lidx, int ridx, int step) {
+    if (REV) {
+        if (step == 0) x[idx] -= (x[lidx] + x[ridx]) >> 1;
+        else x[idx] += (x[lidx] + x[ridx] + 2) >> 2;
+    } else {
+        float *f = (float *)x;
+        const float cf = step == 0 ? A97 : (step == 1 ? B97 : (step == 2 ? G97 : D97));
+        float t = f[lidx] + f[ridx];
+        t = cf * t;
+        f[idx] = f[idx] + t;
+    }
+}
+
+template <bool REV>
+__global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
     __shared__ int32_t lds[kDwtLdsWords];
     const int tc = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int tx = threadIdx.x & (kTailCols - 1), ty = threadIdx.x / kTailCols;
     int sh = a.level - 1;
     int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh;
     int H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
+    const int ld = W;  // row stride of the level-`level` input
     {
         const int32_t *s = (const int32_t *)a.src + (size_t)tc * a.src_tc;
-        for (int it = tid; it < W * H; it += kDwtThreads) {
-            const int y = it / W, x = it - y * W;
-            lds[it] = s[(size_t)y * a.src_stride + x];
-        }
+        for (int y = ty; y < H; y += kTailRows)
+            for (int x = tx; x < W; x += kTailCols) lds[y * ld + x] = s[(size_t)y * a.src_stride + x];
     }
     __syncthreads();
     int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
-    for (int lv = a.level; lv <= a.levels; lv++) {
-        const int ld = W;
-        lift_vertical<REV>(lds, 0, H, H, W, ld);
+    const int nsteps = REV ? 2 : 4;
+    for (int lv = a.level, k = 0; lv <= a.levels; lv++, k++) {
+        const int rs = ld << k, cs = 1 << k;  // strides of this level's samples
+        // vertical lifting (odd rows first), symmetric extension at 0 / H-1
+        if (H > 1)
+            for (int st = 0; st < nsteps; st++) {
+                const int par = (st & 1) ? 0 : 1;
+                for (int y = par + 2 * ty; y < H; y += 2 * kTailRows) {
+                    const int l = y > 0 ? y - 1 : y + 1, r = y + 1 < H ? y + 1 : y - 1;
+                    for (int x = tx; x < W; x += kTailCols) tail_lift<REV>(lds, y * rs + x * cs, l * rs + x * cs, r * rs + x * cs, st);
+                }
+                __syncthreads();
+            }
         if (!REV && H > 1) {
             float *f = (float *)lds;
-            for (int it = tid; it < W * H; it += kDwtThreads) {
-                const int y = it / W;
-                f[it] = (y & 1) ? f[it] * K97 : f[it] * INVK97;
-            }
+            for (int y = ty; y < H; y += kTailRows)
+                for (int x = tx; x < W; x += kTailCols) {
+                    const int o = y * rs + x * cs;
+                    f[o] = (y & 1) ? f[o] * K97 : f[o] * INVK97;
+                }
             __syncthreads();
         }
-        lift_horizontal<REV>(lds, 0, H, W, ld);
+        if (W > 1)
+            for (int st = 0; st < nsteps; st++) {
+                const int par = (st & 1) ? 0 : 1;
+                for (int y = ty; y < H; y += kTailRows)
+                    for (int x = par + 2 * tx; x < W; x += 2 * kTailCols) {
+                        const int l = x > 0 ? x - 1 : x + 1, r = x + 1 < W ? x + 1 : x - 1;
+                        tail_lift<REV>(lds, y * rs + x * cs, y * rs + l * cs, y * rs + r * cs, st);
+                    }
+                __syncthreads();
+            }
         const int nlv = (H + 1) / 2, nlh = (W + 1) / 2;
         const bool last = lv == a.levels;
-        // high bands (and the final LL) straight to HBM
-        for (int it = tid; it < W * H; it += kDwtThreads) {
-            const int y = it / W, j = it - y * W;
-            const bool lo = j < nlh, ylo = (y & 1) == 0;
-            if (lo && ylo && !last) continue;
-            const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
-            int32_t v = lds[y * ld + x];
-            if (!REV && W > 1) {
-                float f = __int_as_float(v);
-                f = lo ? f * INVK97 : f * K97;
-                v = __float_as_int(f);
+        // high bands (and the final LL) straight to HBM; the LL of a
+        // non-final level is scaled in place (each element by its owner)
+        for (int y = ty; y < H; y += kTailRows) {
+            const bool ylo = (y & 1) == 0;
+            int32_t *drow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
+            for (int j = tx; j < W; j += kTailCols) {
+                const bool lo = j < nlh;
+                const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
+                const int o = y * rs + x * cs;
+                int32_t v = lds[o];
+                if (!REV && W > 1) {
+                    float f = __int_as_float(v);
+                    f = lo ? f * INVK97 : f * K97;
+                    v = __float_as_int(f);
+                }
+                if (lo && ylo && !last) lds[o] = v;
+                else drow[j] = v;
             }
-            dst[(size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w + j] = v;
         }
         if (last) break;
-        // compact LL (rows 2i, columns 2j, scaled) to the front of LDS
-        constexpr int kPer = kDwtLdsWords / 4 / kDwtThreads;  // LL <= 4096 words
-        int32_t keep[kPer];
-        const int nll = nlv * nlh;
-#pragma unroll
-        for (int q = 0; q < kPer; q++) {
-            const int it = tid + q * kDwtThreads;
-            if (it < nll) {
-                const int i = it / nlh, j = it - i * nlh;
-                int32_t v = lds[(2 * i) * ld + 2 * j];
-                if (!REV && W > 1) v = __float_as_int(__int_as_float(v) * INVK97);
-                keep[q] = v;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < kPer; q++) {
-            const int it = tid + q * kDwtThreads;
-            if (it < nll) lds[it] = keep[q];
-        }
         __syncthreads();
         W = nlh;
         H = nlv;
@@ -377,6 +541,24 @@ static void launch_band_rb(int RB, dim3 g, size_t lds, hipStream_t st, const Dwt
     if (RB == 32) launch_band<REV, INGEST, 32>(g, lds, st, a);
     else if (RB == 16) launch_band<REV, INGEST, 16>(g, lds, st, a);
     else launch_band<REV, INGEST, 8>(g, lds, st, a);
+}
+
+template <bool REV, int NC>
+static void launch_l1_nc(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    static bool wide = false;
+    if (lds > (size_t)kDwtLdsWords * 4 && !wide) {
+        (void)hipFuncSetAttribute((const void *)k_dwt_l1<REV, NC, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kDwtLdsWordsWide * 4);
+        wide = true;
+    }
+    hipLaunchKernelGGL((k_dwt_l1<REV, NC, 8>), g, dim3(kDwtThreads), lds, st, a);
+}
+template <bool REV>
+static void launch_l1(int nc, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    if (nc == 1) launch_l1_nc<REV, 1>(g, lds, st, a);
+    else if (nc == 2) launch_l1_nc<REV, 2>(g, lds, st, a);
+    else if (nc == 3) launch_l1_nc<REV, 3>(g, lds, st, a);
+    else launch_l1_nc<REV, 4>(g, lds, st, a);
 }
 
 // Ingest + all DWT levels on `st`.  Returns false on a launch error.
@@ -407,8 +589,8 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             t.plane = a.plane;
             t.tc_w = p.tc_w; t.tc_h = p.tc_h;
             t.level = lv; t.levels = p.levels;
-            if (p.reversible) hipLaunchKernelGGL(k_dwt_tail<true>, dim3(p.ntc), dim3(kDwtThreads), 0, st, t);
-            else hipLaunchKernelGGL(k_dwt_tail<false>, dim3(p.ntc), dim3(kDwtThreads), 0, st, t);
+            if (p.reversible) hipLaunchKernelGGL(k_dwt_tail<true>, dim3(p.ntc), dim3(kTailThreads), 0, st, t);
+            else hipLaunchKernelGGL(k_dwt_tail<false>, dim3(p.ntc), dim3(kTailThreads), 0, st, t);
             return hipGetLastError() == hipSuccess;
         }
         // kept rows per workgroup: 16, or 8 for rows wider than 2048
@@ -425,9 +607,17 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
         a.ll = lv == p.levels ? nullptr : scratch[lv & 1];
         a.ll_stride = ll_stride;
         a.ll_tc = ll_tc;
-        const size_t lds = (size_t)R * maxW * 4;
+        const size_t lds = ((size_t)R * lds_row_stride(maxW) + kPadL + kPadR) * 4;
         dim3 g((maxH + R - 1) / R, p.ntc);
-        if (lv == 1) {
+        // level 1: every component of a tile in one workgroup when its rows
+        // fit in LDS (each TIFF pixel read once)
+        constexpr int kRb1 = 8;
+        const size_t lds1 = ((size_t)p.nc * kRb1 * lds_row_stride(maxW) + kPadL + kPadR) * 4;
+        if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
+            dim3 g1((maxH + kRb1 - 1) / kRb1, p.ntc / p.nc);
+            if (p.reversible) launch_l1<true>(p.nc, g1, lds1, st, a);
+            else launch_l1<false>(p.nc, g1, lds1, st, a);
+        } else if (lv == 1) {
             if (p.reversible) launch_band_rb<true, true>(R, g, lds, st, a);
             else launch_band_rb<false, true>(R, g, lds, st, a);
         } else {

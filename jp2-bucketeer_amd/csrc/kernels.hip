@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "device_common.h"
@@ -541,99 +542,128 @@ struct QuantArgs {
     uint32_t *est;         // [block][32] predicted coded size of plane p, 1/16 bit
 };
 
+// v_writelane_b32 (the LLVM intrinsic, so the compiler pads the VALU-SGPR
+// hazard after the ballot): lane `L` of `old` takes the wave-uniform `v`
+__device__ int amdgcn_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+template <int L>
+__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v) {
+    return (uint32_t)amdgcn_writelane((int)v, L, (int)old);
+}
+template <int Y, typename F>
+__device__ __forceinline__ void unroll_rows(F &&f) {
+    if constexpr (Y < 64) {
+        f(std::integral_constant<int, Y>{});
+        unroll_rows<Y + 1>(f);
+    }
+}
+
+template <bool REV>
 __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     int b = blockIdx.x;
     BlockDesc d = a.blocks[b];
     int lane = threadIdx.x;
     bool act = lane < d.w;
     const int32_t *src = (const int32_t *)a.coef + (size_t)d.tc * a.plane_w * a.plane_h +
-                         (size_t)d.y0 * a.plane_w + d.x0;
-    int32_t *sm = a.sm + d.sm_off;
+                         (size_t)d.y0 * a.plane_w + d.x0 + (act ? lane : 0);
+    int32_t *sm = a.sm + d.sm_off + lane;
     uint32_t vmax = 0;
     uint32_t lim = (1u << d.Mb) - 1u;
     // the lane's column stays in registers (sign | magnitude; 0 outside the
     // block) for the bit-plane and distortion passes: the coefficients are
-    // read from HBM once
+    // read from HBM once.  Rows past the block end are a wave-uniform exit;
+    // lanes past its width read column 0 and keep 0.
     uint32_t col[64];
 #pragma unroll
     for (int y = 0; y < 64; y++) {
         col[y] = 0;
-        if (!act || y >= d.h) continue;
-        int32_t raw = src[(size_t)y * a.plane_w + lane];
+        if (y >= d.h) continue;
+        const int32_t raw = src[(size_t)y * a.plane_w];
         uint32_t v, s;
-        if (a.reversible) {
+        if constexpr (REV) {
             s = raw < 0;
             v = (uint32_t)(raw < 0 ? -raw : raw);
         } else {
-            float cf = __int_as_float(raw);
+            const float cf = __int_as_float(raw);
             s = cf < 0.0f;
-            float t = fabsf(cf) * d.inv_delta;
-            v = (uint32_t)floorf(t);
+            v = (uint32_t)floorf(fabsf(cf) * d.inv_delta);
         }
-        if (v > lim) v = lim;
-        col[y] = (s << 31) | v;
-        sm[y * 64 + lane] = (int32_t)col[y];
+        v = act ? min(v, lim) : 0u;
+        col[y] = act ? (s << 31) | v : 0u;
+        sm[y * 64] = (int32_t)col[y];
         vmax = max(vmax, v);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-    int P = vmax ? 32 - __clz(vmax) : 0;
+    // the wave-reduced maximum is uniform: keep P (and the plane loop) scalar
+    const int P = __builtin_amdgcn_readfirstlane(vmax ? 32 - __clz(vmax) : 0);
     if (lane == 0) a.P[b] = (uint8_t)P;
     uint64_t *B = a.bp + d.bp_off;
     uint64_t *S = B + (size_t)d.Mb * 64;
     uint64_t *SG = B + (size_t)2 * d.Mb * 64;
-    // lane p also gathers plane p's slope-prediction counts (oracle
-    // plane_stats): significant samples, and insignificant samples with a
-    // significant 8-neighbour (row y-1 is finalised once row y is known)
+    // Planes top-down, rows across the wave: for plane p, row y's mask of
+    // columns with bit p set is one ballot, parked in lane y by writelane, so
+    // after the 64 rows lane y holds B[p][y] and S[p][y] = S[p+1][y] | B[p][y]
+    // and each plane leaves in two coalesced 512-byte stores.  The plane's
+    // slope-prediction counts (oracle plane_stats: significant samples, and
+    // insignificant samples with a significant 8-neighbour) and its exact
+    // distortion decreases (MRP: samples significant above p; significance:
+    // samples whose top bit is p) come from the same pass.
     const uint64_t wmask = d.w >= 64 ? ~0ull : ((1ull << d.w) - 1ull);
     auto dil = [](uint64_t m) { return m | (m << 1) | (m >> 1); };
-    uint64_t up = 0, mid = 0;
-    uint32_t cntS = 0, nnb = 0;
+    {
+        uint32_t sg_lo = 0, sg_hi = 0;
+        unroll_rows<0>([&](auto yc) {
+            constexpr int y = decltype(yc)::value;
+            const uint64_t m = __ballot(col[y] >> 31);
+            sg_lo = writelane<y>(sg_lo, (uint32_t)m);
+            sg_hi = writelane<y>(sg_hi, (uint32_t)(m >> 32));
+        });
+        SG[lane] = ((uint64_t)sg_hi << 32) | sg_lo;
+    }
+    // magnitudes only from here on (fewer live values in the plane loop)
 #pragma unroll
     for (int y = 0; y < 64; y++) {
-        if (y >= d.h) continue;  // (continue, not break: the loop must unroll)
-        const uint32_t word = col[y];
-        const uint32_t v = word & 0x7FFFFFFFu;
-        uint64_t myB = 0, myS = 0;
-        for (int p = 0; p < P; p++) {
-            uint64_t bm = __ballot((v >> p) & 1u);
-            uint64_t sm2 = __ballot((v >> p) != 0u);
-            if (lane == p) { myB = bm; myS = sm2; }
-        }
-        uint64_t sg = __ballot(word >> 31);
-        if (lane < P) {
-            B[(size_t)lane * 64 + y] = myB;
-            S[(size_t)lane * 64 + y] = myS;
-        }
-        if (lane == 63) SG[y] = sg;
-        cntS += __popcll(myS);
-        if (y > 0) nnb += __popcll((dil(up) | dil(mid) | dil(myS)) & ~mid & wmask);
-        up = mid;
-        mid = myS;
+        col[y] &= 0x7FFFFFFFu;
+        asm volatile("" : "+v"(col[y]));  // the signed copies die here
     }
-    nnb += __popcll((dil(up) | dil(mid)) & ~mid & wmask);
-    {
-        const uint32_t nref = (uint32_t)__shfl_down((int)cntS, 1, 64);  // |S[p+1]|
-        const uint32_t nnew = cntS - (lane < 63 ? nref : 0u);
-        if (lane < P) a.est[(size_t)b * 32 + lane] = 16u * (lane < 63 ? nref : 0u) + 56u * nnew + 5u * nnb;
-    }
-    bool lossless = a.reversible != 0;
-    for (int p = 0; p < P; p++) {
+    constexpr bool lossless = REV;
+    constexpr int dd = lossless ? 0 : 1;  // reconstruction offset, half-units
+    uint64_t rowS = 0;
+    uint32_t cnt_above = 0;  // |S[p+1]|
+    for (int p = P - 1; p >= 0; p--) {
+        uint32_t b_lo = 0, b_hi = 0;
         int64_t ref = 0, sig = 0;
-        if (p <= 13) {  // wave-uniform: 32-bit squares suffice (device_common.h)
+        unroll_rows<0>([&](auto yc) {
+            constexpr int y = decltype(yc)::value;
+            const uint32_t v = col[y];  // 0 outside the block
+            const uint64_t m = __ballot((v >> p) & 1u);
+            b_lo = writelane<y>(b_lo, (uint32_t)m);
+            b_hi = writelane<y>(b_hi, (uint32_t)(m >> 32));
+        });
+        // Distortion decreases of the plane (oracle dist_gain, half-units,
+        // d = reconstruction offset): a sample whose top bit is p gains
+        // 2^p (12 v + 6d - 9 2^p); one significant above p, with l = v mod
+        // 2^p, gains 2^p (4l + 2d - 2^p) if bit p is set, else
+        // 2^p (3 2^p - 4l - 2d); lossless p = 0 gains 4 for a new sample
+        // and for a refined 0 bit, nothing else.  So the plane needs the
+        // per-lane sums of v (top bit p) and of +-l (refined), int32 up to
+        // p = 23, and the counts, which come from the masks.
+        int32_t sv = 0, sl = 0;
+        if (p <= 23) {
+            const uint32_t lm = (1u << p) - 1u;
 #pragma unroll
             for (int y = 0; y < 64; y++) {
-                const uint32_t v = col[y] & 0x7FFFFFFFu;  // 0 outside the block
+                const uint32_t v = col[y];
                 const uint32_t hi = v >> p;
-                if (hi == 0) continue;
-                const int64_t g = dist_gain_small(v, p, lossless);
-                if (hi == 1) sig += g;
-                else ref += g;
+                const int32_t l = (int32_t)(v & lm);
+                sv += hi == 1 ? (int32_t)v : 0;
+                sl += hi > 1 ? ((hi & 1u) ? l : -l) : 0;
             }
         } else {
-#pragma unroll
-            for (int y = 0; y < 64; y++) {
-                const uint32_t v = col[y] & 0x7FFFFFFFu;
+            // 64-bit gains per row, the column re-read from the sign-magnitude
+            // copy (never for <= 16-bit sources)
+            for (int y = 0; y < d.h; y++) {
+                const uint32_t v = (uint32_t)sm[y * 64] & 0x7FFFFFFFu;
                 const uint32_t hi = v >> p;
                 if (hi == 0) continue;
                 const int64_t g = dist_gain(v, p, lossless);
@@ -641,12 +671,42 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
                 else ref += g;
             }
         }
-        ref = wave_sum64(ref);
-        sig = wave_sum64(sig);
+        const uint64_t rowB = ((uint64_t)b_hi << 32) | b_lo;
+        uint32_t nb1 = (uint32_t)__popcll(rowB & rowS);  // refined samples with bit p set
+        rowS |= rowB;
+        B[(size_t)p * 64 + lane] = rowB;
+        S[(size_t)p * 64 + lane] = rowS;
+        // counts: lane y's row with its neighbours y-1 / y+1 (0 outside)
+        const uint64_t upS = lane > 0 ? (uint64_t)__shfl_up((long long)rowS, 1, 64) : 0ull;
+        const uint64_t dnS = lane < 63 ? (uint64_t)__shfl_down((long long)rowS, 1, 64) : 0ull;
+        const uint32_t nb = lane < d.h ? (uint32_t)__popcll((dil(upS) | dil(rowS) | dil(dnS)) & ~rowS & wmask) : 0u;
+        uint32_t cS = (uint32_t)__popcll(rowS), cN = nb;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            cS += (uint32_t)__shfl_xor((int)cS, o, 64);
+            cN += (uint32_t)__shfl_xor((int)cN, o, 64);
+            nb1 += (uint32_t)__shfl_xor((int)nb1, o, 64);
+        }
+        if (p <= 23) {
+            const int64_t SV = wave_sum64(sv), SL = wave_sum64(sl);
+            const int64_t n1 = cS - cnt_above, nr1 = nb1, nr0 = cnt_above - nb1, q = (int64_t)1 << p;
+            if (lossless && p == 0) {
+                sig = 4 * n1;
+                ref = 4 * nr0;
+            } else {
+                sig = q * (12 * SV + (6 * dd - 9 * q) * n1);
+                ref = q * (4 * SL + nr1 * (2 * dd - q) + nr0 * (3 * q - 2 * dd));
+            }
+        } else {
+            ref = wave_sum64(ref);
+            sig = wave_sum64(sig);
+        }
         if (lane == 0) {
+            a.est[(size_t)b * 32 + p] = 16u * cnt_above + 56u * (cS - cnt_above) + 5u * cN;
             a.dref[(size_t)b * 32 + p] = ref;
             a.dsig[(size_t)b * 32 + p] = sig;
         }
+        cnt_above = cS;
     }
 }
 
@@ -1156,7 +1216,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.dref = (int64_t *)dref.ptr;
     qa.dsig = (int64_t *)dsig.ptr;
     qa.est = (uint32_t *)est.ptr;
-    if (nb) hipLaunchKernelGGL(k_quant, dim3(nb), dim3(64), 0, stream, qa);
+    if (nb) {
+        if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, dim3(nb), dim3(64), 0, stream, qa);
+        else hipLaunchKernelGGL(k_quant<false>, dim3(nb), dim3(64), 0, stream, qa);
+    }
     HIPCHECK(hipGetLastError());
     // S4b: slope prediction -> lowest coded plane per block
     if (skip_target > 0 && nb) {
