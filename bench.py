@@ -315,7 +315,7 @@ def run(args):
             "data": "synthetic (sinusoids + checker + N(0,6) noise, seed 1234+rank), in-memory baseline TIFF",
             "config": {"workload": "C2: 6000x4000 RGB8 TIFF -> JPX, lossy 9/7 3 bpp, Kakadu recipe "
                                    "(6 levels, 6 layers, 512^2 tiles, 64^2 blocks, RPCL, SOP/EPH/PLT, TP=R)",
-                       "image": "6000x4000x3 u8", "images_in_flight_per_gpu": nf,
+                       "image": "6000x4000x3 u8", "images_in_flight_per_gpu": nf, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "timed_span": "TIFF resident in HBM -> JPX bytes in host memory (jp2hip_encode_device)",
                        "parallelism": f"replicas x{world}", "out_bytes": int(avg["out_bytes"]),
                        "bpp": round(8 * avg["out_bytes"] / npx, 4),
@@ -548,10 +548,14 @@ def main():
                          "c5: one oversized image tile-split across ranks")
     args = ap.parse_args()
     # one hardware queue per in-flight context plus a few for the runtime's
-    # own streams (HIP's default of 4 makes contexts share queues, and the
-    # kernels of a shared queue run one at a time); must be set before
-    # anything initialises HIP.  Sweep: profiles/r01/sweep_q2.txt
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, args.inflight + 4))))
+    # own streams: with HIP's default of 4 (exported as such on the GPU
+    # boxes) the 12 contexts share 4 queues, and the kernels of a shared
+    # queue run one at a time -- the tier-1 MQ kernel (few waves, long) then
+    # runs alone for a fifth of the time.  The deployment sets the same for
+    # the Bucketeer JVM.  Must be set before anything
+    # initialises HIP.  Sweep: profiles/r02/hwq_sweep.txt
+    if not os.environ.get("JP2HIP_KEEP_HW_QUEUES"):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(4, min(32, args.inflight + 4)))
     if args.workload == "c4":
         res = run_c4(args)
         if res is not None:

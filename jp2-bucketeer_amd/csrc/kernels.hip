@@ -1164,6 +1164,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     HIPCHECK(hipEventRecord(ev[0], stream));
     HIPCHECK(hipEventRecord(ev[1], stream));
     const char *dd = getenv("JP2HIP_DUMP_DIR");
+    // experiment knob: launch one stage twice (its marginal cost under load)
+    const char *rep = getenv("JP2HIP_REPEAT_STAGE");
+    const int nrep_dwt = rep && !strcmp(rep, "dwt") ? 2 : 1, nrep_quant = rep && !strcmp(rep, "quant") ? 2 : 1;
+    const int nrep_cm = rep && !strcmp(rep, "cm") ? 2 : 1, nrep_mq = rep && !strcmp(rep, "mq") ? 2 : 1;
     if (plan.rc.levels == 0) {
         // S1+S2 only: no decomposition
         IngestArgs ia;
@@ -1197,10 +1201,11 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
         dl.coef = coef.ptr; dl.scratch0 = llbuf0.ptr; dl.scratch1 = llbuf1.ptr;
-        if (!launch_dwt(dl, stream)) {
-            err = std::string("DWT launch failed: ") + hipGetErrorString(hipGetLastError());
-            return false;
-        }
+        for (int r = 0; r < nrep_dwt; r++)
+            if (!launch_dwt(dl, stream)) {
+                err = std::string("DWT launch failed: ") + hipGetErrorString(hipGetLastError());
+                return false;
+            }
     }
     HIPCHECK(hipEventRecord(ev[2], stream));
     if (dd && !dump(dd, "dwt.bin", coef, plane * plan.ntc * 4, err)) return false;
@@ -1216,7 +1221,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.dref = (int64_t *)dref.ptr;
     qa.dsig = (int64_t *)dsig.ptr;
     qa.est = (uint32_t *)est.ptr;
-    if (nb) {
+    for (int r = 0; nb && r < nrep_quant; r++) {
         if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, dim3(nb), dim3(64), 0, stream, qa);
         else hipLaunchKernelGGL(k_quant<false>, dim3(nb), dim3(64), 0, stream, qa);
     }
@@ -1298,7 +1303,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ca.counts = (uint4 *)counts.ptr;
     ca.dspp = (int64_t *)dspp.ptr;
     ca.lossless = plan.rc.reversible;
-    launch_t1_cm(ca, stream);
+    for (int r = 0; r < nrep_cm; r++) launch_t1_cm(ca, stream);
     HIPCHECK(hipGetLastError());
     // MQ lane order: blocks by decreasing decision count
     if (!ensure<uint32_t>(ordkey, nb, err) || !ensure<uint32_t>(ordkey2, nb, err) || !ensure<int32_t>(ordval, nb, err))
@@ -1346,7 +1351,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!ensure<int64_t>(dbgbuf, (size_t)nb * 4, err)) return false;
         ma.dbg = (int64_t *)dbgbuf.ptr;
     }
-    launch_t1_mq(ma, stream);
+    for (int r = 0; r < nrep_mq; r++) launch_t1_mq(ma, stream);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[4], stream));
     // S6a hulls

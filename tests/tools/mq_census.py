@@ -26,7 +26,7 @@ print("per-block wall us: mean", wt.mean(), "p50", np.median(wt), "p99", np.perc
 print("sum decisions / t1_mq_ms => Gdec/s", dec.sum() / (st.t1_mq_ms * 1e-3) / 1e9)
 print("stages", st.as_dict())
 gi = a[:, 3]
-lanes = int(os.environ.get("JP2HIP_MQ_LANES", "16"))
+lanes = int(os.environ.get("JP2HIP_MQ_LANES", "64"))
 wv = gi[m] // lanes
 import collections
 print("ns per decision (per block wall/dec): p10 %.1f p50 %.1f p90 %.1f" % tuple(np.percentile(wall[m] * 10.0 / dec[m], [10, 50, 90])))
