@@ -27,7 +27,12 @@
 
 namespace jp2hip {
 
-enum { CX_RL = 17, CX_UNI = 18 };
+enum { CX_RL = 17, CX_UNI = 18, CX_PAD = 19 };
+// Every pass stream is padded to a 16-byte boundary with decisions of the
+// neutral context CX_PAD, whose MQ state (Qe = 0, MPS = 0) leaves the coder
+// unchanged: the MQ kernel codes whole 16-decision chunks with no per-decision
+// validity test.
+constexpr uint8_t kPadDecision = CX_PAD << 1;
 
 // zero-coding context (Table D.1) from the 8-neighbour pattern
 // bits: UL U UR L R DL D DR
@@ -70,8 +75,8 @@ __device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m
 
 // bytes reserved per (block, plane) for the three passes' decisions:
 // at most w*h coding decisions + w*h sign decisions + 3 per run-length column
-// (each pass starts on a 16-byte boundary; the MQ kernel reads up to two
-// 16-byte chunks past the end of a pass)
+// (each pass is padded to a 16-byte boundary; the MQ kernel prefetches one
+// 16-byte chunk past the end of a pass)
 __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
     return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
 }
@@ -114,6 +119,13 @@ struct LaneDec {
         n++;
     }
 };
+
+// Pass end: neutral decisions up to the next 16-byte boundary.
+__device__ __forceinline__ int pad_pass(uint8_t *out, int pos, int lane) {
+    const int end = (pos + 15) & ~15;
+    if (lane < end - pos) out[pos + lane] = kPadDecision;
+    return end;
+}
 
 // Stripe hand-off: the lanes' decisions go out in column order (lane c =
 // column c): exclusive prefix of the per-lane counts over the wave, then
@@ -251,7 +263,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
             pos += flush_stripe(out, pos, e, lane);
         }
         n_spp = pos;
-        pos = (pos + 15) & ~15;
+        pos = pad_pass(out, pos, lane);
         const int mrp0 = pos;
         // ---------------- magnitude refinement ----------------
         for (int s = 0; s < nstripes; s++) {
@@ -277,7 +289,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
             pos += flush_stripe(out, pos, e, lane);
         }
         n_mrp = pos - mrp0;
-        pos = (pos + 15) & ~15;
+        pos = pad_pass(out, pos, lane);
     }
     const int cup0 = pos;
     // ---------------- cleanup ----------------
@@ -351,6 +363,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
         pos += flush_stripe(out, pos, e, lane);
     }
     const int n_cup = pos - cup0;
+    pad_pass(out, pos, lane);
     if (spp) {
         // SPP distortion decrease: lane r sums its row's newly significant
         // samples (the sign-magnitude words are read only here)
@@ -424,12 +437,12 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
 // the CODEMPS/CODELPS procedures of Annex C.2 fold into one select -- the
 // interval keeps A-Qe exactly when "MPS" xor "conditional exchange" -- the
 // context moves to NMPS/NLPS exactly when renormalisation happens, and every
-// value of RENORME is computed with selects;
-// the (at most one, common) byte-out is applied by select and its byte is
-// written to the lane's 64-byte LDS ring -- to a dummy slot when nothing is
-// emitted -- so the only per-decision branch is the rare second byte-out of
-// one renormalisation.  `valid` = false makes the step a no-op (partial
-// chunks), again by select.
+// value of RENORME is computed with selects; the (at most one, common)
+// byte-out is applied by select and its byte is written to the lane's
+// 64-byte LDS ring -- to a dummy slot when nothing is emitted -- so the only
+// per-decision branch is the rare second byte-out of one renormalisation.
+// Pass padding (CX_PAD, state 0) makes a step with Qe = 0 and d = MPS: no
+// interval change, no renormalisation, no byte -- so every step is coded.
 __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
     uint32_t B = m.B;
     if (B != 0xFF && m.C >= 0x8000000u) {
@@ -445,48 +458,46 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
 }
 
 __device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint32_t *tab, const uint32_t d,
-                                               const bool valid, uint8_t *ring) {
+                                               uint8_t *ring) {
     const uint32_t qe = t & 0xFFFFu;
-    const uint32_t mps = t >> 31;
+    const bool isM = d == (t >> 31);
     const uint32_t A1 = m.A - qe;
-    const bool isM = d == mps;
     const bool keep = isM != (A1 < qe);
-    const uint32_t An0 = keep ? A1 : qe;
+    const uint32_t An = keep ? A1 : qe;  // never 0: Qe >= 1, and A1 = A >= 0x8000 for Qe = 0
     const uint32_t C0 = m.C + (keep ? qe : 0u);
-    const bool ren = (!isM) || (A1 < 0x8000u);
-    const uint32_t idx = (t >> (isM ? 16 : 22)) & 63u;
-    const uint32_t nm = mps ^ ((isM ? 0u : 1u) & (t >> 28));
-    const uint32_t tw = tab[idx] | (nm << 31);
-    const int n = __clz(An0) - 16;
-    const bool bo = n >= m.CT;
-    const int s1 = bo ? m.CT : n;
+    const bool ren = !isM || A1 < 0x8000u;
+    // next state: NMPS / NLPS entry; an LPS in a SWITCH state flips the MPS
+    const uint32_t tw = tab[__builtin_amdgcn_ubfe(t, isM ? 16u : 22u, 6u)] |
+                        ((isM ? t : (t ^ (t << 3))) & 0x80000000u);
+    const int n = __builtin_clz(An) - 16;  // renormalisation shifts
+    const int CT = m.CT;
+    const bool bo = n >= CT;  // a byte-out inside this renormalisation
+    const int s1 = min(n, CT);
     const uint32_t C1 = C0 << s1;
     const bool carry = (m.B != 0xFFu) && (C1 >= 0x8000000u);
     const uint32_t Bc = m.B + (carry ? 1u : 0u);
     const uint32_t C2 = carry ? (C1 & 0x7FFFFFFu) : C1;
     const bool ff = Bc == 0xFFu;
-    const bool emit = valid && bo;
+    const uint32_t sh = ff ? 20u : 19u;
     // byte -1 (the MQ coder's initial pending byte, never output) lands in
     // slot 63, which byte 63 overwrites before that group is flushed
-    ring[emit ? (m.bp & 63) : 64] = (uint8_t)Bc;
-    uint32_t Cx = bo ? (C2 & (ff ? 0xFFFFFu : 0x7FFFFu)) : C1;
-    int CTx = bo ? (ff ? 7 : 8) : m.CT - n;
+    ring[bo ? (m.bp & 63) : 64] = (uint8_t)Bc;
+    uint32_t Cx = bo ? (C2 & ((1u << sh) - 1u)) : C1;
+    int CTx = bo ? 27 - (int)sh : CT - n;
     int rem = n - s1;
-    m.B = emit ? (ff ? (C2 >> 20) : (C2 >> 19)) : m.B;
-    m.bp += emit ? 1 : 0;
-    m.A = valid ? (An0 << n) : m.A;
-    if (emit && rem >= CTx) {  // rare: a second byte-out in this renormalisation
+    m.B = bo ? (C2 >> sh) : m.B;
+    m.bp += bo ? 1 : 0;
+    m.A = An << n;
+    if (bo && rem >= CTx) {  // rare: a second byte-out in this renormalisation
         m.C = Cx << CTx;
         rem -= CTx;
         ring_byteout(m, ring);
         Cx = m.C;
         CTx = m.CT;
     }
-    Cx <<= rem;
-    CTx -= rem;
-    m.C = valid ? Cx : m.C;
-    m.CT = valid ? CTx : m.CT;
-    return (valid && ren) ? tw : t;
+    m.C = Cx << rem;
+    m.CT = CTx - rem;
+    return ren ? tw : t;
 }
 
 // Copy the lane's completed 16-byte ring groups to the code-block output.
@@ -534,7 +545,7 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
 // -- rather than an event interval that also holds time spent waiting for
 // CUs behind other images' kernels.
 __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
-    __shared__ uint32_t cxs[32 * 64];  // 19 contexts; indices 19..31 absorb bytes read past a pass end
+    __shared__ uint32_t cxs[20 * 64];  // 19 contexts + CX_PAD, lane-interleaved
     __shared__ uint32_t mqt[48];
     __shared__ uint32_t rings[64 * 17];  // 68 bytes per lane: 64-byte ring + dummy slot
     if (threadIdx.x == 0) atomicMin(&a.span[0], (unsigned long long)wall_clock64());
@@ -568,6 +579,7 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
     uint32_t *cx = cxs + lane;
 #pragma unroll
     for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];
+    cx[CX_PAD * 64] = 0u;  // Qe 0, MPS 0: the padding decisions' no-op state
     cx[0] = mqt[4];
     cx[CX_RL * 64] = mqt[3];
     cx[CX_UNI * 64] = mqt[46];
@@ -610,8 +622,9 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
             cur = ptr[0];
         }
         if (s >= nseg) break;
-        // one chunk of up to 16 decisions; the next chunk's load is in flight
-        // behind it, and each context state is read one decision ahead
+        // one chunk of 16 decisions (a pass's last chunk is padded); the
+        // next chunk's load is in flight behind it, and each context state
+        // is read one decision ahead
         const uint4 nxt = ptr[1];
         const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
         const int n = min(16, left);
@@ -624,9 +637,9 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
             uint32_t nxt_cx = 0, nt = 0;
             if (j < 15) {
                 nxt_cx = __builtin_amdgcn_ubfe(w[(j + 1) >> 2], ((j + 1) & 3) * 8 + 1, 5);
-                nt = cx[nxt_cx * 64];  // may be past the pass end (then unused)
+                nt = cx[nxt_cx * 64];
             }
-            const uint32_t tn = mq_step(m, t, mqt, d, j < n, ring);
+            const uint32_t tn = mq_step(m, t, mqt, d, ring);
             cx[cur_cx * 64] = tn;
             t = (nxt_cx == cur_cx) ? tn : nt;
         }
