@@ -319,7 +319,9 @@ def run(args):
                        "timed_span": "TIFF resident in HBM -> JPX bytes in host memory (jp2hip_encode_device)",
                        "parallelism": f"replicas x{world}", "out_bytes": int(avg["out_bytes"]),
                        "bpp": round(8 * avg["out_bytes"] / npx, 4),
-                       "single_image_latency_ms": round(1e3 * min(lat), 3)},
+                       "single_image_latency_ms": round(1e3 * min(lat), 3),
+                       "host_waits_per_encode": int(max(a["host_waits"] for a in alone)),
+                       "rate_iterations": int(max(a["rate_iterations"] for a in alone))},
             # the same steps with the TIFF in pinned host memory and the H2D
             # inside the timed span (PCIe-inclusive rate)
             "value_pcie_inclusive": {"value": round(world * mp * args.steps / dt_h_max, 3), "unit": "MP/s",

@@ -120,7 +120,7 @@ typedef struct jp2hip_stats {
     int64_t t1_bytes;     /* MQ bytes produced by tier-1 (before truncation)  */
     int64_t out_bytes;
     int32_t rate_iterations;
-    int32_t reserved;
+    int32_t host_waits;   /* times the host blocked on the GPU during the encode */
     double t1_cm_ms;      /* tier-1 context-modelling kernel (part of t1_ms)  */
     double t1_mq_ms;      /* tier-1 MQ-coder kernel (part of t1_ms)           */
     int64_t mq_decisions; /* MQ-coded decisions (one decision-stream byte each) */

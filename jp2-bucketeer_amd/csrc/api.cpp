@@ -380,7 +380,7 @@ void layer_end_of(const jp2hip::Plan &P, int64_t tp_hdr_bytes, const int64_t *la
 }
 
 void fill_stats(jp2hip_stats *stats, const jp2hip::StageTimes &st, double t_start, double h2d_ms, int64_t nb,
-                const jp2hip::T2Summary &sum, int64_t out_bytes, int iters) {
+                const jp2hip::T2Summary &sum, int64_t out_bytes, int iters, int waits) {
     if (!stats) return;
     std::memset(stats, 0, sizeof *stats);
     stats->total_ms = now_ms() - t_start;
@@ -399,6 +399,7 @@ void fill_stats(jp2hip_stats *stats, const jp2hip::StageTimes &st, double t_star
     stats->coded_passes = sum.coded_passes;
     stats->out_bytes = out_bytes;
     stats->rate_iterations = iters;
+    stats->host_waits = waits;
     stats->mq_decisions = sum.decisions;
 }
 
@@ -417,6 +418,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     if (recipe) rc = *recipe;
     else default_recipe(&rc, conversion);
     if (!lay || !d_src) return fail("null source or layout");
+    ctx->gpu.take_waits();  // count this encode's host waits (stats)
     Plan plan;
     std::string err;
     jp2hip_layout ulay;
@@ -427,10 +429,13 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     const bool prof = ctx->cfg.profile != 0;
     StageTimes st;
     int64_t skip_target = skip_target_of(rc, plan.w, plan.h);
-    if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, skip_target)) return fail(err);
+    // tier-2 tables first: every host->device copy of the encode is issued
+    // while the stream is idle (a copy queued behind kernels holds up the
+    // copy engine for the other contexts)
     T2Tables tabs;
     t2_tables(plan, 0, plan.ntx * plan.nty, 0, tabs);
     if (!ctx->gpu.t2_load(plan, tabs, err)) return fail(err);
+    if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, skip_target)) return fail(err);
     const int L = rc.layers;
     std::vector<uint8_t> mh;
     main_header(plan, mh, nullptr, nullptr);
@@ -446,31 +451,32 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         iters = 1;
         cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
     } else {
-        const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
-        int64_t budget = target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
-        std::vector<int64_t> budgets((size_t)L, 0);
-        for (int it = 0; it < 8; it++) {
-            if (budget < 0) budget = 0;
-            for (int l = 0; l < L; l++) budgets[l] = budget >> (L - 1 - l);
-            if (!ctx->gpu.select(plan, budgets, err) || !ctx->gpu.t2_size(plan, true, prof, st, sum, err))
-                return fail(err);
+        // the rate loop runs on the device (GpuEncoder::rate_loop): three
+        // iterations are enqueued per host wait, the usual encode needs two
+        RateState init;
+        std::memset(&init, 0, sizeof init);
+        init.target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
+        init.budget = init.target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
+        init.fixed = (int64_t)mh.size() + 2;
+        init.skip_target = skip_target;
+        RateState rs;
+        bool restart = true;
+        for (;;) {
+            if (!ctx->gpu.rate_loop(plan, init, restart, 3, prof, st, rs, sum, err)) return fail(err);
+            restart = false;
             if (sum.err) return fail("tier-1 output capacity exceeded");
-            if (it == 0 && skip_target > 0 && sum.skipped && sum.t1_bytes < skip_target) {
+            if (rs.safety) {
                 // slope prediction's safety net (oracle predict_and_code):
                 // planes were skipped, yet every coded byte fits -> code all
-                skip_target = 0;
+                init.skip_target = 0;
                 if (!ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, 0)) return fail(err);
-                it = -1;
-                budget = target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
-                iters = 0;
+                restart = true;
                 continue;
             }
-            iters++;
-            cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
-            if (cs_bytes <= target) break;
-            // exponential back-off + 1/16 of the overshoot + 64 B, as the oracle
-            budget -= ((cs_bytes - target) << it) + ((cs_bytes - target) >> 4) + 64;
+            if (rs.halt) break;
         }
+        iters = rs.iters;
+        cs_bytes = rs.cs_bytes;
     }
     // Kdu-Layer-Info: the final selection's slope keys (lossless: the last
     // layer takes every pass) and the code-stream bytes through each layer
@@ -494,7 +500,8 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     buf[n - 1] = 0xD9;
     *out = buf;
     *out_len = n;
-    fill_stats(stats, st, t_start, h2d_ms, (int64_t)plan.blocks.size(), sum, (int64_t)n, iters);
+    fill_stats(stats, st, t_start, h2d_ms, (int64_t)plan.blocks.size(), sum, (int64_t)n, iters,
+               ctx->gpu.take_waits());
     return 0;
 }
 
@@ -519,6 +526,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     if (recipe) rc = *recipe;
     else default_recipe(&rc, conversion);
     if (!lay || !d_src) return fail("null source or layout");
+    ctx->gpu.take_waits();
     Plan full;
     std::string err;
     // every rank sees the same layout, so all of them stop here together
@@ -550,18 +558,18 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
         std::copy(v.begin(), v.end() - 1, h.begin());
         return true;
     };
+    T2Tables tabs;  // loaded before the front (host->device copies on an idle stream)
+    const int tile0 = sub.tile0, tile1 = sub.tile0 + full.ntx * (tr1 - tr0);
+    if (ok && have) {
+        t2_tables(full, tile0, tile1, sub.block0, tabs);
+        ok = ctx->gpu.t2_load(sub, tabs, err);
+    }
     ok = ok && (!have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, skip_target, &reduce));
     if (skip_target > 0 && !hist_done) {  // no blocks here, or failed before the exchange
         std::vector<int64_t> v((size_t)kSlopeBins + 1, 0);
         v.back() = ok ? 0 : 1;
         if (!allreduce(v.data(), (int)v.size())) return fail("split: all-reduce failed");
         if (ok && v.back()) { ok = false; err = "split: another rank failed"; }
-    }
-    T2Tables tabs;
-    const int tile0 = sub.tile0, tile1 = sub.tile0 + full.ntx * (tr1 - tr0);
-    if (ok && have) {
-        t2_tables(full, tile0, tile1, sub.block0, tabs);
-        ok = ctx->gpu.t2_load(sub, tabs, err);
     }
     const int L = rc.layers;
     std::vector<int64_t> budgets((size_t)L, 0);
@@ -609,7 +617,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
             skip_target = 0;
             iters = 0;
         }
-        ok = ok && (!have || ctx->gpu.segments(keys, cum, err));
+        ok = ok && (!have || ctx->gpu.segments(sub, keys, cum, err));
         {
             int64_t flag = ok ? 0 : 1;
             if (!allreduce(&flag, 1)) return fail("split: all-reduce failed");
@@ -682,7 +690,8 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     *out_len = part;
     if (file_offset) *file_offset = off;
     if (file_len) *file_len = flen;
-    fill_stats(stats, st, t_start, 0.0, (int64_t)sub.blocks.size(), sum, (int64_t)flen, iters);
+    fill_stats(stats, st, t_start, 0.0, (int64_t)sub.blocks.size(), sum, (int64_t)flen, iters,
+               ctx->gpu.take_waits());
     return 0;
 }
 

@@ -24,8 +24,9 @@ struct T2Args;  // t2_device.hip
 
 // tier-1 kernels (t1.hip)
 struct T1CmArgs {
-    const int2 *items;  // (block, plane)
-    int nitems;
+    const int2 *items;   // (block, plane)
+    const int *nitems;   // item count (device); the grid covers max_items
+    int max_items;
     const BlockDesc *blocks;
     const uint64_t *bp;
     const int32_t *sm;
@@ -68,6 +69,10 @@ struct DwtLaunch {
 bool launch_dwt(const DwtLaunch &p, hipStream_t st);
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st);
+void launch_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
+                     const BlockDesc *blocks, int32_t *flags, uint64_t *slot_bytes, hipStream_t st);
+void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, const int32_t *flags,
+                     const int32_t *pos, int2 *items, int *nitems, hipStream_t st);
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
                     int32_t *vals, hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
@@ -112,6 +117,12 @@ class GpuEncoder {
     // part (tile-parts, in stream order) written in HBM and copied to host_dst
     bool t2_load(const Plan &plan, const T2Tables &T, std::string &err);
     bool t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum, std::string &err);
+    // rate-driven encode: the whole rate loop on the device (RateState),
+    // `batch` iterations enqueued per host wait; returns the final state and
+    // the summary of the selection it stopped at.  restart = begin a new loop
+    // (else continue the one on the device).
+    bool rate_loop(const Plan &plan, const RateState &init, bool restart, int batch, bool profile, StageTimes &st,
+                   RateState &rs, T2Summary &sum, std::string &err);
     // host_dst must be pinned (hipHostMalloc) memory
     bool t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
                  StageTimes &st, std::string &err);
@@ -121,38 +132,55 @@ class GpuEncoder {
     // after the encode's last host wait)
     bool collect_profile(StageTimes &st, std::string &err);
     // this encode's hull segments: slope keys (descending) and inclusive byte sums
-    bool segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err);
+    bool segments(const Plan &plan, std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err);
     hipStream_t get_stream() const { return stream; }
+    // host waits since the last call (stats: host_waits per encode)
+    int take_waits() {
+        const int w = waits;
+        waits = 0;
+        return w;
+    }
 
   private:
     // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
-    bool apply_thresholds(const Plan &plan, std::string &err);
+    bool apply_thresholds(const Plan &plan, const int *halt, std::string &err);
     T2Args t2_args(const Plan &plan) const;
+    void t2_size_launch(const Plan &plan, bool with_kc, const int *halt);
     bool host_wait(std::string &err);
+    // host -> device copy through this context's pinned staging memory: a
+    // pageable source goes through the runtime's shared staging buffer and
+    // blocks until the stream reaches the copy, serialising the contexts
+    bool h2d(void *dst, const void *src, size_t bytes, std::string &err);
+    struct PinnedChunk {
+        uint8_t *p;
+        size_t cap;
+    };
+    std::vector<PinnedChunk> stg;
+    size_t stg_used = 0;
+    hipEvent_t stg_ev = nullptr;  // after the last staged copy
     static constexpr int kNumEvents = 12;
     int device = 0;
+    int waits = 0;
     hipEvent_t sync_ev = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
         est, hist, kcut, pmin, mqspan, stage, soff, lzwtab, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
-        dbgbuf;
+        dbgbuf, t1ord, t1flags, t1pos, slotbytes, nitems_d;
     // device tier-2 (t2_device.hip)
-    DevBuf hdist;
+    DevBuf hdist, rstate;
+    RateState *h_rs = nullptr;  // pinned
     DevBuf t2prec, t2tp, t2tt, t2lblock, t2incl, t2pklen, t2pkoff, t2tplen, t2tphdr, t2tpoff, t2blkdst, t2out, t2sum;
     int t2_nprec = 0, t2_ntp = 0;
     T2Summary *h_sum = nullptr;
-    int64_t *h_tot = nullptr;  // pinned: t1_totals / profile read-back
+    int64_t *h_tot = nullptr;  // pinned [8]: t1 total, -, k_t1_mq span[2], unpack error, segment tail[2]
     bool profiled = false;
-    int nseg = 0;
+    int nseg = 0;  // segment arrays' length: the bound sum(3 Mb - 2), zero-key padded
     uint8_t *h_packed = nullptr;
     size_t h_packed_cap = 0;
-    std::vector<uint8_t> h_P, h_pmin;
     std::vector<int64_t> h_hist;
-    std::vector<int2> h_items;
-    std::vector<uint64_t> h_slot;
 };
 
 }  // namespace jp2hip

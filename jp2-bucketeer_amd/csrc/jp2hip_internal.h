@@ -142,6 +142,17 @@ struct T2Summary {
     int64_t decisions;                // MQ-coded decisions
     int32_t skipped, err;             // slope prediction skipped planes; tier-1 overflow
 };
+// Rate control of a rate-driven encode, run on the device (kernels.hip
+// k_rate_step; the oracle's loop in oracle_encode): iteration `it` selects
+// with `budget`, sizes the code-stream, stops when it fits `target` (or after
+// 8 iterations), else lowers the budget.  `halt` stops the remaining
+// iterations' kernels; `safety` = slope prediction's safety net fired
+// (planes were skipped yet every coded byte fits: the host re-runs the front
+// with every plane coded).
+struct RateState {
+    int64_t budget, target, fixed, skip_target, cs_bytes;
+    int32_t it, halt, safety, iters;
+};
 // Main header (SOC .. COM) for the Kdu-Layer-Info values (nullptr: zeros;
 // the length does not depend on them).
 void main_header(const Plan &P, std::vector<uint8_t> &v, const uint64_t *K, const int64_t *layer_end);

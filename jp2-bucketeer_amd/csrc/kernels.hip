@@ -889,9 +889,9 @@ __global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nh
 // the Kdu-Layer-Info slope: one above the first key not taken, 0 if every
 // segment is taken (= the tile-split bisection's K'; oracle select_threshold)
 __global__ void k_thresh(int nseg, int layers, const uint64_t *keys, const int64_t *cum,
-                         const int64_t *budget, uint64_t *K, uint64_t *Kc) {
+                         const int64_t *budget, uint64_t *K, uint64_t *Kc, const int *halt) {
     int l = threadIdx.x;
-    if (l >= layers) return;
+    if (l >= layers || (halt && *halt)) return;
     int64_t bgt = budget[l];
     int lo = 0, hi = nseg;  // first index with cum > bgt
     while (lo < hi) {
@@ -911,7 +911,7 @@ __global__ void k_thresh(int nseg, int layers, const uint64_t *keys, const int64
         j = l2 - 1;
     }
     K[l] = (j >= 0) ? keys[j] : 0xFFFFFFFFFFFFFFFFull;
-    Kc[l] = (j + 1 < nseg) ? keys[j + 1] + 1 : 0ull;
+    Kc[l] = (j + 1 < nseg && keys[j + 1] != 0) ? keys[j + 1] + 1 : 0ull;  // key 0 = padding
 }
 
 // last hull index whose key >= K (0 = nothing); hull keys strictly decrease
@@ -926,6 +926,7 @@ __device__ __forceinline__ int hull_pick(const uint64_t *hk, int nh, uint64_t K)
 }
 
 struct ApplyArgs {
+    const int *halt;  // device rate loop: nothing to do once it has stopped
     int nblocks, layers, lossless;
     const uint8_t *nhull, *hpass, *npasses;
     const uint64_t *hkey, *K;
@@ -936,7 +937,7 @@ struct ApplyArgs {
 
 __global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
     int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.nblocks) return;
+    if (b >= a.nblocks || (a.halt && *a.halt)) return;
     const int L = a.layers;
     const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
     const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
@@ -977,16 +978,20 @@ GpuEncoder::~GpuEncoder() {
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwtab, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
-                     &t2blkdst, &t2out, &t2sum, &hdist};
+                     &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
+                     &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
+    if (stg_ev) (void)hipEventDestroy(stg_ev);
+    for (const PinnedChunk &c : stg) (void)hipHostFree(c.p);
     if (stream) (void)hipStreamDestroy(stream);
     for (int i = 0; i < kNumEvents; i++)
         if (ev[i]) (void)hipEventDestroy(ev[i]);
     if (h_packed) (void)hipHostFree(h_packed);
     if (h_sum) (void)hipHostFree(h_sum);
     if (h_tot) (void)hipHostFree(h_tot);
+    if (h_rs) (void)hipHostFree(h_rs);
 }
 
 bool GpuEncoder::init(int dev, std::string &err) {
@@ -995,6 +1000,39 @@ bool GpuEncoder::init(int dev, std::string &err) {
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (int i = 0; i < kNumEvents; i++) HIPCHECK(hipEventCreate(&ev[i]));
     HIPCHECK(hipEventCreateWithFlags(&sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&stg_ev, hipEventDisableTiming));
+    HIPCHECK(hipHostMalloc((void **)&h_tot, 8 * sizeof(int64_t), hipHostMallocDefault));
+    return true;
+}
+
+bool GpuEncoder::h2d(void *dst, const void *src, size_t bytes, std::string &err) {
+    if (!bytes) return true;
+    if (hipEventQuery(stg_ev) == hipSuccess) {  // every staged copy has landed: reuse from the start
+        if (stg.size() > 1) {
+            size_t tot = 0;
+            for (const PinnedChunk &c : stg) {
+                tot += c.cap;
+                HIPCHECK(hipHostFree(c.p));
+            }
+            stg.clear();
+            PinnedChunk c{nullptr, tot};
+            HIPCHECK(hipHostMalloc((void **)&c.p, tot, hipHostMallocDefault));
+            stg.push_back(c);
+        }
+        stg_used = 0;
+    }
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (stg.empty() || stg_used + need > stg.back().cap) {  // a new chunk; the older ones stay until the copies land
+        PinnedChunk c{nullptr, std::max<size_t>(need, stg.empty() ? (size_t)1 << 20 : 2 * stg.back().cap)};
+        HIPCHECK(hipHostMalloc((void **)&c.p, c.cap, hipHostMallocDefault));
+        stg.push_back(c);
+        stg_used = 0;
+    }
+    uint8_t *h = stg.back().p + stg_used;
+    stg_used += need;
+    std::memcpy(h, src, bytes);
+    HIPCHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipEventRecord(stg_ev, stream));
     return true;
 }
 
@@ -1002,6 +1040,7 @@ bool GpuEncoder::init(int dev, std::string &err) {
 // spinning: with many images in flight the spinning callers would take the
 // cores the tier-2 threads need.
 bool GpuEncoder::host_wait(std::string &err) {
+    waits++;
     HIPCHECK(hipEventRecord(sync_ev, stream));
     HIPCHECK(hipEventSynchronize(sync_ev));
     return true;
@@ -1010,8 +1049,9 @@ bool GpuEncoder::host_wait(std::string &err) {
 bool GpuEncoder::upload_source(const void *host, size_t len, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     if (!ensure<uint8_t>(src, len, err)) return false;
+    // stream-ordered: the encode that follows (same stream) waits for it, and
+    // the caller's buffer outlives the synchronous encode call
     HIPCHECK(hipMemcpyAsync(src.ptr, host, len, hipMemcpyHostToDevice, stream));
-    if (!host_wait(err)) return false;
     return true;
 }
 
@@ -1045,9 +1085,9 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
     const bool decode = lay.compression > 1;
     if (!ensure<uint64_t>(soff, (size_t)ns * 2, err) || !ensure<int>(this->err, 4, err)) return false;
     if (decode && !ensure<uint8_t>(stage, stride * ns, err)) return false;
-    HIPCHECK(hipMemcpyAsync(soff.ptr, lay.strip_offsets, sizeof(uint64_t) * ns, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync((uint64_t *)soff.ptr + ns, lay.strip_bytes, sizeof(uint64_t) * ns, hipMemcpyHostToDevice,
-                            stream));
+    if (!h2d(soff.ptr, lay.strip_offsets, sizeof(uint64_t) * ns, err) ||
+        !h2d((uint64_t *)soff.ptr + ns, lay.strip_bytes, sizeof(uint64_t) * ns, err))
+        return false;
     HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
     if (decode) {
         UnpackArgs ua;
@@ -1099,9 +1139,9 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
     } else {
         for (int i = 0; i < ns; i++) out_offs[i] = (uint64_t)i * stride;
     }
-    int herr = 0;
-    HIPCHECK(hipMemcpyAsync(&herr, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(h_tot + 4, this->err.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (!host_wait(err)) return false;
+    const int herr = *(const int *)(h_tot + 4);
     if (herr & 4) {
         err = "tiff: old-style (pre-TIFF 6.0, LSB-first) LZW strips are not supported";
         return false;
@@ -1154,11 +1194,13 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<int32_t>(tch, plan.ntc, err)) return false;
     if (!ensure<uint64_t>(strips, lay.nstrips, err)) return false;
 
-    HIPCHECK(hipMemcpyAsync(blocks.ptr, plan.blocks.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(weight.ptr, plan.weight.data(), sizeof(double) * nb, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, hipMemcpyHostToDevice, stream));
+    if (!h2d(blocks.ptr, plan.blocks.data(), sizeof(BlockDesc) * nb, err) ||
+        !h2d(weight.ptr, plan.weight.data(), sizeof(double) * nb, err) ||
+        !h2d(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, err) ||
+        !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err) ||
+        !h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err) ||
+        !ensure<int32_t>(t1ord, nb, err) || !h2d(t1ord.ptr, plan.t1_order.data(), sizeof(int32_t) * nb, err))
+        return false;
     HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
 
     HIPCHECK(hipEventRecord(ev[0], stream));
@@ -1243,6 +1285,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         HIPCHECK(hipGetLastError());
         if (reduce) {
             h_hist.resize(kSlopeBins);
+            if (!host_wait(err)) return false;  // (a pageable copy waits for the stream holding a shared lock)
             HIPCHECK(hipMemcpyAsync(h_hist.data(), hist.ptr, sizeof(int64_t) * kSlopeBins, hipMemcpyDeviceToHost,
                                     stream));
             if (!host_wait(err)) return false;
@@ -1250,8 +1293,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
                 err = "split: slope-prediction exchange failed";
                 return false;
             }
-            HIPCHECK(hipMemcpyAsync(hist.ptr, h_hist.data(), sizeof(int64_t) * kSlopeBins, hipMemcpyHostToDevice,
-                                    stream));
+            if (!h2d(hist.ptr, h_hist.data(), sizeof(int64_t) * kSlopeBins, err)) return false;
         }
         hipLaunchKernelGGL(k_plane_cut, dim3(1), dim3(64), 0, stream, (const unsigned long long *)hist.ptr,
                            skip_target * 128, (int *)kcut.ptr);
@@ -1262,38 +1304,50 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     }
     HIPCHECK(hipEventRecord(ev[3], stream));
     // S5: tier-1.  Items (block, plane) ordered by plane depth from the top,
-    // then by block shape, so a wavefront's lanes do similar work.
-    h_P.resize(nb);
-    h_pmin.resize(nb);
-    HIPCHECK(hipMemcpyAsync(h_P.data(), P.ptr, nb, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(h_pmin.data(), pmin.ptr, nb, hipMemcpyDeviceToHost, stream));
-    if (!host_wait(err)) return false;
-    h_slot.resize(nb);
-    uint64_t stream_bytes = 0;
-    int maxP = 0;
+    // then by block shape, so a wavefront's lanes do similar work.  The list
+    // and the blocks' stream slots are built on the device (t1.hip
+    // k_t1_flags / k_t1_items) from the coded plane counts; buffers and the
+    // grid are sized by the plan's bound (every plane of every block coded).
+    int kmax = 0;
+    uint64_t stream_bound = 0;
     for (int i = 0; i < nb; i++) {
-        const int pc = h_P[i] - h_pmin[i];  // coded planes, from the top
-        h_slot[i] = stream_bytes;
-        stream_bytes += (uint64_t)pc * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
-        maxP = std::max(maxP, pc);
+        const BlockDesc &bd = plan.blocks[i];
+        kmax = std::max(kmax, (int)bd.Mb);
+        stream_bound += (uint64_t)bd.Mb * t1_plane_stream_cap(bd.w, bd.h);
     }
-    h_items.clear();
-    for (int k = 0; k < maxP; k++)
-        for (int i = 0; i < nb; i++) {
-            int bb = plan.t1_order[i];
-            if (h_P[bb] - h_pmin[bb] > k) h_items.push_back(make_int2(bb, h_P[bb] - 1 - k));
-        }
-    const int nitems = (int)h_items.size();
-    if (!ensure<int2>(items, std::max(nitems, 1), err) || !ensure<uint64_t>(slotoff, nb, err) ||
-        !ensure<uint8_t>(stream_buf, stream_bytes, err) || !ensure<uint4>(counts, (size_t)nb * 32, err) ||
-        !ensure<int64_t>(dspp, (size_t)nb * 32, err))
+    const size_t nflags = (size_t)nb * kmax;
+    if (!ensure<int2>(items, std::max<size_t>(nflags, 1), err) || !ensure<uint64_t>(slotoff, nb, err) ||
+        !ensure<uint8_t>(stream_buf, stream_bound, err) || !ensure<uint4>(counts, (size_t)nb * 32, err) ||
+        !ensure<int64_t>(dspp, (size_t)nb * 32, err) || !ensure<int32_t>(t1ord, nb, err) ||
+        !ensure<int32_t>(t1flags, nflags, err) || !ensure<int32_t>(t1pos, nflags, err) ||
+        !ensure<uint64_t>(slotbytes, nb, err) || !ensure<int>(nitems_d, 1, err))
         return false;
-    if (nitems) HIPCHECK(hipMemcpyAsync(items.ptr, h_items.data(), sizeof(int2) * nitems, hipMemcpyHostToDevice, stream));
-    HIPCHECK(hipMemcpyAsync(slotoff.ptr, h_slot.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemsetAsync(nitems_d.ptr, 0, sizeof(int), stream));
+    launch_t1_flags(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr,
+                    (const BlockDesc *)blocks.ptr, (int32_t *)t1flags.ptr, (uint64_t *)slotbytes.ptr, stream);
+    HIPCHECK(hipGetLastError());
+    if (nflags) {
+        size_t tb = 0;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int32_t *)t1flags.ptr, (int32_t *)t1pos.ptr,
+                                                  (int)nflags, stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (int32_t *)t1flags.ptr, (int32_t *)t1pos.ptr,
+                                                  (int)nflags, stream));
+        tb = 0;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint64_t *)slotbytes.ptr, (uint64_t *)slotoff.ptr, nb,
+                                                  stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (uint64_t *)slotbytes.ptr, (uint64_t *)slotoff.ptr,
+                                                  nb, stream));
+    }
+    launch_t1_items(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const int32_t *)t1flags.ptr,
+                    (const int32_t *)t1pos.ptr, (int2 *)items.ptr, (int *)nitems_d.ptr, stream);
+    HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[10], stream));
     T1CmArgs ca;
     ca.items = (const int2 *)items.ptr;
-    ca.nitems = nitems;
+    ca.nitems = (const int *)nitems_d.ptr;
+    ca.max_items = (int)nflags;
     ca.blocks = (const BlockDesc *)blocks.ptr;
     ca.bp = (const uint64_t *)bp.ptr;
     ca.sm = (const int32_t *)sm.ptr;
@@ -1377,17 +1431,20 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
         HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr, nb, stream));
     }
-    int32_t tail[2] = {0, 0};
-    if (nb) {
-        HIPCHECK(hipMemcpyAsync(&tail[0], (int32_t *)segoff.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
-        HIPCHECK(hipMemcpyAsync(&tail[1], (int32_t *)segcnt.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
-    }
-    if (!host_wait(err)) return false;
-    nseg = tail[0] + tail[1];
+    // the segment arrays have the bound's length (no host wait for the real
+    // count): unused entries keep key 0 and size 0, sort after every real
+    // key (slopes are > 0) and leave the prefix sums flat
+    int64_t nseg_bound = 0;
+    for (int i = 0; i < nb; i++) nseg_bound += std::max(0, 3 * (int)plan.blocks[i].Mb - 2);
+    nseg = (int)nseg_bound;
     if (!ensure<uint64_t>(segkey, std::max(nseg, 1), err) || !ensure<uint64_t>(segkey2, std::max(nseg, 1), err) ||
         !ensure<int64_t>(segval, std::max(nseg, 1), err) || !ensure<int64_t>(segval2, std::max(nseg, 1), err) ||
         !ensure<int64_t>(segcum, std::max(nseg, 1), err) || !ensure<uint64_t>(thr, 2 * kMaxLayers, err))
         return false;
+    if (nseg > 0) {
+        HIPCHECK(hipMemsetAsync(segkey.ptr, 0, sizeof(uint64_t) * nseg, stream));
+        HIPCHECK(hipMemsetAsync(segval.ptr, 0, sizeof(int64_t) * nseg, stream));
+    }
     if (nb) hipLaunchKernelGGL(k_seg_emit, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
                                (const uint8_t *)nhull.ptr, (const uint8_t *)hpass.ptr,
                                (const uint64_t *)hkey.ptr, (const int32_t *)rates.ptr,
@@ -1444,13 +1501,13 @@ bool GpuEncoder::collect_profile(StageTimes &st, std::string &err) {
 bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     const int L = plan.rc.layers;
-    HIPCHECK(hipMemcpyAsync(budget.ptr, budgets.data(), sizeof(int64_t) * L, hipMemcpyHostToDevice, stream));
+    if (!h2d(budget.ptr, budgets.data(), sizeof(int64_t) * L, err)) return false;
     HIPCHECK(hipEventRecord(ev[6], stream));
     hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
                        (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
-                       (uint64_t *)thr.ptr + kMaxLayers);
+                       (uint64_t *)thr.ptr + kMaxLayers, (const int *)nullptr);
     HIPCHECK(hipGetLastError());
-    return apply_thresholds(plan, err);
+    return apply_thresholds(plan, nullptr, err);
 }
 
 // lossless "-rate -": layer l's budget is total >> (L-1-l), total = every
@@ -1477,23 +1534,24 @@ bool GpuEncoder::select_lossless(const Plan &plan, std::string &err) {
                        (int64_t *)budget.ptr);
     hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
                        (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
-                       (uint64_t *)thr.ptr + kMaxLayers);
+                       (uint64_t *)thr.ptr + kMaxLayers, (const int *)nullptr);
     HIPCHECK(hipGetLastError());
-    return apply_thresholds(plan, err);
+    return apply_thresholds(plan, nullptr, err);
 }
 
 bool GpuEncoder::select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    HIPCHECK(hipMemcpyAsync(thr.ptr, K.data(), sizeof(uint64_t) * plan.rc.layers, hipMemcpyHostToDevice, stream));
+    if (!h2d(thr.ptr, K.data(), sizeof(uint64_t) * plan.rc.layers, err)) return false;
     HIPCHECK(hipEventRecord(ev[6], stream));
-    return apply_thresholds(plan, err);
+    return apply_thresholds(plan, nullptr, err);
 }
 
 // per-block layer tables for the thresholds in `thr` (ev[6] already recorded)
-bool GpuEncoder::apply_thresholds(const Plan &plan, std::string &err) {
+bool GpuEncoder::apply_thresholds(const Plan &plan, const int *halt, std::string &err) {
     const int nb = (int)plan.blocks.size();
     const int L = plan.rc.layers;
     ApplyArgs aa;
+    aa.halt = halt;
     aa.nblocks = nb;
     aa.layers = L;
     aa.lossless = plan.rc.rate_bpp <= 0.0;
@@ -1508,6 +1566,84 @@ bool GpuEncoder::apply_thresholds(const Plan &plan, std::string &err) {
     if (nb) hipLaunchKernelGGL(k_apply, dim3((nb + 255) / 256), dim3(256), 0, stream, aa);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[7], stream));
+    return true;
+}
+
+// Device rate loop (RateState, jp2hip_internal.h): same arithmetic as the
+// host loop it replaces and the oracle's (oracle_encode, rate_bpp > 0).
+__device__ __forceinline__ void rate_budgets(const RateState &r, int L, int64_t *budget) {
+    const int64_t b = r.budget < 0 ? 0 : r.budget;
+    for (int l = 0; l < L; l++) budget[l] = b >> (L - 1 - l);
+}
+__global__ void k_rate_init(RateState *rs, RateState init, int L, int64_t *budget) {
+    RateState r = init;
+    r.it = 0;
+    r.halt = 0;
+    r.safety = 0;
+    r.iters = 0;
+    r.cs_bytes = 0;
+    if (r.budget < 0) r.budget = 0;
+    *rs = r;
+    rate_budgets(r, L, budget);
+}
+__global__ void k_rate_step(RateState *rs, const T2Summary *sum, int L, int64_t *budget) {
+    RateState r = *rs;
+    if (r.halt) return;
+    if (sum->err) {  // tier-1 overflow: the host reports it
+        rs->halt = 1;
+        return;
+    }
+    if (r.it == 0 && r.skip_target > 0 && sum->skipped && sum->t1_bytes < r.skip_target) {
+        rs->safety = 1;
+        rs->halt = 1;
+        return;
+    }
+    r.iters++;
+    r.cs_bytes = r.fixed + sum->part_bytes;
+    if (r.cs_bytes <= r.target || r.it == 7) {
+        r.halt = 1;
+    } else {
+        // exponential back-off + 1/16 of the overshoot + 64 B, as the oracle
+        const int64_t over = r.cs_bytes - r.target;
+        r.budget -= (over << r.it) + (over >> 4) + 64;
+        if (r.budget < 0) r.budget = 0;
+        r.it++;
+        rate_budgets(r, L, budget);
+    }
+    *rs = r;
+}
+
+bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart, int batch, bool profile,
+                           StageTimes &st, RateState &rs, T2Summary &sum, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    const int L = plan.rc.layers;
+    if (!ensure<RateState>(rstate, 1, err)) return false;
+    if (!h_rs) HIPCHECK(hipHostMalloc((void **)&h_rs, sizeof(RateState), hipHostMallocDefault));
+    RateState *d = (RateState *)rstate.ptr;
+    const int *halt = &d->halt;
+    HIPCHECK(hipEventRecord(ev[6], stream));
+    if (restart) hipLaunchKernelGGL(k_rate_init, dim3(1), dim3(1), 0, stream, d, init, L, (int64_t *)budget.ptr);
+    for (int i = 0; i < batch; i++) {
+        hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
+                           (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
+                           (uint64_t *)thr.ptr + kMaxLayers, halt);
+        if (!apply_thresholds(plan, halt, err)) return false;
+        t2_size_launch(plan, true, halt);
+        hipLaunchKernelGGL(k_rate_step, dim3(1), dim3(1), 0, stream, d, (const T2Summary *)t2sum.ptr, L,
+                           (int64_t *)budget.ptr);
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(h_sum, t2sum.ptr, sizeof(T2Summary), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(h_rs, d, sizeof(RateState), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipEventRecord(ev[9], stream));
+    if (!host_wait(err)) return false;
+    sum = *h_sum;
+    rs = *h_rs;
+    if (profile) {
+        float t;
+        HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[9]));
+        st.t2 += t;
+    }
     return true;
 }
 
@@ -1528,7 +1664,6 @@ __global__ void __launch_bounds__(256) k_sum_lengths(int nblocks, const int32_t 
 bool GpuEncoder::t1_totals(const Plan &plan, int64_t &bytes, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     if (!ensure<int64_t>(hist, kSlopeBins, err)) return false;
-    if (!h_tot) HIPCHECK(hipHostMalloc((void **)&h_tot, 4 * sizeof(int64_t), hipHostMallocDefault));
     hipLaunchKernelGGL(k_sum_lengths, dim3(1), dim3(256), 0, stream, (int)plan.blocks.size(),
                        (const int32_t *)lengths.ptr, (int64_t *)hist.ptr);
     HIPCHECK(hipGetLastError());
@@ -1538,13 +1673,24 @@ bool GpuEncoder::t1_totals(const Plan &plan, int64_t &bytes, std::string &err) {
     return true;
 }
 
-bool GpuEncoder::segments(std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err) {
+bool GpuEncoder::segments(const Plan &plan, std::vector<uint64_t> &keys, std::vector<int64_t> &cum,
+                          std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    keys.resize((size_t)nseg);
-    cum.resize((size_t)nseg);
-    if (nseg > 0) {
-        HIPCHECK(hipMemcpyAsync(keys.data(), segkey2.ptr, sizeof(uint64_t) * nseg, hipMemcpyDeviceToHost, stream));
-        HIPCHECK(hipMemcpyAsync(cum.data(), segcum.ptr, sizeof(int64_t) * nseg, hipMemcpyDeviceToHost, stream));
+    // the real segment count (the arrays are padded to the bound)
+    const int nb = (int)plan.blocks.size();
+    int32_t *tail = (int32_t *)(h_tot + 5);  // pinned
+    tail[0] = tail[1] = 0;
+    if (nb) {
+        HIPCHECK(hipMemcpyAsync(&tail[0], (int32_t *)segoff.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(&tail[1], (int32_t *)segcnt.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
+    }
+    if (!host_wait(err)) return false;
+    const int n = tail[0] + tail[1];
+    keys.resize((size_t)n);
+    cum.resize((size_t)n);
+    if (n > 0) {
+        HIPCHECK(hipMemcpyAsync(keys.data(), segkey2.ptr, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(cum.data(), segcum.ptr, sizeof(int64_t) * n, hipMemcpyDeviceToHost, stream));
     }
     if (!host_wait(err)) return false;
     return true;

@@ -179,13 +179,16 @@ constexpr int kCmWaves = 4;  // items per workgroup
 __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
     __shared__ uint8_t lzc[4 * 256];
     __shared__ uint8_t lsc[256];
+    // the grid covers the largest possible list; workgroups past the real
+    // item count (known on the device only) leave at once
+    if ((int)blockIdx.x * kCmWaves >= *a.nitems) return;
     for (int i = threadIdx.x; i < 1024; i += 64 * kCmWaves) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
     for (int i = threadIdx.x; i < 256; i += 64 * kCmWaves) lsc[i] = (uint8_t)sc_lut(i);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int gi = blockIdx.x * kCmWaves + wv;
-    if (gi >= a.nitems) return;
+    if (gi >= *a.nitems) return;
     const int2 item = a.items[gi];
     const int b = item.x, p = item.y;
     const BlockDesc d = a.blocks[b];
@@ -685,9 +688,47 @@ __global__ void __launch_bounds__(256) k_t1_keys(int nblocks, const uint8_t *P, 
     vals[b] = b;
 }
 
+// Tier-1 work list, built on the device from the coded plane counts
+// (P - pmin): flags[k * nb + j] = block order[j] codes a plane at depth k
+// (counted from its top plane); an exclusive scan of the flags places each
+// (block, plane) item -- depth-major, then in plan order -- and slot_bytes
+// sizes each block's decision-stream slot.
+__global__ void __launch_bounds__(256) k_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P,
+                                                  const uint8_t *pmin, const BlockDesc *blocks, int32_t *flags,
+                                                  uint64_t *slot_bytes) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nb * kmax) return;
+    const int k = i / nb, b = order[i - k * nb];
+    const int pc = P[b] - pmin[b];
+    flags[i] = k < pc ? 1 : 0;
+    if (k == 0) slot_bytes[b] = (uint64_t)pc * plane_stream_cap(blocks[b].w, blocks[b].h);
+}
+__global__ void __launch_bounds__(256) k_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P,
+                                                  const int32_t *flags, const int32_t *pos, int2 *items,
+                                                  int *nitems) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = nb * kmax;
+    if (i >= n) return;
+    const int k = i / nb, b = order[i - k * nb];
+    if (flags[i]) items[pos[i]] = make_int2(b, P[b] - 1 - k);
+    if (i == n - 1) *nitems = pos[i] + flags[i];
+}
+
+void launch_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
+                     const BlockDesc *blocks, int32_t *flags, uint64_t *slot_bytes, hipStream_t st) {
+    const long n = (long)nb * kmax;
+    if (n) hipLaunchKernelGGL(k_t1_flags, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nb, kmax, order, P,
+                              pmin, blocks, flags, slot_bytes);
+}
+void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, const int32_t *flags,
+                     const int32_t *pos, int2 *items, int *nitems, hipStream_t st) {
+    const long n = (long)nb * kmax;
+    if (n) hipLaunchKernelGGL(k_t1_items, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nb, kmax, order, P,
+                              flags, pos, items, nitems);
+}
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
-    if (a.nitems)
-        hipLaunchKernelGGL(k_t1_cm, dim3((a.nitems + kCmWaves - 1) / kCmWaves), dim3(64 * kCmWaves), 0, st, a);
+    if (a.max_items)
+        hipLaunchKernelGGL(k_t1_cm, dim3((a.max_items + kCmWaves - 1) / kCmWaves), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
                     int32_t *vals, hipStream_t st) {

@@ -58,6 +58,7 @@ struct T2Args {
     uint64_t *blkdst;       // [block][L] offset of the block's layer-l bytes in `out`
     uint8_t *out;           // the part: tile-parts from byte `base`
     uint64_t base;
+    const int *halt;        // sizing kernels do nothing while *halt (device rate loop); may be null
 };
 
 // Packet-header bit writer (B.10.1): MSB first, a byte after 0xFF carries 7
@@ -171,7 +172,7 @@ template <bool EMIT>
 __global__ void __launch_bounds__(64) k_t2_code(T2Args a) {
     __shared__ uint32_t lds_nodes[64 * kLdsNodes];
     const int pi = blockIdx.x * 64 + threadIdx.x;
-    if (pi >= a.nprec) return;
+    if (pi >= a.nprec || (!EMIT && a.halt && *a.halt)) return;
     const PrecDesc d = a.prec[pi];
     const int L = a.L;
     int nodes = 0;
@@ -301,7 +302,7 @@ __device__ __forceinline__ int varint_len(uint32_t v) {
 // Psot and SOT + PLT + SOD bytes of each tile-part (thread per tile-part)
 __global__ void __launch_bounds__(64) k_t2_tparts(T2Args a) {
     const int t = blockIdx.x * 64 + threadIdx.x;
-    if (t >= a.ntp) return;
+    if (t >= a.ntp || (a.halt && *a.halt)) return;
     const TpDesc d = a.tps[t];
     const size_t p0 = (size_t)d.prec0 * a.L, p1 = (size_t)(d.prec0 + d.nprec) * a.L;
     uint64_t body = 0, plt = 0, seg = 0;
@@ -329,6 +330,7 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
                                                   const uint64_t *kc, const uint32_t *ndec_key, T2Summary *sum) {
     __shared__ uint64_t part[256];
     __shared__ int64_t lay[256][kMaxLayers > 8 ? 8 : kMaxLayers];
+    if (a.halt && *a.halt) return;  // the whole workgroup
     const int tid = threadIdx.x;
     const int chunk = (a.ntp + 255) / 256;
     const int t0 = min(a.ntp, tid * chunk), t1 = min(a.ntp, t0 + chunk);
@@ -545,26 +547,29 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
         !ensure_t2<uint64_t>(t2blkdst, (size_t)nb * L, err) || !ensure_t2<T2Summary>(t2sum, 1, err))
         return false;
     if (!h_sum) HIPCHECK(hipHostMalloc((void **)&h_sum, sizeof(T2Summary), hipHostMallocDefault));
-    if (!h_tot) HIPCHECK(hipHostMalloc((void **)&h_tot, 4 * sizeof(int64_t), hipHostMallocDefault));
-    if (t2_nprec) HIPCHECK(hipMemcpyAsync(t2prec.ptr, T.prec.data(), sizeof(PrecDesc) * T.prec.size(),
-                                          hipMemcpyHostToDevice, stream));
-    if (t2_ntp) HIPCHECK(hipMemcpyAsync(t2tp.ptr, T.tp.data(), sizeof(TpDesc) * T.tp.size(), hipMemcpyHostToDevice,
-                                        stream));
+    if (!h2d(t2prec.ptr, T.prec.data(), sizeof(PrecDesc) * T.prec.size(), err) ||
+        !h2d(t2tp.ptr, T.tp.data(), sizeof(TpDesc) * T.tp.size(), err))
+        return false;
     return true;
 }
 
-bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,
-                         std::string &err) {
-    HIPCHECK(hipSetDevice(device));
+void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt) {
     const int nb = (int)plan.blocks.size();
     T2Args a = t2_args(plan);
-    HIPCHECK(hipEventRecord(ev[8], stream));
+    a.halt = halt;
     if (t2_nprec) hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
     if (t2_ntp) hipLaunchKernelGGL(k_t2_tparts, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
                        (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
                        with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
                        (const uint32_t *)ordkey2.ptr, (T2Summary *)t2sum.ptr);
+}
+
+bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,
+                         std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(hipEventRecord(ev[8], stream));
+    t2_size_launch(plan, with_kc, nullptr);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipMemcpyAsync(h_sum, t2sum.ptr, sizeof(T2Summary), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipEventRecord(ev[9], stream));

@@ -54,11 +54,11 @@ class Stats(Structure):
                 ("dwt_ms", c_double), ("quant_ms", c_double), ("t1_ms", c_double),
                 ("pcrd_ms", c_double), ("d2h_ms", c_double), ("t2_ms", c_double),
                 ("codeblocks", c_int64), ("coded_passes", c_int64), ("t1_bytes", c_int64),
-                ("out_bytes", c_int64), ("rate_iterations", c_int32), ("reserved", c_int32),
+                ("out_bytes", c_int64), ("rate_iterations", c_int32), ("host_waits", c_int32),
                 ("t1_cm_ms", c_double), ("t1_mq_ms", c_double), ("mq_decisions", c_int64)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 # every symbol include/jp2hip.h declares

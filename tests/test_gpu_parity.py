@@ -132,6 +132,9 @@ def test_c2_full_size_jpx_on_rate(encoder, golden):
     assert 0.97 * 3.0 * 6000 * 4000 / 8 <= len(cs) <= 3.0 * 6000 * 4000 / 8
     c = [x for x in golden["lossy"] if x["name"] == "c2_synth_rgb8_6000x4000"][0]
     assert hashlib.sha256(cs).hexdigest() == c["oracle_sha256"]
+    # the rate loop runs on the device: one wait for the final size, one for
+    # the bytes (a third batch of rate iterations would add one)
+    assert st.host_waits <= 2, st.host_waits
 
 
 def test_c3_full_size_lossless_roundtrip(encoder):
@@ -140,6 +143,7 @@ def test_c3_full_size_lossless_roundtrip(encoder):
     rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
     got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSLESS, rc)
     assert np.array_equal(im.decode_opj(got), img)
+    assert st.host_waits <= 2, st.host_waits
 
 
 def test_deterministic_and_reusable_context(encoder):
