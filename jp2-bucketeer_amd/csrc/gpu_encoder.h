@@ -174,6 +174,7 @@ class GpuEncoder {
     RateState *h_rs = nullptr;  // pinned
     DevBuf t2prec, t2tp, t2tt, t2lblock, t2incl, t2pklen, t2pkoff, t2tplen, t2tphdr, t2tpoff, t2blkdst, t2out, t2sum;
     int t2_nprec = 0, t2_ntp = 0;
+    uint64_t front_gen = 0, t2_gen = 0;  // plan generation whose tables are resident
     T2Summary *h_sum = nullptr;
     int64_t *h_tot = nullptr;  // pinned [8]: t1 total, -, k_t1_mq span[2], unpack error, segment tail[2]
     bool profiled = false;

@@ -86,6 +86,10 @@ struct Plan {
     // [tile0, tile0 + ntc/nc) = image rows [row0, row0 + band_h); its blocks
     // are the full plan's blocks [block0, block0 + blocks.size())
     int row0 = 0, band_h = 0, tile0 = 0, block0 = 0;
+    // identity of this plan's contents (build_plan / make_subplan): a device
+    // context that already holds the tables of generation `gen` skips
+    // uploading them again
+    uint64_t gen = 0;
 };
 
 bool build_plan(Plan &plan, const jp2hip_recipe &rc, int w, int h, int nc, int bits,

@@ -1194,13 +1194,20 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<int32_t>(tch, plan.ntc, err)) return false;
     if (!ensure<uint64_t>(strips, lay.nstrips, err)) return false;
 
-    if (!h2d(blocks.ptr, plan.blocks.data(), sizeof(BlockDesc) * nb, err) ||
-        !h2d(weight.ptr, plan.weight.data(), sizeof(double) * nb, err) ||
-        !h2d(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, err) ||
-        !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err) ||
-        !h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err) ||
-        !ensure<int32_t>(t1ord, nb, err) || !h2d(t1ord.ptr, plan.t1_order.data(), sizeof(int32_t) * nb, err))
+    if (!ensure<int32_t>(t1ord, nb, err) || !h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err))
         return false;
+    // the plan's tables stay resident while the context encodes the same
+    // geometry (plan.gen; buffers only grow, so they are still in place)
+    if (!plan.gen || plan.gen != front_gen) {
+        front_gen = 0;
+        if (!h2d(blocks.ptr, plan.blocks.data(), sizeof(BlockDesc) * nb, err) ||
+            !h2d(weight.ptr, plan.weight.data(), sizeof(double) * nb, err) ||
+            !h2d(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, err) ||
+            !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err) ||
+            !h2d(t1ord.ptr, plan.t1_order.data(), sizeof(int32_t) * nb, err))
+            return false;
+        front_gen = plan.gen;
+    }
     HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
 
     HIPCHECK(hipEventRecord(ev[0], stream));

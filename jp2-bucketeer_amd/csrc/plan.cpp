@@ -5,6 +5,7 @@
 // KakaduConverter.java:38-44 (tiles anchored at 0, 2^L | tile size, so every
 // decomposition level starts at an even coordinate).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -14,6 +15,10 @@
 namespace jp2hip {
 
 static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static uint64_t next_gen() {
+    static std::atomic<uint64_t> g{0};
+    return ++g;
+}
 
 int prec_log2(const jp2hip_recipe &rc, int r, bool vertical) {
     int idx = rc.levels - r;  // Kakadu lists the highest resolution first
@@ -278,6 +283,7 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
     P.sm_words = smw;
     P.out_bytes = ob;
     t1_lane_order(P);
+    P.gen = next_gen();
     return true;
 }
 

@@ -547,9 +547,12 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
         !ensure_t2<uint64_t>(t2blkdst, (size_t)nb * L, err) || !ensure_t2<T2Summary>(t2sum, 1, err))
         return false;
     if (!h_sum) HIPCHECK(hipHostMalloc((void **)&h_sum, sizeof(T2Summary), hipHostMallocDefault));
+    if (plan.gen && plan.gen == t2_gen) return true;  // resident (same plan, same tables)
+    t2_gen = 0;
     if (!h2d(t2prec.ptr, T.prec.data(), sizeof(PrecDesc) * T.prec.size(), err) ||
         !h2d(t2tp.ptr, T.tp.data(), sizeof(TpDesc) * T.tp.size(), err))
         return false;
+    t2_gen = plan.gen;
     return true;
 }
 
