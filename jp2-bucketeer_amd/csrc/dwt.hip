@@ -261,6 +261,86 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn r
     }
 }
 
+// Horizontal lifting without barriers: thread = (staged row, 16-sample
+// segment), the segment's 16 samples plus a 4-sample halo on each side read
+// from LDS into registers (six 16-byte reads), lifted there (the halo absorbs
+// the 4-step footprint: the 16 kept samples are exact, as in lift_regs),
+// scaled and written de-interleaved as 8 low + 8 high words (two 16-byte
+// stores each when the row is aligned).  Rows as in hlift_write.
+template <bool REV, int NROWS, typename RowFn>
+__device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, RowFn rows) {
+    const int nseg = (W + 15) >> 4;
+    const int nlh = (W + 1) / 2;
+    for (int it = threadIdx.x; it < NROWS * nseg; it += kDwtThreads) {
+        const int r = it / nseg, k = it - r * nseg;
+        int32_t *lrow, *hrow;
+        if (!rows(r, lrow, hrow)) continue;
+        const int x0 = (k << 4) - 4;  // window: samples x0 .. x0+23 (even start)
+        const int4 *src = (const int4 *)(lds + kPadL + r * ld + x0);
+        int32_t v[24];
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            const int4 t = src[q];
+            v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+        }
+        if (W > 1) {
+            const int pl = -x0;             // window slot of x = 0 (4 for segment 0)
+            const int pr = W - 1 - x0;      // window slot of x = W-1
+            const bool interior = x0 >= 0 && x0 + 24 <= W;
+            const int nsteps = REV ? 2 : 4;
+#pragma unroll
+            for (int st = 0; st < nsteps; st++) {
+                const int par = (st & 1) ? 0 : 1;  // odd samples first
+#pragma unroll
+                for (int p = 1 + (par ^ 1); p < 23; p += 2) {
+                    int32_t l = v[p - 1], rr = v[p + 1];
+                    if (!interior) {
+                        if (p < pl || p > pr) continue;  // outside the signal
+                        if (p == pl) l = v[p + 1];       // symmetric extension at x = 0
+                        if (p == pr) rr = v[p - 1];      // ... and at x = W-1
+                    }
+                    if (REV) {
+                        if (st == 0) v[p] -= (l + rr) >> 1;
+                        else v[p] += (l + rr + 2) >> 2;
+                    } else {
+                        const float cf = st == 0 ? A97 : (st == 1 ? B97 : (st == 2 ? G97 : D97));
+                        float t = __int_as_float(l) + __int_as_float(rr);
+                        t = cf * t;
+                        v[p] = __float_as_int(__int_as_float(v[p]) + t);
+                    }
+                }
+            }
+        }
+        // slots 4..19 = samples k*16 .. k*16+15: even -> low j = x/2, odd -> high
+        int32_t lo[8], hi[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            lo[q] = v[4 + 2 * q];
+            hi[q] = v[5 + 2 * q];
+            if (!REV && W > 1) {
+                lo[q] = __float_as_int(__int_as_float(lo[q]) * INVK97);
+                hi[q] = __float_as_int(__int_as_float(hi[q]) * K97);
+            }
+        }
+        const int j0 = k << 3;
+        int32_t *ld_ = lrow + j0, *hd = hrow + nlh + j0;
+        const bool full = (k << 4) + 16 <= W;
+        if (full && (((uintptr_t)ld_ | (uintptr_t)hd) & 15) == 0) {
+            ((int4 *)ld_)[0] = make_int4(lo[0], lo[1], lo[2], lo[3]);
+            ((int4 *)ld_)[1] = make_int4(lo[4], lo[5], lo[6], lo[7]);
+            ((int4 *)hd)[0] = make_int4(hi[0], hi[1], hi[2], hi[3]);
+            ((int4 *)hd)[1] = make_int4(hi[4], hi[5], hi[6], hi[7]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int x = (k << 4) + 2 * q;
+                if (x < W) ld_[q] = lo[q];
+                if (x + 1 < W) hd[q] = hi[q];
+            }
+        }
+    }
+}
+
 template <bool REV, bool INGEST, int RB>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     extern __shared__ int32_t lds[];
@@ -300,7 +380,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     const int nlv = (H + 1) / 2;
     int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
     int32_t *ll = a.ll ? (int32_t *)a.ll + (size_t)tc * a.ll_tc : nullptr;
-    hlift_write<REV, RB>(lds, W, ld, [&](int k, int32_t *&lrow, int32_t *&hrow) -> bool {
+    hlift_seg<REV, RB>(lds, W, ld, [&](int k, int32_t *&lrow, int32_t *&hrow) -> bool {
         if (k >= nkeep) return false;
         const int y = r0 + k;
         const bool ylo = (y & 1) == 0;
@@ -416,6 +496,171 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
         lrow = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride : hrow;
         return true;
     });
+}
+
+// Level 1 with ingest, streaming: a workgroup owns a band of kStreamBand
+// output rows of one tile (every component); thread = up to CPT columns.
+// The vertical lifting runs as a pipeline down the band instead of over a
+// window with a halo per 8 rows: at row pair (m-1, m) step k updates row
+// m-1-k (k = 0..NS-1), after which rows m-NS and m-NS+1 are final, so each
+// TIFF row is read and lifted once (plus NS rows above and below the band).
+// Every 8 final rows go through LDS for the horizontal lifting and the
+// de-interleaved write (hlift_write).  Each sample sees the same expressions
+// in the same order as lift_regs / oracle fwd97_1d (bit-exact): an update
+// whose neighbour lies outside the streamed rows is skipped, as lift_regs
+// leaves a window's edge stale, and never reaches a kept row.
+constexpr int kStreamBand = 64;
+template <bool REV, int NC, int CPT>
+__global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
+    extern __shared__ int32_t lds[];
+    constexpr int NS = REV ? 2 : 4;  // lifting steps
+    constexpr int NWIN = NS + 2;     // rows m-NS-1 .. m
+    constexpr int RB = 8;            // rows per horizontal batch
+    const int t = blockIdx.y;
+    const int tc0 = t * NC;
+    const int W = a.tc_w[tc0], H = a.tc_h[tc0];
+    const int r0 = blockIdx.x * kStreamBand;
+    if (r0 >= H) return;
+    const int r1 = min(H, r0 + kStreamBand);
+    const int s = max(0, r0 - NS), e = min(H, r1 + NS);  // rows streamed [s, e); s even
+    const int tid = threadIdx.x;
+    const int ld = lds_row_stride(W);
+    const int32_t off = 1 << (a.bits - 1);
+    const int bps = a.bits >> 3;
+    const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : NC) * bps;
+    const int gx0 = (t % a.ntx) * a.tile_w, gy0 = a.row0 + (t / a.ntx) * a.tile_h;
+    const bool mct = a.mct && NC >= 3;
+    // strip walk: the strip and row-in-strip of the next row to load
+    int strip = (gy0 + s) / a.rps, ly = gy0 + s - strip * a.rps;
+    int32_t w[CPT][NC][NWIN];
+#pragma unroll
+    for (int j = 0; j < CPT; j++)
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i < NWIN; i++) w[j][c][i] = 0;
+    auto load_row = [&](int slot) {  // the next row (s, s+1, ...) into window slot `slot`
+        uint64_t ro[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+            ro[c] = a.strip_off[a.planar == 2 ? (size_t)c * a.spp_strips + strip : (size_t)strip] +
+                    (size_t)ly * row_bytes;
+        if (++ly == a.rps) {
+            ly = 0;
+            strip++;
+        }
+#pragma unroll
+        for (int j = 0; j < CPT; j++) {
+            const int x = tid + j * kDwtThreads;
+            if (x >= W) continue;
+            const size_t xo = a.planar == 2 ? (size_t)(gx0 + x) * bps : (size_t)(gx0 + x) * NC * bps;
+            int32_t smp[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const uint8_t *p8 = a.tif + (a.planar == 2 ? ro[c] : ro[0] + (size_t)c * bps) + xo;
+                if (a.bits == 8) smp[c] = (int32_t)p8[0];
+                else smp[c] = a.big_endian ? (((int32_t)p8[0] << 8) | p8[1]) : (p8[0] | ((int32_t)p8[1] << 8));
+                smp[c] -= off;
+            }
+#pragma unroll
+            for (int c = 0; c < NC; c++) w[j][c][slot] = REV ? smp[c] : __float_as_int((float)smp[c]);
+            if constexpr (NC >= 3) if (mct) {
+                if (REV) {
+                    w[j][0][slot] = (smp[0] + 2 * smp[1] + smp[2]) >> 2;
+                    w[j][1][slot] = smp[2] - smp[1];
+                    w[j][2][slot] = smp[0] - smp[1];
+                } else {
+                    const float R = (float)smp[0], G = (float)smp[1], B = (float)smp[2];
+                    float f0 = 0.299f * R; f0 = f0 + 0.587f * G; f0 = f0 + 0.114f * B;
+                    float f1 = -0.16875f * R; f1 = f1 - 0.33126f * G; f1 = f1 + 0.5f * B;
+                    float f2 = 0.5f * R; f2 = f2 - 0.41869f * G; f2 = f2 - 0.08131f * B;
+                    w[j][0][slot] = __float_as_int(f0);
+                    w[j][1][slot] = __float_as_int(f1);
+                    w[j][2][slot] = __float_as_int(f2);
+                }
+            }
+        }
+    };
+    const int nlv = (H + 1) / 2;
+    int bb = r0;  // first row of the batch being filled
+    // iteration m (even): rows m-1, m arrive; the last iteration emits row r1-1
+    const int m_last = ((r1 - 1 + NS - 1) + 1) & ~1;
+    for (int m = s; m <= m_last; m += 2) {
+#pragma unroll
+        for (int j = 0; j < CPT; j++)
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+#pragma unroll
+                for (int i = 0; i + 2 < NWIN; i++) w[j][c][i] = w[j][c][i + 2];
+        if (m - 1 >= s && m - 1 < e) load_row(NWIN - 2);
+        if (m < e) load_row(NWIN - 1);
+        if (H > 1) {
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                const int tr = m - 1 - k, ti = NWIN - 2 - k;  // target row, its window slot
+                if (tr < s || tr >= e) continue;
+                // neighbours: window slots ti-1 / ti+1; symmetric extension at
+                // rows 0 and H-1; a neighbour outside the streamed rows -> skip
+                int li = ti - 1, ri = ti + 1;
+                if (tr == 0) li = ti + 1;
+                else if (tr - 1 < s) continue;
+                if (tr + 1 >= H) ri = ti - 1;
+                else if (tr + 1 >= e) continue;
+#pragma unroll
+                for (int j = 0; j < CPT; j++)
+#pragma unroll
+                    for (int c = 0; c < NC; c++) {
+                        // constant slots after unrolling: select among the few candidates
+                        const int32_t lv = li == ti - 1 ? w[j][c][ti - 1] : w[j][c][ti + 1];
+                        const int32_t rv = ri == ti + 1 ? w[j][c][ti + 1] : w[j][c][ti - 1];
+                        if (REV) {
+                            if (k == 0) w[j][c][ti] -= (lv + rv) >> 1;
+                            else w[j][c][ti] += (lv + rv + 2) >> 2;
+                        } else {
+                            const float cf = k == 0 ? A97 : (k == 1 ? B97 : (k == 2 ? G97 : D97));
+                            float tt = __int_as_float(lv) + __int_as_float(rv);
+                            tt = cf * tt;
+                            w[j][c][ti] = __float_as_int(__int_as_float(w[j][c][ti]) + tt);
+                        }
+                    }
+            }
+        }
+        // rows m-NS (even) and m-NS+1 (odd) are final: scale, stage in LDS
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int y = m - NS + q;
+            if (y < r0 || y >= r1) continue;
+#pragma unroll
+            for (int j = 0; j < CPT; j++) {
+                const int x = tid + j * kDwtThreads;
+                if (x >= W) continue;
+#pragma unroll
+                for (int c = 0; c < NC; c++) {
+                    int32_t v = w[j][c][1 + q];
+                    if (!REV && H > 1) v = __float_as_int(__int_as_float(v) * (q ? K97 : INVK97));
+                    lds[kPadL + (c * RB + (y - bb)) * ld + x] = v;
+                }
+            }
+        }
+        const int ylast = m - NS + 1;
+        if (ylast >= r0 && (ylast - bb == RB - 1 || ylast >= r1 - 1)) {
+            __syncthreads();
+            const int nkeep = min(RB, r1 - bb);
+            hlift_seg<REV, NC * RB>(lds, W, ld, [&](int r, int32_t *&lrow, int32_t *&hrow) -> bool {
+                const int c = r / RB, k = r - c * RB;
+                if (k >= nkeep) return false;
+                const int tc = tc0 + c, y = bb + k;
+                const bool ylo = (y & 1) == 0;
+                int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
+                hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
+                lrow = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride
+                                     : hrow;
+                return true;
+            });
+            __syncthreads();
+            bb += RB;
+        }
+    }
 }
 
 struct DwtTailArgs {
@@ -553,6 +798,29 @@ static void launch_l1_nc(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &
     }
     hipLaunchKernelGGL((k_dwt_l1<REV, NC, 8>), g, dim3(kDwtThreads), lds, st, a);
 }
+template <bool REV, int NC, int CPT>
+static void launch_l1s_c(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    static bool wide = false;
+    if (lds > (size_t)kDwtLdsWords * 4 && !wide) {
+        (void)hipFuncSetAttribute((const void *)k_dwt_l1s<REV, NC, CPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kDwtLdsWordsWide * 4);
+        wide = true;
+    }
+    hipLaunchKernelGGL((k_dwt_l1s<REV, NC, CPT>), g, dim3(kDwtThreads), lds, st, a);
+}
+template <bool REV, int NC>
+static void launch_l1s_nc(int cpt, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    if (cpt == 1) launch_l1s_c<REV, NC, 1>(g, lds, st, a);
+    else if (cpt == 2) launch_l1s_c<REV, NC, 2>(g, lds, st, a);
+    else launch_l1s_c<REV, NC, 4>(g, lds, st, a);
+}
+template <bool REV>
+static void launch_l1s(int nc, int cpt, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    if (nc == 1) launch_l1s_nc<REV, 1>(cpt, g, lds, st, a);
+    else if (nc == 2) launch_l1s_nc<REV, 2>(cpt, g, lds, st, a);
+    else if (nc == 3) launch_l1s_nc<REV, 3>(cpt, g, lds, st, a);
+    else launch_l1s_nc<REV, 4>(cpt, g, lds, st, a);
+}
 template <bool REV>
 static void launch_l1(int nc, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
     if (nc == 1) launch_l1_nc<REV, 1>(g, lds, st, a);
@@ -613,7 +881,14 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
         // fit in LDS (each TIFF pixel read once)
         constexpr int kRb1 = 8;
         const size_t lds1 = ((size_t)p.nc * kRb1 * lds_row_stride(maxW) + kPadL + kPadR) * 4;
-        if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
+        const int cpt = maxW <= kDwtThreads ? 1 : (maxW <= 2 * kDwtThreads ? 2 : 4);
+        if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && maxW <= 4 * kDwtThreads &&
+            !getenv("JP2HIP_DWT_L1_WINDOW") && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
+            // streaming vertical pass (k_dwt_l1s), bands of kStreamBand rows
+            dim3 g1((maxH + kStreamBand - 1) / kStreamBand, p.ntc / p.nc);
+            if (p.reversible) launch_l1s<true>(p.nc, cpt, g1, lds1, st, a);
+            else launch_l1s<false>(p.nc, cpt, g1, lds1, st, a);
+        } else if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
             dim3 g1((maxH + kRb1 - 1) / kRb1, p.ntc / p.nc);
             if (p.reversible) launch_l1<true>(p.nc, g1, lds1, st, a);
             else launch_l1<false>(p.nc, g1, lds1, st, a);

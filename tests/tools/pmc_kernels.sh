@@ -1,9 +1,12 @@
 #!/bin/bash
 # rocprofv3 PMC passes (one counter set per run, as the pool requires) over
 # single-image C2 encodes: SQ instruction / wait / LDS counters and HBM bytes
-# for the front-end kernels (DWT, quantiser, tier-1).
+# for the front-end kernels (DWT, quantiser, tier-1).  GPU_MAX_HW_QUEUES is
+# set here, in the environment rocprofv3 hands to bench.py, to the value
+# bench.py itself uses for 12 contexts (16).
 set -o pipefail
 export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=16 JP2HIP_KEEP_HW_QUEUES=1
 o=gpurun_out/${1:-pmc}
 re=${2:-"k_dwt|k_quant|k_t1_cm|k_t1_mq"}
 mkdir -p $o
