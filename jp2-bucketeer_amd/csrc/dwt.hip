@@ -130,6 +130,7 @@ struct DwtBandArgs {
     size_t ll_tc;
     const int32_t *tc_w, *tc_h;
     int level, R;
+    int ragged;  // some tile width is not a multiple of 16 (k_dwt_l1s second launch)
 };
 
 __device__ __forceinline__ int32_t tiff_sample(const DwtBandArgs &a, size_t rowoff, int x, int c) {
@@ -267,7 +268,7 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn r
 // the 4-step footprint: the 16 kept samples are exact, as in lift_regs),
 // scaled and written de-interleaved as 8 low + 8 high words (two 16-byte
 // stores each when the row is aligned).  Rows as in hlift_write.
-template <bool REV, int NROWS, typename RowFn>
+template <bool REV, int NROWS, bool ALIGNED, typename RowFn>
 __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, RowFn rows) {
     const int nseg = (W + 15) >> 4;
     const int nlh = (W + 1) / 2;
@@ -283,7 +284,38 @@ __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, Row
             const int4 t = src[q];
             v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
         }
-        if (W > 1) {
+        if (ALIGNED) {  // caller: W > 1 and a multiple of 16
+            // W a multiple of 16 (every full tile): the signal ends fall on
+            // fixed window slots, so the symmetric extension is written into
+            // the window (x = -i -> i, x = W-1+i -> W-1-i) and every segment
+            // lifts the same straight-line code.  The lifting steps keep a
+            // symmetric signal symmetric (commutative sums), so this equals
+            // mirroring at every step, bit for bit.
+            if (k == 0) {
+                v[0] = v[8]; v[1] = v[7]; v[2] = v[6]; v[3] = v[5];
+            }
+            if (k == nseg - 1) {
+                v[20] = v[18]; v[21] = v[17]; v[22] = v[16]; v[23] = v[15];
+            }
+            const int nsteps = REV ? 2 : 4;
+#pragma unroll
+            for (int st = 0; st < nsteps; st++) {
+                const int par = (st & 1) ? 0 : 1;  // odd samples first
+#pragma unroll
+                for (int p = 1 + (par ^ 1); p < 23; p += 2) {
+                    const int32_t l = v[p - 1], rr = v[p + 1];
+                    if (REV) {
+                        if (st == 0) v[p] -= (l + rr) >> 1;
+                        else v[p] += (l + rr + 2) >> 2;
+                    } else {
+                        const float cf = st == 0 ? A97 : (st == 1 ? B97 : (st == 2 ? G97 : D97));
+                        float t = __int_as_float(l) + __int_as_float(rr);
+                        t = cf * t;
+                        v[p] = __float_as_int(__int_as_float(v[p]) + t);
+                    }
+                }
+            }
+        } else if (W > 1) {
             const int pl = -x0;             // window slot of x = 0 (4 for segment 0)
             const int pr = W - 1 - x0;      // window slot of x = W-1
             const bool interior = x0 >= 0 && x0 + 24 <= W;
@@ -312,30 +344,27 @@ __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, Row
             }
         }
         // slots 4..19 = samples k*16 .. k*16+15: even -> low j = x/2, odd -> high
-        int32_t lo[8], hi[8];
+        if (!REV && W > 1) {
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            lo[q] = v[4 + 2 * q];
-            hi[q] = v[5 + 2 * q];
-            if (!REV && W > 1) {
-                lo[q] = __float_as_int(__int_as_float(lo[q]) * INVK97);
-                hi[q] = __float_as_int(__int_as_float(hi[q]) * K97);
+            for (int q = 0; q < 8; q++) {
+                v[4 + 2 * q] = __float_as_int(__int_as_float(v[4 + 2 * q]) * INVK97);
+                v[5 + 2 * q] = __float_as_int(__int_as_float(v[5 + 2 * q]) * K97);
             }
         }
         const int j0 = k << 3;
         int32_t *ld_ = lrow + j0, *hd = hrow + nlh + j0;
         const bool full = (k << 4) + 16 <= W;
         if (full && (((uintptr_t)ld_ | (uintptr_t)hd) & 15) == 0) {
-            ((int4 *)ld_)[0] = make_int4(lo[0], lo[1], lo[2], lo[3]);
-            ((int4 *)ld_)[1] = make_int4(lo[4], lo[5], lo[6], lo[7]);
-            ((int4 *)hd)[0] = make_int4(hi[0], hi[1], hi[2], hi[3]);
-            ((int4 *)hd)[1] = make_int4(hi[4], hi[5], hi[6], hi[7]);
+            ((int4 *)ld_)[0] = make_int4(v[4], v[6], v[8], v[10]);
+            ((int4 *)ld_)[1] = make_int4(v[12], v[14], v[16], v[18]);
+            ((int4 *)hd)[0] = make_int4(v[5], v[7], v[9], v[11]);
+            ((int4 *)hd)[1] = make_int4(v[13], v[15], v[17], v[19]);
         } else {
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int x = (k << 4) + 2 * q;
-                if (x < W) ld_[q] = lo[q];
-                if (x + 1 < W) hd[q] = hi[q];
+                if (x < W) ld_[q] = v[4 + 2 * q];
+                if (x + 1 < W) hd[q] = v[5 + 2 * q];
             }
         }
     }
@@ -380,14 +409,16 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     const int nlv = (H + 1) / 2;
     int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
     int32_t *ll = a.ll ? (int32_t *)a.ll + (size_t)tc * a.ll_tc : nullptr;
-    hlift_seg<REV, RB>(lds, W, ld, [&](int k, int32_t *&lrow, int32_t *&hrow) -> bool {
+    auto rows = [&](int k, int32_t *&lrow, int32_t *&hrow) -> bool {
         if (k >= nkeep) return false;
         const int y = r0 + k;
         const bool ylo = (y & 1) == 0;
         hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
         lrow = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : hrow;
         return true;
-    });
+    };
+    if (W > 1 && (W & 15) == 0) hlift_seg<REV, RB, true>(lds, W, ld, rows);
+    else hlift_seg<REV, RB, false>(lds, W, ld, rows);
 }
 
 // Level 1 with ingest, every component of a tile at once: a workgroup owns
@@ -510,17 +541,18 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
 // whose neighbour lies outside the streamed rows is skipped, as lift_regs
 // leaves a window's edge stale, and never reaches a kept row.
 constexpr int kStreamBand = 64;
-template <bool REV, int NC, int CPT>
+template <bool REV, int NC, int CPT, int RB, bool ALIGNED>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     extern __shared__ int32_t lds[];
     constexpr int NS = REV ? 2 : 4;  // lifting steps
     constexpr int NWIN = NS + 2;     // rows m-NS-1 .. m
-    constexpr int RB = 8;            // rows per horizontal batch
     const int t = blockIdx.y;
     const int tc0 = t * NC;
     const int W = a.tc_w[tc0], H = a.tc_h[tc0];
     const int r0 = blockIdx.x * kStreamBand;
-    if (r0 >= H) return;
+    // two launches cover the tiles: widths that are multiples of 16 (the
+    // straight-line horizontal lifting) and the rest
+    if (r0 >= H || ALIGNED != (W > 1 && (W & 15) == 0)) return;
     const int r1 = min(H, r0 + kStreamBand);
     const int s = max(0, r0 - NS), e = min(H, r1 + NS);  // rows streamed [s, e); s even
     const int tid = threadIdx.x;
@@ -530,7 +562,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : NC) * bps;
     const int gx0 = (t % a.ntx) * a.tile_w, gy0 = a.row0 + (t / a.ntx) * a.tile_h;
     const bool mct = a.mct && NC >= 3;
-    // strip walk: the strip and row-in-strip of the next row to load
+    // strip walk: the strip and row-in-strip of the next row to fetch
     int strip = (gy0 + s) / a.rps, ly = gy0 + s - strip * a.rps;
     int32_t w[CPT][NC][NWIN];
 #pragma unroll
@@ -539,7 +571,10 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         for (int c = 0; c < NC; c++)
 #pragma unroll
             for (int i = 0; i < NWIN; i++) w[j][c][i] = 0;
-    auto load_row = [&](int slot) {  // the next row (s, s+1, ...) into window slot `slot`
+    // raw (level-shifted) samples of the next row pair, fetched one
+    // iteration ahead so the loads are in flight during the lifting
+    int32_t pf[2][CPT][NC];
+    auto fetch = [&](int q) {  // the next row (s, s+1, ...) into pf[q]
         uint64_t ro[NC];
 #pragma unroll
         for (int c = 0; c < NC; c++)
@@ -551,17 +586,22 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < CPT; j++) {
-            const int x = tid + j * kDwtThreads;
-            if (x >= W) continue;
+            const int x = min(tid + j * kDwtThreads, W - 1);  // columns past W repeat the last one
             const size_t xo = a.planar == 2 ? (size_t)(gx0 + x) * bps : (size_t)(gx0 + x) * NC * bps;
-            int32_t smp[NC];
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const uint8_t *p8 = a.tif + (a.planar == 2 ? ro[c] : ro[0] + (size_t)c * bps) + xo;
-                if (a.bits == 8) smp[c] = (int32_t)p8[0];
-                else smp[c] = a.big_endian ? (((int32_t)p8[0] << 8) | p8[1]) : (p8[0] | ((int32_t)p8[1] << 8));
-                smp[c] -= off;
+                int32_t v;
+                if (a.bits == 8) v = (int32_t)p8[0];
+                else v = a.big_endian ? (((int32_t)p8[0] << 8) | p8[1]) : (p8[0] | ((int32_t)p8[1] << 8));
+                pf[q][j][c] = v - off;
             }
+        }
+    };
+    auto place = [&](int q, int slot) {  // colour transform, into window slot `slot`
+#pragma unroll
+        for (int j = 0; j < CPT; j++) {
+            const int32_t *smp = pf[q][j];
 #pragma unroll
             for (int c = 0; c < NC; c++) w[j][c][slot] = REV ? smp[c] : __float_as_int((float)smp[c]);
             if constexpr (NC >= 3) if (mct) {
@@ -581,6 +621,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
             }
         }
     };
+    fetch(1);  // row s (iteration m = s takes rows s-1, s)
     const int nlv = (H + 1) / 2;
     int bb = r0;  // first row of the batch being filled
     // iteration m (even): rows m-1, m arrive; the last iteration emits row r1-1
@@ -592,8 +633,10 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
             for (int c = 0; c < NC; c++)
 #pragma unroll
                 for (int i = 0; i + 2 < NWIN; i++) w[j][c][i] = w[j][c][i + 2];
-        if (m - 1 >= s && m - 1 < e) load_row(NWIN - 2);
-        if (m < e) load_row(NWIN - 1);
+        if (m - 1 >= s && m - 1 < e) place(0, NWIN - 2);
+        if (m < e) place(1, NWIN - 1);
+        if (m + 1 < e) fetch(0);
+        if (m + 2 < e) fetch(1);
         if (H > 1) {
 #pragma unroll
             for (int k = 0; k < NS; k++) {
@@ -646,7 +689,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         if (ylast >= r0 && (ylast - bb == RB - 1 || ylast >= r1 - 1)) {
             __syncthreads();
             const int nkeep = min(RB, r1 - bb);
-            hlift_seg<REV, NC * RB>(lds, W, ld, [&](int r, int32_t *&lrow, int32_t *&hrow) -> bool {
+            hlift_seg<REV, NC * RB, ALIGNED>(lds, W, ld, [&](int r, int32_t *&lrow, int32_t *&hrow) -> bool {
                 const int c = r / RB, k = r - c * RB;
                 if (k >= nkeep) return false;
                 const int tc = tc0 + c, y = bb + k;
@@ -798,15 +841,23 @@ static void launch_l1_nc(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &
     }
     hipLaunchKernelGGL((k_dwt_l1<REV, NC, 8>), g, dim3(kDwtThreads), lds, st, a);
 }
-template <bool REV, int NC, int CPT>
-static void launch_l1s_c(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+template <bool REV, int NC, int CPT, int RB>
+static void launch_l1s_rb(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
     static bool wide = false;
     if (lds > (size_t)kDwtLdsWords * 4 && !wide) {
-        (void)hipFuncSetAttribute((const void *)k_dwt_l1s<REV, NC, CPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  kDwtLdsWordsWide * 4);
+        (void)hipFuncSetAttribute((const void *)k_dwt_l1s<REV, NC, CPT, RB, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwtLdsWordsWide * 4);
+        (void)hipFuncSetAttribute((const void *)k_dwt_l1s<REV, NC, CPT, RB, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDwtLdsWordsWide * 4);
         wide = true;
     }
-    hipLaunchKernelGGL((k_dwt_l1s<REV, NC, CPT>), g, dim3(kDwtThreads), lds, st, a);
+    hipLaunchKernelGGL((k_dwt_l1s<REV, NC, CPT, RB, true>), g, dim3(kDwtThreads), lds, st, a);
+    if (a.ragged) hipLaunchKernelGGL((k_dwt_l1s<REV, NC, CPT, RB, false>), g, dim3(kDwtThreads), lds, st, a);
+}
+template <bool REV, int NC, int CPT>
+static void launch_l1s_c(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    if (a.R == 8) launch_l1s_rb<REV, NC, CPT, 8>(g, lds, st, a);
+    else launch_l1s_rb<REV, NC, CPT, 4>(g, lds, st, a);
 }
 template <bool REV, int NC>
 static void launch_l1s_nc(int cpt, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
@@ -841,6 +892,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
     a.plane_w = p.plane_w;
     a.plane = (size_t)p.plane_w * p.plane_h;
     a.tc_w = p.tc_w; a.tc_h = p.tc_h;
+    a.ragged = (p.tile_w & 15) || (p.last_tile_w & 15) || p.last_tile_w == 1;
     const int ll_stride = (p.plane_w + 1) / 2;
     const size_t ll_tc = (size_t)ll_stride * ((p.plane_h + 1) / 2);
     void *scratch[2] = {p.scratch0, p.scratch1};
@@ -884,10 +936,14 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
         const int cpt = maxW <= kDwtThreads ? 1 : (maxW <= 2 * kDwtThreads ? 2 : 4);
         if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && maxW <= 4 * kDwtThreads &&
             !getenv("JP2HIP_DWT_L1_WINDOW") && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
-            // streaming vertical pass (k_dwt_l1s), bands of kStreamBand rows
+            // streaming vertical pass (k_dwt_l1s), bands of kStreamBand rows,
+            // horizontal batches of 4 rows (8: JP2HIP_DWT_L1_RB=8)
+            const char *rbe = getenv("JP2HIP_DWT_L1_RB");
+            a.R = (rbe && atoi(rbe) == 8) ? 8 : 4;
+            const size_t lds_s = ((size_t)p.nc * a.R * lds_row_stride(maxW) + kPadL + kPadR) * 4;
             dim3 g1((maxH + kStreamBand - 1) / kStreamBand, p.ntc / p.nc);
-            if (p.reversible) launch_l1s<true>(p.nc, cpt, g1, lds1, st, a);
-            else launch_l1s<false>(p.nc, cpt, g1, lds1, st, a);
+            if (p.reversible) launch_l1s<true>(p.nc, cpt, g1, lds_s, st, a);
+            else launch_l1s<false>(p.nc, cpt, g1, lds_s, st, a);
         } else if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
             dim3 g1((maxH + kRb1 - 1) / kRb1, p.ntc / p.nc);
             if (p.reversible) launch_l1<true>(p.nc, g1, lds1, st, a);

@@ -63,6 +63,7 @@ struct DwtLaunch {
     const uint64_t *strip_off;
     int rps, img_w, nc, bits, planar, big_endian, mct, spp_strips;
     int ntx, tile_w, tile_h, row0, plane_w, plane_h, ntc, levels, reversible;
+    int last_tile_w;  // width of the last tile column (the others are tile_w)
     const int32_t *tc_w, *tc_h;
     void *coef, *scratch0, *scratch1;  // scratch: ntc * ceil(plane_w/2) * ceil(plane_h/2) words each
 };

@@ -1246,6 +1246,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.planar = lay.planar; dl.big_endian = lay.big_endian; dl.mct = plan.rc.mct;
         dl.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
         dl.ntx = plan.ntx; dl.tile_w = plan.rc.tile_w; dl.tile_h = plan.rc.tile_h; dl.row0 = plan.row0;
+        dl.last_tile_w = plan.w - (plan.ntx - 1) * plan.rc.tile_w;
         dl.plane_w = plan.plane_w; dl.plane_h = plan.plane_h; dl.ntc = plan.ntc;
         dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
