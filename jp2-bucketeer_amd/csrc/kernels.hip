@@ -600,6 +600,11 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     uint64_t *B = a.bp + d.bp_off;
     uint64_t *S = B + (size_t)d.Mb * 64;
     uint64_t *SG = B + (size_t)2 * d.Mb * 64;
+    // the same masks transposed (column masks: lane c, bit y = row y), for
+    // the tier-1 context modelling: BT[p][c], ST[p][c], SGT[c]
+    uint64_t *BT = B + (size_t)(2 * d.Mb + 1) * 64;
+    uint64_t *ST = BT + (size_t)d.Mb * 64;
+    uint64_t *SGT = BT + (size_t)2 * d.Mb * 64;
     // Planes top-down, rows across the wave: for plane p, row y's mask of
     // columns with bit p set is one ballot, parked in lane y by writelane, so
     // after the 64 rows lane y holds B[p][y] and S[p][y] = S[p+1][y] | B[p][y]
@@ -619,6 +624,13 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             sg_hi = writelane<y>(sg_hi, (uint32_t)(m >> 32));
         });
         SG[lane] = ((uint64_t)sg_hi << 32) | sg_lo;
+        uint32_t t_lo = 0, t_hi = 0;
+#pragma unroll
+        for (int y = 0; y < 32; y++) {
+            t_lo |= (col[y] >> 31) << y;
+            t_hi |= (col[y + 32] >> 31) << y;
+        }
+        SGT[lane] = ((uint64_t)t_hi << 32) | t_lo;
     }
     // magnitudes only from here on (fewer live values in the plane loop)
 #pragma unroll
@@ -653,7 +665,8 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             const uint32_t lm = (1u << p) - 1u;
 #pragma unroll
             for (int y = 0; y < 64; y++) {
-                const uint32_t v = col[y];
+                uint32_t v = col[y];
+                asm volatile("" : "+v"(v));  // no common subexpressions with the ballot loop (register pressure)
                 const uint32_t hi = v >> p;
                 const int32_t l = (int32_t)(v & lm);
                 sv += hi == 1 ? (int32_t)v : 0;
@@ -707,6 +720,20 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             a.dsig[(size_t)b * 32 + p] = sig;
         }
         cnt_above = cS;
+    }
+    // the same masks transposed: this lane's column, bit y = bit p of row y
+    uint64_t colS = 0;
+    for (int p = P - 1; p >= 0; p--) {
+        uint32_t c_lo = 0, c_hi = 0;
+#pragma unroll
+        for (int y = 0; y < 32; y++) {
+            c_lo |= __builtin_amdgcn_ubfe(col[y], (uint32_t)p, 1u) << y;
+            c_hi |= __builtin_amdgcn_ubfe(col[y + 32], (uint32_t)p, 1u) << y;
+        }
+        const uint64_t colB = ((uint64_t)c_hi << 32) | c_lo;
+        colS |= colB;
+        BT[(size_t)p * 64 + lane] = colB;
+        ST[(size_t)p * 64 + lane] = colS;
     }
 }
 
@@ -979,7 +1006,7 @@ GpuEncoder::~GpuEncoder() {
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwtab, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
-                     &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d};
+                     &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d, &cmcensus};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -1365,6 +1392,12 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ca.counts = (uint4 *)counts.ptr;
     ca.dspp = (int64_t *)dspp.ptr;
     ca.lossless = plan.rc.reversible;
+    ca.census = nullptr;
+    if (dd) {
+        if (!ensure<unsigned long long>(cmcensus, 8, err)) return false;
+        HIPCHECK(hipMemsetAsync(cmcensus.ptr, 0, 8 * sizeof(unsigned long long), stream));
+        ca.census = (unsigned long long *)cmcensus.ptr;
+    }
     for (int r = 0; r < nrep_cm; r++) launch_t1_cm(ca, stream);
     HIPCHECK(hipGetLastError());
     // MQ lane order: blocks by decreasing decision count
@@ -1484,6 +1517,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!dump(dd, "dsig.bin", dsig, (size_t)nb * 32 * 8, err)) return false;
         if (!dump(dd, "bp.bin", bp, plan.bp_words * 8, err)) return false;
         if (!dump(dd, "mqdbg.bin", dbgbuf, (size_t)nb * 4 * 8, err)) return false;
+        if (!dump(dd, "cmcensus.bin", cmcensus, 8 * 8, err)) return false;
     }
     // no host wait: tier-1 totals and the overflow flag reach the host with
     // the first tier-2 summary (t2_size), stage times via collect_profile()

@@ -22,6 +22,8 @@
 // oracle_t1_encode); the parity tests compare them byte for byte.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device_common.h"
 #include "gpu_encoder.h"
 
@@ -212,15 +214,25 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
     const RowV S2v = rowv(inr && has2 ? SP[(size_t)(p + 2) * 64 + lane] : 0ull);
     const RowV SGv = rowv(inr ? SGp[lane] : 0ull);
     RowV Nv = {0u, 0u};
+    // quiet stripes: rows (bit r) with anything significant at planes >= p
+    // (M0) and > p (M1).  A stripe whose 6-row window r0-1 .. r0+4 is empty
+    // in M1 has no SPP candidate (unless the stripe above just gained
+    // significance) and no refinement; one empty in M0 codes only run-length
+    // "0" decisions in the cleanup pass -- both without the mask algebra.
+    const uint64_t M0 = __ballot(inr && (S0v.lo | S0v.hi) != 0u);
+    const uint64_t M1 = __ballot(inr && (S1v.lo | S1v.hi) != 0u);
+    auto win6 = [](uint64_t M, int r0) { return r0 == 0 ? (M & 0x1Full) : ((M >> (r0 - 1)) & 0x3Full); };
     uint8_t *out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
     int64_t dspp = 0;
     int n_spp = 0, n_mrp = 0, pos = 0;
     const bool spp = p < P - 1;
+    uint64_t tc0 = a.census ? clock64() : 0, tc1 = tc0, tc2 = tc0;
     if (spp) {
         // ---------------- significance propagation ----------------
         uint64_t nprev = 0;
         for (int s = 0; s < nstripes; s++) {
             const int r0 = s * 4, nr = min(4, h - r0);
+            if (nprev == 0 && win6(M1, r0) == 0) continue;  // quiet: no candidate, N stays 0
             uint64_t s1[6], sg[6], bt[4], n[4] = {0, 0, 0, 0}, mem[4];
             ROWS6(s1, S1v);
             ROWS6(sg, SGv);
@@ -267,10 +279,12 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
         }
         n_spp = pos;
         pos = pad_pass(out, pos, lane);
+        if (a.census) tc1 = clock64();
         const int mrp0 = pos;
         // ---------------- magnitude refinement ----------------
         for (int s = 0; s < nstripes; s++) {
             const int r0 = s * 4, nr = min(4, h - r0);
+            if (((M1 >> r0) & 0xFull) == 0) continue;  // nothing to refine
             uint64_t post[6], bt[4], mem[4], fr[4];
 #pragma unroll
             for (int i = 0; i < 6; i++) post[i] = row(S1v, r0 - 1 + i, h) | row(Nv, r0 - 1 + i, h);
@@ -294,10 +308,17 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
         n_mrp = pos - mrp0;
         pos = pad_pass(out, pos, lane);
     }
+    if (a.census) tc2 = clock64();
     const int cup0 = pos;
     // ---------------- cleanup ----------------
     for (int s = 0; s < nstripes; s++) {
         const int r0 = s * 4, nr = min(4, h - r0);
+        if (nr == 4 && win6(M0, r0) == 0) {
+            // quiet: every column is one run-length decision "0"
+            if (lane < w) out[pos + lane] = (uint8_t)(CX_RL << 1);
+            pos += w;
+            continue;
+        }
         uint64_t s1[6], post[6], s0[6], sg[6], bt[4], mem[4];
         ROWS6(s1, S1v);
 #pragma unroll
@@ -367,6 +388,16 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
     }
     const int n_cup = pos - cup0;
     pad_pass(out, pos, lane);
+    if (a.census && lane == 0) {  // debug: shader cycles per pass, summed over items
+        const uint64_t tc3 = clock64();
+        atomicAdd(&a.census[0], (unsigned long long)(spp ? tc1 - tc0 : 0));
+        atomicAdd(&a.census[1], (unsigned long long)(spp ? tc2 - tc1 : 0));
+        atomicAdd(&a.census[2], (unsigned long long)(tc3 - tc2));
+        atomicAdd(&a.census[3], 1ull);
+        atomicAdd(&a.census[4], (unsigned long long)n_spp);
+        atomicAdd(&a.census[5], (unsigned long long)n_mrp);
+        atomicAdd(&a.census[6], (unsigned long long)n_cup);
+    }
     if (spp) {
         // SPP distortion decrease: lane r sums its row's newly significant
         // samples (the sign-magnitude words are read only here)
@@ -384,6 +415,292 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
     dspp = wave_sum64(dspp);
     if (lane == 0) {
         uint4 cnt;  // decisions per pass; pass streams start at 16-byte boundaries
+        cnt.x = (uint32_t)n_spp;
+        cnt.y = (uint32_t)n_mrp;
+        cnt.z = (uint32_t)n_cup;
+        cnt.w = 0;
+        a.counts[(size_t)b * 32 + k] = cnt;
+        a.dspp[(size_t)b * 32 + k] = dspp;
+    }
+}
+
+// --------------------------------------------------------------------------
+// Context modelling on column masks (k_t1_cm2; the default).  Same items,
+// same decision streams as k_t1_cm, computed in the transposed layout: lane
+// c holds column c of every mask as a 64-bit word (bit r = row r; k_quant
+// writes them), so a vertical neighbour is a bit shift inside the lane and a
+// horizontal one is the next lane.  The neighbourhood and context rules then
+// run once per (block, plane) for all 64 rows at a time, bit-sliced (a
+// context number as four masks), instead of once per sample; per stripe a
+// lane only picks its four rows' bits and writes its decision bytes.
+//
+// Causal states, as in k_t1_cm: a neighbour already visited in the scan
+// (stripe by stripe, column by column, top to bottom) is seen in the state
+// Vb, one not yet visited in Va -- SPP: Vb = S[p+1] | N, Va = S[p+1];
+// CUP: Vb = S[p], Va = S[p+1] | N.  For row r, column c: (r-1, c), (r, c-1),
+// (r-1, c-1) are visited; (r+1, c), (r, c+1), (r+1, c+1) are not; (r-1, c+1)
+// is visited only when r starts a stripe, (r+1, c-1) only when it does not
+// end one.
+// --------------------------------------------------------------------------
+constexpr uint64_t kStripeTop = 0x1111111111111111ull;  // rows with r % 4 == 0
+constexpr uint64_t kStripeBot = 0x8888888888888888ull;  // rows with r % 4 == 3
+
+__device__ __forceinline__ uint64_t col_left(uint64_t x, int lane) {  // column c-1's word
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, 1, 64);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), 1, 64);
+    return lane == 0 ? 0ull : (((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint64_t col_right(uint64_t x, int lane) {  // column c+1's word
+    const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)x, 1, 64);
+    const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(x >> 32), 1, 64);
+    return lane == 63 ? 0ull : (((uint64_t)hi << 32) | lo);
+}
+
+// The 8 neighbour masks of every row of the lane's column under (Vb, Va).
+struct Nbr8 {
+    uint64_t UL, U, UR, L, R, DL, D, DR;
+};
+__device__ __forceinline__ Nbr8 nbr8(uint64_t Vb, uint64_t Va, uint64_t LVb, uint64_t RVb, uint64_t LVa,
+                                     uint64_t RVa) {
+    Nbr8 n;
+    n.UL = LVb << 1;
+    n.U = Vb << 1;
+    n.UR = ((RVb << 1) & kStripeTop) | ((RVa << 1) & ~kStripeTop);
+    n.L = LVb;
+    n.R = RVa;
+    n.DL = ((LVa >> 1) & kStripeBot) | ((LVb >> 1) & ~kStripeBot);
+    n.D = Va >> 1;
+    n.DR = RVa >> 1;
+    return n;
+}
+
+// Zero-coding context (Table D.1, zc_ctx) of every row, as 4 bit masks.
+struct Ctx4 {
+    uint64_t b0, b1, b2, b3;
+};
+__device__ __forceinline__ Ctx4 zc_masks(int band, const Nbr8 &n) {
+    const uint64_t s1x = n.UL ^ n.UR, s1a = n.UL & n.UR, s2x = n.DL ^ n.DR, s2a = n.DL & n.DR;
+    const uint64_t dge1 = s1x | s1a | s2x | s2a;
+    const uint64_t dge2 = s1a | s2a | (s1x & s2x);
+    uint64_t I1, I2, I3, I4, I5, I6, I7, I8;
+    if (band == 3) {
+        const uint64_t dge3 = (s1a & (s2x | s2a)) | (s2a & (s1x | s1a));
+        const uint64_t hvge1 = n.L | n.R | n.U | n.D;
+        const uint64_t hvge2 = (n.L & n.R) | (n.U & n.D) | ((n.L ^ n.R) & (n.U ^ n.D));
+        const uint64_t hv1 = hvge1 & ~hvge2;
+        const uint64_t d2 = dge2 & ~dge3, d1 = dge1 & ~dge2, d0 = ~dge1;
+        I8 = dge3;
+        I7 = d2 & hvge1;
+        I6 = d2 & ~hvge1;
+        I5 = d1 & hvge2;
+        I4 = d1 & hv1;
+        I3 = d1 & ~hvge1;
+        I2 = d0 & hvge2;
+        I1 = d0 & hv1;
+    } else {
+        // h: horizontal neighbours, v: vertical (swapped for the HL band)
+        const uint64_t A1 = band == 1 ? n.U : n.L, A2 = band == 1 ? n.D : n.R;
+        const uint64_t B1 = band == 1 ? n.L : n.U, B2 = band == 1 ? n.R : n.D;
+        const uint64_t h2 = A1 & A2, h1 = A1 ^ A2, h0 = ~(A1 | A2);
+        const uint64_t vge1 = B1 | B2, v2 = B1 & B2, v1 = B1 ^ B2;
+        I8 = h2;
+        I7 = h1 & vge1;
+        I6 = h1 & ~vge1 & dge1;
+        I5 = h1 & ~vge1 & ~dge1;
+        I4 = h0 & v2;
+        I3 = h0 & v1;
+        I2 = h0 & ~vge1 & dge2;
+        I1 = h0 & ~vge1 & dge1 & ~dge2;
+    }
+    Ctx4 z;
+    z.b0 = I1 | I3 | I5 | I7;
+    z.b1 = I2 | I3 | I6 | I7;
+    z.b2 = I4 | I5 | I6 | I7;
+    z.b3 = I8;
+    return z;
+}
+
+// Sign-coding context (Tables D.2/D.3, sc_lut) of every row: context 9..13
+// (bit 3 always set) in b0..b2 and the XOR bit.
+struct Sc4 {
+    uint64_t b0, b1, b2, xr;
+};
+__device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, uint64_t Rn, uint64_t Us, uint64_t Un,
+                                        uint64_t Ds, uint64_t Dn) {
+    const uint64_t pL = Ls & ~Ln, nL = Ls & Ln, pR = Rs & ~Rn, nR = Rs & Rn;
+    const uint64_t pU = Us & ~Un, nU = Us & Un, pD = Ds & ~Dn, nD = Ds & Dn;
+    const uint64_t hp = (pL & pR) | ((pL | pR) & ~(nL | nR));
+    const uint64_t hn = (nL & nR) | ((nL | nR) & ~(pL | pR));
+    const uint64_t vp = (pU & pD) | ((pU | pD) & ~(nU | nD));
+    const uint64_t vn = (nU & nD) | ((nU | nD) & ~(pU | pD));
+    const uint64_t hz = ~(hp | hn), vz = ~(vp | vn);
+    const uint64_t I13 = (hp & vp) | (hn & vn), I12 = (hp | hn) & vz, I11 = (hp & vn) | (hn & vp);
+    const uint64_t I9 = hz & vz, I10 = hz & (vp | vn);
+    Sc4 c;
+    c.b0 = I9 | I11 | I13;
+    c.b1 = I10 | I11;
+    c.b2 = I12 | I13;
+    c.xr = hn | (hz & vn);
+    return c;
+}
+
+// per stripe: a mask's bits of rows 4s .. 4s+3 at bits 0..3
+__device__ __forceinline__ uint32_t nib4(uint64_t m, int sh) { return (uint32_t)(m >> sh) & 0xFu; }
+__device__ __forceinline__ uint32_t bitq(uint32_t x, int q) { return (x >> q) & 1u; }
+
+__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm2(T1CmArgs a) {
+    if ((int)blockIdx.x * kCmWaves >= *a.nitems) return;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gi = blockIdx.x * kCmWaves + wv;
+    if (gi >= *a.nitems) return;
+    const int2 item = a.items[gi];
+    const int b = item.x, p = item.y;
+    const BlockDesc d = a.blocks[b];
+    const int P = a.P[b];
+    const int k = P - 1 - p;
+    const bool lossless = a.lossless != 0;
+    const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
+    const bool vl = lane < w;
+    const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;  // this column's rows
+    const uint64_t *CT = a.bp + d.bp_off + (size_t)(2 * Mb + 1) * 64;      // column masks
+    const uint64_t B = vl ? CT[(size_t)p * 64 + lane] : 0ull;
+    const uint64_t S0 = vl ? CT[(size_t)(Mb + p) * 64 + lane] : 0ull;
+    const uint64_t S1 = (vl && p + 1 < P) ? CT[(size_t)(Mb + p + 1) * 64 + lane] : 0ull;
+    const uint64_t S2 = (vl && p + 2 < P) ? CT[(size_t)(Mb + p + 2) * 64 + lane] : 0ull;
+    const uint64_t SG = vl ? CT[(size_t)2 * Mb * 64 + lane] : 0ull;
+    const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
+    const int nstripes = (h + 3) >> 2;
+    uint8_t *out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
+    int n_spp = 0, n_mrp = 0, pos = 0;
+    const bool spp = p < P - 1;
+    const uint64_t LS1 = col_left(S1, lane), RS1 = col_right(S1, lane);
+    uint64_t N = 0, memS = 0;
+    if (spp) {
+        // ---- significance propagation: least fixed point of the causal rule ----
+        for (;;) {
+            const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
+            const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
+            const uint64_t cand = ~S1 & VR & (nb.UL | nb.U | nb.UR | nb.L | nb.R | nb.DL | nb.D | nb.DR);
+            const uint64_t Nn = cand & B;
+            if (!__any(Nn != N)) {
+                memS = cand;
+                break;
+            }
+            N = Nn;
+        }
+        const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
+        const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
+        const Ctx4 z = zc_masks(band, nb);
+        // sign: L (visited) in Vb, R (not) in Va = S1, U in Vb, D in S1
+        const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
+        for (int s = 0; s < nstripes; s++) {
+            const int sh = s * 4;
+            const uint32_t mem = nib4(memS, sh);
+            LaneDec e{0, 0, 0};
+            if (mem) {
+                const uint32_t bb = nib4(B, sh), z0 = nib4(z.b0, sh), z1 = nib4(z.b1, sh), z2 = nib4(z.b2, sh),
+                               z3 = nib4(z.b3, sh), c0 = nib4(sc.b0, sh), c1 = nib4(sc.b1, sh),
+                               c2 = nib4(sc.b2, sh), xr = nib4(sc.xr, sh), sg = nib4(SG, sh);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (!bitq(mem, q)) continue;
+                    const uint32_t bv = bitq(bb, q);
+                    e.put(bitq(z0, q) | (bitq(z1, q) << 1) | (bitq(z2, q) << 2) | (bitq(z3, q) << 3), bv);
+                    if (bv) e.put(8u | bitq(c0, q) | (bitq(c1, q) << 1) | (bitq(c2, q) << 2), bitq(sg ^ xr, q));
+                }
+            }
+            if (__any(e.n)) pos += flush_stripe(out, pos, e, lane);
+        }
+        n_spp = pos;
+        pos = pad_pass(out, pos, lane);
+        const int mrp0 = pos;
+        // ---- magnitude refinement: neighbours in the post-SPP state ----
+        const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
+        const uint64_t anyn = (Pst << 1) | (Pst >> 1) | LP | RP | (LP << 1) | (RP << 1) | (LP >> 1) | (RP >> 1);
+        const uint64_t memM = S1 & VR, fr = S1 & ~S2;
+        for (int s = 0; s < nstripes; s++) {
+            const int sh = s * 4;
+            const uint32_t mem = nib4(memM, sh);
+            LaneDec e{0, 0, 0};
+            if (mem) {
+                const uint32_t bb = nib4(B, sh), f = nib4(fr, sh), an = nib4(anyn, sh);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (!bitq(mem, q)) continue;
+                    const uint32_t ctx = bitq(f, q) ? (bitq(an, q) ? 15u : 14u) : 16u;
+                    e.put(ctx, bitq(bb, q));
+                }
+            }
+            if (__any(e.n)) pos += flush_stripe(out, pos, e, lane);
+        }
+        n_mrp = pos - mrp0;
+        pos = pad_pass(out, pos, lane);
+    }
+    const int cup0 = pos;
+    // ---- cleanup: visited neighbours in S[p], the others post-SPP ----
+    {
+        const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
+        const uint64_t LS0 = col_left(S0, lane), RS0 = col_right(S0, lane);
+        const Nbr8 nb = nbr8(S0, Pst, LS0, RS0, LP, RP);
+        const Ctx4 z = zc_masks(band, nb);
+        const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
+        const uint64_t memC = ~S1 & ~memS & VR;
+        // run-length: four members and no significant neighbour -- left
+        // column (visited) in S[p], right column post-SPP, the row above in
+        // S[p], the row below post-SPP
+        const uint64_t side = LS0 | RP, above = S0 | LS0 | RS0, below = Pst | LP | RP;
+        for (int s = 0; s < nstripes; s++) {
+            const int sh = s * 4, nr = min(4, h - sh);
+            const uint32_t mem = nib4(memC, sh);
+            LaneDec e{0, 0, 0};
+            if (mem) {
+                const uint32_t bb = nib4(B, sh), z0 = nib4(z.b0, sh), z1 = nib4(z.b1, sh), z2 = nib4(z.b2, sh),
+                               z3 = nib4(z.b3, sh), c0 = nib4(sc.b0, sh), c1 = nib4(sc.b1, sh),
+                               c2 = nib4(sc.b2, sh), xr = nib4(sc.xr, sh), sg = nib4(SG, sh);
+                int qstart = 0;
+                const bool rl = nr == 4 && mem == 0xFu && nib4(side, sh) == 0 &&
+                                (sh == 0 || ((above >> (sh - 1)) & 1ull) == 0) &&
+                                (sh + 4 >= 64 || ((below >> (sh + 4)) & 1ull) == 0);
+                if (rl) {
+                    if (bb == 0) {
+                        e.put(CX_RL, 0);
+                        qstart = 4;
+                    } else {
+                        const int r = __builtin_ctz(bb);
+                        e.put(CX_RL, 1);
+                        e.put(CX_UNI, (uint32_t)r >> 1);
+                        e.put(CX_UNI, (uint32_t)r & 1u);
+                        e.put(8u | bitq(c0, r) | (bitq(c1, r) << 1) | (bitq(c2, r) << 2), bitq(sg ^ xr, r));
+                        qstart = r + 1;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (q < qstart || !bitq(mem, q)) continue;
+                    const uint32_t bv = bitq(bb, q);
+                    e.put(bitq(z0, q) | (bitq(z1, q) << 1) | (bitq(z2, q) << 2) | (bitq(z3, q) << 3), bv);
+                    if (bv) e.put(8u | bitq(c0, q) | (bitq(c1, q) << 1) | (bitq(c2, q) << 2), bitq(sg ^ xr, q));
+                }
+            }
+            if (__any(e.n)) pos += flush_stripe(out, pos, e, lane);
+        }
+    }
+    const int n_cup = pos - cup0;
+    pad_pass(out, pos, lane);
+    int64_t dspp = 0;
+    if (spp && N) {  // SPP distortion decrease: this column's newly significant samples
+        const int32_t *SMc = a.sm + d.sm_off + lane;
+        uint64_t m = N;
+        while (m) {
+            const int r = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            dspp += dist_gain((uint32_t)SMc[(size_t)r * 64] & 0x7FFFFFFFu, p, lossless);
+        }
+    }
+    dspp = wave_sum64(dspp);
+    if (lane == 0) {
+        uint4 cnt;
         cnt.x = (uint32_t)n_spp;
         cnt.y = (uint32_t)n_mrp;
         cnt.z = (uint32_t)n_cup;
@@ -727,8 +1044,10 @@ void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, c
                               flags, pos, items, nitems);
 }
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
-    if (a.max_items)
-        hipLaunchKernelGGL(k_t1_cm, dim3((a.max_items + kCmWaves - 1) / kCmWaves), dim3(64 * kCmWaves), 0, st, a);
+    if (!a.max_items) return;
+    const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
+    if (getenv("JP2HIP_CM_ROWS")) hipLaunchKernelGGL(k_t1_cm, g, dim3(64 * kCmWaves), 0, st, a);  // row-mask variant
+    else hipLaunchKernelGGL(k_t1_cm2, g, dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
                     int32_t *vals, hipStream_t st) {
