@@ -22,7 +22,9 @@
 // oracle_t1_encode); the parity tests compare them byte for byte.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "device_common.h"
 #include "gpu_encoder.h"
@@ -711,6 +713,302 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm2(T1CmArgs a) {
 }
 
 // --------------------------------------------------------------------------
+// k_t1_cm3 (the default): the masks and contexts of k_t1_cm2, with a
+// branch-free stripe step and LDS-staged output.
+//
+// Per stripe a lane (column) builds its four rows' decision bytes at once,
+// one byte per row in a dword: the zero-coding byte (ctx << 1 | bit) and the
+// sign byte ((8 | ctx) << 1 | sign ^ xor) from the context masks' nibbles,
+// spread to byte lanes by one multiply (nibble * 0x204081 & 0x01010101).  The
+// member samples' bytes are compacted in scan order by two v_perm_b32 whose
+// selectors come from a 256-entry table indexed by (members | members with a
+// 1 bit << 4) -- no per-sample branch.  The wave's lanes place their <= 12
+// bytes at an exclusive prefix of the counts (ballots + mbcnt) in a 2 KB LDS
+// ring per wave, OR-ing whole dwords (the ring is zero where nothing has
+// been written, and a lane's bytes are zero-padded, so neighbours' partial
+// dwords merge); every full KiB leaves the ring in one 16-byte store per lane.
+// Items are taken in a grid-stride loop (the grid is sized to the chip, not
+// to the plan's item bound).
+// --------------------------------------------------------------------------
+constexpr int kRingBytes = 2048;
+constexpr int kCm3Blocks = 2048;  // workgroups (4 waves each) at most
+
+__device__ __forceinline__ uint32_t spread4(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
+// spread4(nib) << k, as one 24-bit multiply (k <= 4: nib << k < 2^24)
+__device__ __forceinline__ uint32_t spread4s(uint32_t nib, int k) {
+    return __umul24(nib << k, 0x00204081u) & (0x01010101u << k);
+}
+__device__ __forceinline__ uint32_t nibw(uint32_t w, int sh) { return __builtin_amdgcn_ubfe(w, (uint32_t)sh, 4u); }
+
+// Ring writer state (wave-uniform): `pos` = next byte of the plane's slot,
+// `fl` = bytes already stored to HBM (a multiple of 16).
+struct Ring {
+    uint32_t *r;  // this wave's ring (kRingBytes)
+    uint8_t *out;
+    int pos, fl;
+};
+
+// Place this lane's n bytes (o0, o1, o2 little-endian) at pos + its prefix;
+// returns the wave's total.
+__device__ __forceinline__ int ring_put(Ring &g, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t n, int lane) {
+    // inclusive scan over the wave: DPP row shifts 1, 2, 4, 8, then lane 15
+    // into 16..31 / 47 into 48..63 and lane 31 into 32..63
+    int v = (int)n;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    const int total = __builtin_amdgcn_readlane(v, 63);
+    const uint32_t at = (uint32_t)g.pos + (uint32_t)v - n;
+    const uint32_t s = (at & 3u) * 8u;
+    const uint64_t w01 = (((uint64_t)o1 << 32) | o0) << s;
+    const uint32_t w2 = (uint32_t)(((((uint64_t)o2 << 32) | o1) << s) >> 32);
+    const uint32_t w3 = (uint32_t)(((uint64_t)o2 << s) >> 32);
+    const uint32_t d = at >> 2;
+    constexpr uint32_t M = kRingBytes / 4 - 1;
+    if (n) {
+        atomicOr(&g.r[d & M], (uint32_t)w01);
+        atomicOr(&g.r[(d + 1) & M], (uint32_t)(w01 >> 32));
+        atomicOr(&g.r[(d + 2) & M], w2);
+        atomicOr(&g.r[(d + 3) & M], w3);
+    }
+    return total;
+}
+
+// Store ring bytes [fl, upto) (upto a multiple of 16) and zero them.
+__device__ __forceinline__ void ring_drain(Ring &g, int upto, int lane) {
+    for (int o = g.fl + 16 * lane; o < upto; o += 1024) {
+        uint4 *src = (uint4 *)((uint8_t *)g.r + (o & (kRingBytes - 1)));
+        const uint4 v = *src;
+        *src = make_uint4(0u, 0u, 0u, 0u);
+        *(uint4 *)(g.out + o) = v;
+    }
+    g.fl = upto;
+}
+
+// After a stripe: whole KiBs leave the ring (a stripe adds <= 768 bytes, so
+// at most 1792 are pending).
+__device__ __forceinline__ void ring_step(Ring &g, int lane) {
+    if (g.pos - g.fl >= 1024) ring_drain(g, g.fl + 1024, lane);
+}
+
+// Pass end: neutral decisions to the next 16-byte boundary, every byte out.
+__device__ __forceinline__ void ring_pass_end(Ring &g, int lane) {
+    const int end = (g.pos + 15) & ~15;
+    if (lane < end - g.pos) ((uint8_t *)g.r)[(g.pos + lane) & (kRingBytes - 1)] = kPadDecision;
+    ring_drain(g, end, lane);
+    g.pos = end;
+}
+
+// 32-bit halves of the masks a stripe step reads
+struct Half {
+    uint32_t mem, bb, z0, z1, z2, z3, c0, c1, c2, xs, x;
+};
+__device__ __forceinline__ Half half_of(int hf, uint64_t mem, uint64_t bb, const Ctx4 &z, const Sc4 &sc, uint64_t xs,
+                                        uint64_t x) {
+    const int sh = hf * 32;
+    return Half{(uint32_t)(mem >> sh),  (uint32_t)(bb >> sh),    (uint32_t)(z.b0 >> sh), (uint32_t)(z.b1 >> sh),
+                (uint32_t)(z.b2 >> sh), (uint32_t)(z.b3 >> sh),  (uint32_t)(sc.b0 >> sh), (uint32_t)(sc.b1 >> sh),
+                (uint32_t)(sc.b2 >> sh), (uint32_t)(xs >> sh), (uint32_t)(x >> sh)};
+}
+// the four rows' zero-coding bytes and sign bytes of a stripe
+__device__ __forceinline__ void zc_sg_bytes(const Half &m, int sh, uint32_t &zc, uint32_t &sg) {
+    zc = spread4s(nibw(m.bb, sh), 0) | spread4s(nibw(m.z0, sh), 1) | spread4s(nibw(m.z1, sh), 2) |
+         spread4s(nibw(m.z2, sh), 3) | spread4s(nibw(m.z3, sh), 4);
+    sg = 0x10101010u | spread4s(nibw(m.xs, sh), 0) | spread4s(nibw(m.c0, sh), 1) | spread4s(nibw(m.c1, sh), 2) |
+         spread4s(nibw(m.c2, sh), 3);
+}
+
+__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
+    __shared__ uint2 lut[256];
+    __shared__ uint32_t rings[kCmWaves][kRingBytes / 4];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // compaction selectors: entry K = members (bits 0-3) | members with a 1
+    // bit (bits 4-7); output byte order q = 0..3: zc byte q (selector q), then
+    // its sign byte (selector 4 + q); unused bytes select 0x00 (0x0C)
+    for (int K = threadIdx.x; K < 256; K += 64 * kCmWaves) {
+        uint32_t sel[8] = {12, 12, 12, 12, 12, 12, 12, 12};
+        int n = 0;
+        for (int q = 0; q < 4; q++) {
+            if ((K >> q) & 1) sel[n++] = (uint32_t)q;
+            if ((K >> (4 + q)) & 1) sel[n++] = 4u + (uint32_t)q;
+        }
+        lut[K] = make_uint2(sel[0] | sel[1] << 8 | sel[2] << 16 | sel[3] << 24,
+                            sel[4] | sel[5] << 8 | sel[6] << 16 | sel[7] << 24);
+    }
+    for (int i = threadIdx.x; i < kCmWaves * kRingBytes / 4; i += 64 * kCmWaves) (&rings[0][0])[i] = 0u;
+    __syncthreads();
+    const int nitems = *a.nitems;
+    Ring g;
+    g.r = rings[wv];
+    for (int gi = blockIdx.x * kCmWaves + wv; gi < nitems; gi += gridDim.x * kCmWaves) {
+        const int2 item = a.items[gi];
+        const int b = item.x, p = item.y;
+        const BlockDesc d = a.blocks[b];
+        const int P = a.P[b];
+        const int k = P - 1 - p;
+        const bool lossless = a.lossless != 0;
+        const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
+        const bool vl = lane < w;
+        const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;
+        const uint64_t *CT = a.bp + d.bp_off + (size_t)(2 * Mb + 1) * 64;
+        const uint64_t B = vl ? CT[(size_t)p * 64 + lane] : 0ull;
+        const uint64_t S0 = vl ? CT[(size_t)(Mb + p) * 64 + lane] : 0ull;
+        const uint64_t S1 = (vl && p + 1 < P) ? CT[(size_t)(Mb + p + 1) * 64 + lane] : 0ull;
+        const uint64_t S2 = (vl && p + 2 < P) ? CT[(size_t)(Mb + p + 2) * 64 + lane] : 0ull;
+        const uint64_t SG = vl ? CT[(size_t)2 * Mb * 64 + lane] : 0ull;
+        const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
+        const int nstripes = (h + 3) >> 2;
+        g.out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
+        g.pos = 0;
+        g.fl = 0;
+        int n_spp = 0, n_mrp = 0;
+        const bool spp = p < P - 1;
+        const uint64_t LS1 = col_left(S1, lane), RS1 = col_right(S1, lane);
+        uint64_t N = 0, memS = 0;
+        if (spp) {
+            // ---- significance propagation: least fixed point of the causal rule ----
+            for (;;) {
+                const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
+                const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
+                const uint64_t cand = ~S1 & VR & (nb.UL | nb.U | nb.UR | nb.L | nb.R | nb.DL | nb.D | nb.DR);
+                const uint64_t Nn = cand & B;
+                if (!__any(Nn != N)) {
+                    memS = cand;
+                    break;
+                }
+                N = Nn;
+            }
+            {
+                const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
+                const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
+                const Ctx4 z = zc_masks(band, nb);
+                const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
+                for (int hf = 0; hf * 8 < nstripes; hf++) {
+                    const Half m = half_of(hf, memS, B, z, sc, SG ^ sc.xr, 0);
+                    for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                        const int sh = s4 * 4;
+                        const uint32_t mem = nibw(m.mem, sh);
+                        if (!__any(mem)) continue;
+                        uint32_t zc, sg;
+                        zc_sg_bytes(m, sh, zc, sg);
+                        const uint32_t K = mem | ((mem & nibw(m.bb, sh)) << 4);
+                        const uint2 sel = lut[K];
+                        const uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
+                        g.pos += ring_put(g, o0, o1, 0u, (uint32_t)__popc(K), lane);
+                        ring_step(g, lane);
+                    }
+                }
+            }
+            n_spp = g.pos;
+            ring_pass_end(g, lane);
+            const int mrp0 = g.pos;
+            // ---- magnitude refinement: neighbours in the post-SPP state ----
+            {
+                const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
+                const uint64_t anyn = (Pst << 1) | (Pst >> 1) | LP | RP | (LP << 1) | (RP << 1) | (LP >> 1) | (RP >> 1);
+                const uint64_t memM = S1 & VR, fr = S1 & ~S2, fa = fr & anyn;
+                for (int hf = 0; hf * 8 < nstripes; hf++) {
+                    const int hs = hf * 32;
+                    const uint32_t wm = (uint32_t)(memM >> hs), wb = (uint32_t)(B >> hs), wf = (uint32_t)(fr >> hs),
+                                   wa = (uint32_t)(fa >> hs);
+                    for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                        const int sh = s4 * 4;
+                        const uint32_t mem = nibw(wm, sh);
+                        if (!__any(mem)) continue;
+                        // ctx 14 (first refinement), 15 (... with a significant
+                        // neighbour), 16 (later refinements): bytes 0x1C, 0x1E, 0x20
+                        const uint32_t f = spread4(nibw(wf, sh));
+                        const uint32_t mr = spread4(nibw(wb, sh)) | (f * 0x1Cu) | (spread4(nibw(wa, sh)) << 1) |
+                                            ((0x01010101u ^ f) << 5);
+                        const uint32_t o0 = __builtin_amdgcn_perm(0u, mr, lut[mem].x);
+                        g.pos += ring_put(g, o0, 0u, 0u, (uint32_t)__popc(mem), lane);
+                        ring_step(g, lane);
+                    }
+                }
+            }
+            n_mrp = g.pos - mrp0;
+            ring_pass_end(g, lane);
+        }
+        const int cup0 = g.pos;
+        // ---- cleanup: visited neighbours in S[p], the others post-SPP ----
+        {
+            const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
+            const uint64_t LS0 = col_left(S0, lane), RS0 = col_right(S0, lane);
+            const Nbr8 nb = nbr8(S0, Pst, LS0, RS0, LP, RP);
+            const Ctx4 z = zc_masks(band, nb);
+            const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
+            const uint64_t memC = ~S1 & ~memS & VR;
+            // run-length mode blocked by a significant neighbour: left column
+            // (visited) in S[p], right column post-SPP, the row above a stripe
+            // in S[p], the row below it post-SPP
+            const uint64_t side = LS0 | RP, above = S0 | LS0 | RS0, below = Pst | LP | RP;
+            const uint64_t blk = side | ((above << 1) & kStripeTop) | ((below >> 1) & kStripeBot);
+            for (int hf = 0; hf * 8 < nstripes; hf++) {
+                const Half m = half_of(hf, memC, B, z, sc, SG ^ sc.xr, blk);
+                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                    const int sh = s4 * 4;
+                    const uint32_t mem = nibw(m.mem, sh);
+                    if (!__any(mem)) continue;
+                    uint32_t zc, sg;
+                    zc_sg_bytes(m, sh, zc, sg);
+                    const uint32_t bb = nibw(m.bb, sh);
+                    // four members, none with a significant neighbour (mem ==
+                    // 0xF implies the stripe's four rows lie inside the block)
+                    const bool rl = mem == 0xFu && nibw(m.x, sh) == 0u;
+                    const uint32_t r = __builtin_ctz(bb | 16u);
+                    const uint32_t mr = rl ? (0xEu << r) & 0xFu : mem;  // samples coded normally
+                    const uint32_t K = mr | ((mr & bb) << 4);
+                    const uint2 sel = lut[K];
+                    uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
+                    uint32_t o2 = 0u;
+                    uint32_t n = (uint32_t)__popc(K);
+                    if (rl) {  // run-length prefix: RL 0 alone, or RL 1, two UNI bits, row r's sign
+                        if (bb == 0u) {
+                            o0 = (uint32_t)(CX_RL << 1);
+                            n = 1;
+                        } else {
+                            o2 = o1;
+                            o1 = o0;
+                            o0 = (uint32_t)((CX_RL << 1) | 1) | ((uint32_t)((CX_UNI << 1) | (r >> 1)) << 8) |
+                                 ((uint32_t)((CX_UNI << 1) | (r & 1u)) << 16) | (((sg >> (8 * r)) & 0xFFu) << 24);
+                            n += 4;
+                        }
+                    }
+                    g.pos += ring_put(g, o0, o1, o2, n, lane);
+                    ring_step(g, lane);
+                }
+            }
+        }
+        const int n_cup = g.pos - cup0;
+        ring_pass_end(g, lane);
+        int64_t dspp = 0;
+        if (spp && N) {  // SPP distortion decrease: this column's newly significant samples
+            const int32_t *SMc = a.sm + d.sm_off + lane;
+            uint64_t mm = N;
+            while (mm) {
+                const int rr = __ffsll((unsigned long long)mm) - 1;
+                mm &= mm - 1;
+                dspp += dist_gain((uint32_t)SMc[(size_t)rr * 64] & 0x7FFFFFFFu, p, lossless);
+            }
+        }
+        dspp = wave_sum64(dspp);
+        if (lane == 0) {
+            uint4 cnt;
+            cnt.x = (uint32_t)n_spp;
+            cnt.y = (uint32_t)n_mrp;
+            cnt.z = (uint32_t)n_cup;
+            cnt.w = 0;
+            a.counts[(size_t)b * 32 + k] = cnt;
+            a.dspp[(size_t)b * 32 + k] = dspp;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // MQ coder
 // --------------------------------------------------------------------------
 __constant__ uint16_t c_qe[47] = {
@@ -1046,8 +1344,10 @@ void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, c
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (!a.max_items) return;
     const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
-    if (getenv("JP2HIP_CM_ROWS")) hipLaunchKernelGGL(k_t1_cm, g, dim3(64 * kCmWaves), 0, st, a);  // row-mask variant
-    else hipLaunchKernelGGL(k_t1_cm2, g, dim3(64 * kCmWaves), 0, st, a);
+    static const char *v = getenv("JP2HIP_CM");  // experiment knob: "rows" / "2" = earlier variants
+    if (v && !strcmp(v, "rows")) hipLaunchKernelGGL(k_t1_cm, g, dim3(64 * kCmWaves), 0, st, a);
+    else if (v && !strcmp(v, "2")) hipLaunchKernelGGL(k_t1_cm2, g, dim3(64 * kCmWaves), 0, st, a);
+    else hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
                     int32_t *vals, hipStream_t st) {
