@@ -4,9 +4,10 @@
 Workload (BASELINE.json configs[1], "C2"): a 6000x4000 8-bit RGB TIFF,
 lossy 9/7 at 3 bpp with the Bucketeer/Kakadu recipe (6 levels, 6 layers, 512^2
 tiles, 64^2 blocks, RPCL, SOP/EPH/PLT, tile-parts per resolution), JPX out.
-One step = one full encode of one image per GPU: TIFF strips already resident
-in HBM -> JPX bytes in host memory (ingest, DWT, quantiser, tier-1, PCRD,
-tier-2).  Images are independent, so N GPUs run N replicas (weak scaling,
+One step = one batch of full encodes per GPU (--batch images, default one per
+in-flight context, 16): TIFF strips already resident in HBM -> JPX bytes in
+host memory (ingest, DWT, quantiser, tier-1, PCRD, tier-2) for every image of
+the batch; value = megapixels of every image encoded / timed seconds.  Images are independent, so N GPUs run N replicas (weak scaling,
 no collective on the data path); the barrier/max are only for timing.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -217,9 +218,11 @@ def run(args):
     # context (own HIP stream and buffers): the batch path's per-GPU queue.
     # Steps are spread evenly over the contexts (no context does an extra
     # image after the others have drained).
-    nf = max(1, min(args.inflight, args.steps))
-    rounds = -(-args.steps // nf)
-    nf = -(-args.steps // rounds)
+    # a step is one batch of `batch` images (default: one per in-flight
+    # context), spread over the contexts from a shared counter
+    nf = max(1, args.inflight)
+    batch = max(1, args.batch or nf)
+    total = args.steps * batch
     host_threads = max(2, 16 // nf)
     encs = [jp2hip.Encoder(local, host_threads=host_threads, profile=True) for _ in range(nf)]
     rc = jp2hip.recipe(jp2hip.LOSSY)
@@ -251,7 +254,7 @@ def run(args):
                     with mu:
                         step = nxt[0]
                         nxt[0] += 1
-                    if step >= args.steps:
+                    if step >= total:
                         return
                     _, st = encode(encs[k])
                     with mu:
@@ -278,7 +281,7 @@ def run(args):
     dt, stages = timed(lambda e: e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc))
     dt_max = barrier_max(world, dt, device)
     mp = img.shape[0] * img.shape[1] / 1e6
-    value = world * mp * args.steps / dt_max
+    value = world * mp * total / dt_max
     # PCIe-inclusive: TIFF bytes in pinned host memory -> jp2hip_encode_tiff
     # (header parse, H2D of the 72 MB file, encode) -> JPX bytes in host memory
     dt_h, _ = timed(lambda e: e.encode_tiff_ptr(h_src.data_ptr(), h_src.numel(), jp2hip.LOSSY, rc))
@@ -311,11 +314,13 @@ def run(args):
         res = {
             "metric": METRIC, "value": round(value, 3), "unit": "MP/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 3),
+            "images_per_step": batch,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+i32",
             "data": "synthetic (sinusoids + checker + N(0,6) noise, seed 1234+rank), in-memory baseline TIFF",
             "config": {"workload": "C2: 6000x4000 RGB8 TIFF -> JPX, lossy 9/7 3 bpp, Kakadu recipe "
                                    "(6 levels, 6 layers, 512^2 tiles, 64^2 blocks, RPCL, SOP/EPH/PLT, TP=R)",
-                       "image": "6000x4000x3 u8", "images_in_flight_per_gpu": nf, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "image": "6000x4000x3 u8", "step": f"one batch of {batch} C2 images per GPU",
+                       "images_per_step": batch, "images_in_flight_per_gpu": nf, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "timed_span": "TIFF resident in HBM -> JPX bytes in host memory (jp2hip_encode_device)",
                        "parallelism": f"replicas x{world}", "out_bytes": int(avg["out_bytes"]),
                        "bpp": round(8 * avg["out_bytes"] / npx, 4),
@@ -324,7 +329,7 @@ def run(args):
                        "rate_iterations": int(max(a["rate_iterations"] for a in alone))},
             # the same steps with the TIFF in pinned host memory and the H2D
             # inside the timed span (PCIe-inclusive rate)
-            "value_pcie_inclusive": {"value": round(world * mp * args.steps / dt_h_max, 3), "unit": "MP/s",
+            "value_pcie_inclusive": {"value": round(world * mp * total / dt_h_max, 3), "unit": "MP/s",
                                      "ms_per_step": round(dt_h_max * 1e3 / args.steps, 3),
                                      "timed_span": "TIFF bytes in pinned host memory -> jp2hip_encode_tiff (parse, "
                                                    "H2D, encode) -> JPX bytes in host memory"},
@@ -539,10 +544,12 @@ def run_c5(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inflight", type=int, default=int(os.environ.get("JP2HIP_INFLIGHT", "12")),
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("JP2HIP_INFLIGHT", "16")),
                     help="independent images in flight per GPU (separate contexts/streams)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="images per step (default: --inflight); value = MP of every image / time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lossless", action="store_true")
     ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",

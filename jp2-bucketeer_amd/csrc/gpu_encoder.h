@@ -36,7 +36,6 @@ struct T1CmArgs {
     uint4 *counts;    // [block][32] (end of SPP, end of MRP, end of CUP)
     int64_t *dspp;    // [block][32]
     int lossless;
-    unsigned long long *census;  // debug (JP2HIP_DUMP_DIR): cycles per pass, items, decisions per pass [7]
 };
 struct T1MqArgs {
     const BlockDesc *blocks;
@@ -170,7 +169,7 @@ class GpuEncoder {
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
         est, hist, kcut, pmin, mqspan, stage, soff, lzwtab, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
-        dbgbuf, t1ord, t1flags, t1pos, slotbytes, nitems_d, cmcensus;
+        dbgbuf, t1ord, t1flags, t1pos, slotbytes, nitems_d;
     // device tier-2 (t2_device.hip)
     DevBuf hdist, rstate;
     RateState *h_rs = nullptr;  // pinned

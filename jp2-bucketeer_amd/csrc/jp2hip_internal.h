@@ -41,8 +41,8 @@ struct BlockDesc {
     int8_t pad0, pad1;
     float inv_delta;    // irreversible quantiser reciprocal
     uint32_t pad2;
-    uint64_t bp_off;    // bit-plane storage offset, in uint64 words: (2Mb+1)*64 row masks, then
-                        // (2Mb+1)*64 column masks (kernels.hip k_quant)
+    uint64_t bp_off;    // bit-plane storage offset, in uint64 words: (2Mb+1)*64 column masks
+                        // (kernels.hip k_quant)
     uint64_t sm_off;    // sign-magnitude storage offset, in int32 words
     uint64_t out_off;   // tier-1 output offset, bytes
     uint32_t out_cap;   // tier-1 output capacity, bytes

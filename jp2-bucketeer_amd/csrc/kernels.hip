@@ -528,8 +528,8 @@ __global__ void __launch_bounds__(256) k_untile(const uint8_t *base, const uint6
 
 // --------------------------------------------------------------------------
 // S4: quantisation + bit-planes.  One wavefront per code-block; lane = column.
-// Layout per block (uint64 words): B[p][64 rows] for p < Mb, then
-// S[p][64 rows] = OR_{q>=p} B[q], then sign[64 rows].
+// Layout per block (uint64 words, lane c = column c, bit y = row y): B[p][64]
+// for p < Mb, then S[p][64] = OR_{q>=p} B[q], then sign[64].
 // --------------------------------------------------------------------------
 struct QuantArgs {
     const BlockDesc *blocks;
@@ -540,25 +540,12 @@ struct QuantArgs {
     uint8_t *P;
     int64_t *dref, *dsig;  // [block][32]
     uint32_t *est;         // [block][32] predicted coded size of plane p, 1/16 bit
+    int max_mb;            // largest Mb of the plan (LDS: max_mb * 512 bytes)
 };
-
-// v_writelane_b32 (the LLVM intrinsic, so the compiler pads the VALU-SGPR
-// hazard after the ballot): lane `L` of `old` takes the wave-uniform `v`
-__device__ int amdgcn_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
-template <int L>
-__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v) {
-    return (uint32_t)amdgcn_writelane((int)v, L, (int)old);
-}
-template <int Y, typename F>
-__device__ __forceinline__ void unroll_rows(F &&f) {
-    if constexpr (Y < 64) {
-        f(std::integral_constant<int, Y>{});
-        unroll_rows<Y + 1>(f);
-    }
-}
 
 template <bool REV>
 __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
+    extern __shared__ uint64_t planes[];  // [plane][lane], a.max_mb planes
     int b = blockIdx.x;
     BlockDesc d = a.blocks[b];
     int lane = threadIdx.x;
@@ -597,33 +584,13 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
     // the wave-reduced maximum is uniform: keep P (and the plane loop) scalar
     const int P = __builtin_amdgcn_readfirstlane(vmax ? 32 - __clz(vmax) : 0);
     if (lane == 0) a.P[b] = (uint8_t)P;
-    uint64_t *B = a.bp + d.bp_off;
-    uint64_t *S = B + (size_t)d.Mb * 64;
-    uint64_t *SG = B + (size_t)2 * d.Mb * 64;
-    // the same masks transposed (column masks: lane c, bit y = row y), for
-    // the tier-1 context modelling: BT[p][c], ST[p][c], SGT[c]
-    uint64_t *BT = B + (size_t)(2 * d.Mb + 1) * 64;
+    // column masks (lane c, bit y = row y): BT[p][c] = bit p of the
+    // column, ST[p][c] = OR of BT[q], q >= p, then the sign column SGT[c] --
+    // the layout the tier-1 context modelling reads (t1.hip k_t1_cm3)
+    uint64_t *BT = a.bp + d.bp_off;
     uint64_t *ST = BT + (size_t)d.Mb * 64;
     uint64_t *SGT = BT + (size_t)2 * d.Mb * 64;
-    // Planes top-down, rows across the wave: for plane p, row y's mask of
-    // columns with bit p set is one ballot, parked in lane y by writelane, so
-    // after the 64 rows lane y holds B[p][y] and S[p][y] = S[p+1][y] | B[p][y]
-    // and each plane leaves in two coalesced 512-byte stores.  The plane's
-    // slope-prediction counts (oracle plane_stats: significant samples, and
-    // insignificant samples with a significant 8-neighbour) and its exact
-    // distortion decreases (MRP: samples significant above p; significance:
-    // samples whose top bit is p) come from the same pass.
-    const uint64_t wmask = d.w >= 64 ? ~0ull : ((1ull << d.w) - 1ull);
-    auto dil = [](uint64_t m) { return m | (m << 1) | (m >> 1); };
     {
-        uint32_t sg_lo = 0, sg_hi = 0;
-        unroll_rows<0>([&](auto yc) {
-            constexpr int y = decltype(yc)::value;
-            const uint64_t m = __ballot(col[y] >> 31);
-            sg_lo = writelane<y>(sg_lo, (uint32_t)m);
-            sg_hi = writelane<y>(sg_hi, (uint32_t)(m >> 32));
-        });
-        SG[lane] = ((uint64_t)sg_hi << 32) | sg_lo;
         uint32_t t_lo = 0, t_hi = 0;
 #pragma unroll
         for (int y = 0; y < 32; y++) {
@@ -632,45 +599,50 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
         }
         SGT[lane] = ((uint64_t)t_hi << 32) | t_lo;
     }
-    // magnitudes only from here on (fewer live values in the plane loop)
+    // magnitudes only from here on
 #pragma unroll
-    for (int y = 0; y < 64; y++) {
-        col[y] &= 0x7FFFFFFFu;
-        asm volatile("" : "+v"(col[y]));  // the signed copies die here
+    for (int y = 0; y < 64; y++) col[y] &= 0x7FFFFFFFu;
+    // every plane's column mask, kept in LDS for the distortion sums below
+    for (int p = 0; p < P; p++) {
+        uint32_t c_lo = 0, c_hi = 0;
+#pragma unroll
+        for (int y = 0; y < 32; y++) {
+            c_lo |= __builtin_amdgcn_ubfe(col[y], (uint32_t)p, 1u) << y;
+            c_hi |= __builtin_amdgcn_ubfe(col[y + 32], (uint32_t)p, 1u) << y;
+        }
+        const uint64_t m = ((uint64_t)c_hi << 32) | c_lo;
+        planes[p * 64 + lane] = m;
+        BT[(size_t)p * 64 + lane] = m;
     }
     constexpr bool lossless = REV;
     constexpr int dd = lossless ? 0 : 1;  // reconstruction offset, half-units
-    uint64_t rowS = 0;
-    uint32_t cnt_above = 0;  // |S[p+1]|
+    const uint64_t hmask = d.h >= 64 ? ~0ull : ((1ull << d.h) - 1ull);
+    const bool wcol = lane < d.w;
+    uint64_t colS = 0;       // S[p+1] of this column
+    uint32_t cnt_above = 0;  // |S[p+1]| over the block
+    // Planes top-down.  Distortion decreases of plane p (oracle dist_gain,
+    // half-units, d = reconstruction offset): a sample whose top bit is p
+    // gains 2^p (12 v + 6d - 9 2^p); one significant above p, with l = v mod
+    // 2^p, gains 2^p (4l + 2d - 2^p) if bit p is set, else 2^p (3 2^p - 4l -
+    // 2d); lossless p = 0 gains 4 for a new sample and for a refined 0 bit,
+    // nothing else.  The sums of v over new samples (N) and of +-l over
+    // refined ones (R1: bit p set, R0: clear) come from the column masks:
+    // sum_N v = sum_{q<=p} 2^q |N & B[q]|, sum_R +-l = sum_{q<p} 2^q (|R1 &
+    // B[q]| - |R0 & B[q]|), int32 per lane up to p = 23.  The slope-prediction
+    // counts (oracle plane_stats): significant samples, and insignificant
+    // samples with a significant 8-neighbour.
     for (int p = P - 1; p >= 0; p--) {
-        uint32_t b_lo = 0, b_hi = 0;
+        const uint64_t Bp = planes[p * 64 + lane];
+        const uint64_t N = Bp & ~colS, R1 = colS & Bp;
+        uint32_t nb1 = (uint32_t)__popcll(R1);  // refined samples with bit p set
         int64_t ref = 0, sig = 0;
-        unroll_rows<0>([&](auto yc) {
-            constexpr int y = decltype(yc)::value;
-            const uint32_t v = col[y];  // 0 outside the block
-            const uint64_t m = __ballot((v >> p) & 1u);
-            b_lo = writelane<y>(b_lo, (uint32_t)m);
-            b_hi = writelane<y>(b_hi, (uint32_t)(m >> 32));
-        });
-        // Distortion decreases of the plane (oracle dist_gain, half-units,
-        // d = reconstruction offset): a sample whose top bit is p gains
-        // 2^p (12 v + 6d - 9 2^p); one significant above p, with l = v mod
-        // 2^p, gains 2^p (4l + 2d - 2^p) if bit p is set, else
-        // 2^p (3 2^p - 4l - 2d); lossless p = 0 gains 4 for a new sample
-        // and for a refined 0 bit, nothing else.  So the plane needs the
-        // per-lane sums of v (top bit p) and of +-l (refined), int32 up to
-        // p = 23, and the counts, which come from the masks.
         int32_t sv = 0, sl = 0;
         if (p <= 23) {
-            const uint32_t lm = (1u << p) - 1u;
-#pragma unroll
-            for (int y = 0; y < 64; y++) {
-                uint32_t v = col[y];
-                asm volatile("" : "+v"(v));  // no common subexpressions with the ballot loop (register pressure)
-                const uint32_t hi = v >> p;
-                const int32_t l = (int32_t)(v & lm);
-                sv += hi == 1 ? (int32_t)v : 0;
-                sl += hi > 1 ? ((hi & 1u) ? l : -l) : 0;
+            sv = __popcll(N) << p;
+            for (int q = 0; q < p; q++) {
+                const uint64_t Bq = planes[q * 64 + lane];
+                sv += __popcll(N & Bq) << q;
+                sl += (2 * __popcll(R1 & Bq) - __popcll(colS & Bq)) * (1 << q);
             }
         } else {
             // 64-bit gains per row, the column re-read from the sign-magnitude
@@ -684,16 +656,18 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
                 else ref += g;
             }
         }
-        const uint64_t rowB = ((uint64_t)b_hi << 32) | b_lo;
-        uint32_t nb1 = (uint32_t)__popcll(rowB & rowS);  // refined samples with bit p set
-        rowS |= rowB;
-        B[(size_t)p * 64 + lane] = rowB;
-        S[(size_t)p * 64 + lane] = rowS;
-        // counts: lane y's row with its neighbours y-1 / y+1 (0 outside)
-        const uint64_t upS = lane > 0 ? (uint64_t)__shfl_up((long long)rowS, 1, 64) : 0ull;
-        const uint64_t dnS = lane < 63 ? (uint64_t)__shfl_down((long long)rowS, 1, 64) : 0ull;
-        const uint32_t nb = lane < d.h ? (uint32_t)__popcll((dil(upS) | dil(rowS) | dil(dnS)) & ~rowS & wmask) : 0u;
-        uint32_t cS = (uint32_t)__popcll(rowS), cN = nb;
+        colS |= Bp;
+        ST[(size_t)p * 64 + lane] = colS;
+        // insignificant samples with a significant 8-neighbour (rows < h,
+        // columns < w)
+        // (the shuffles run on every lane: a lane left out of a ds_bpermute
+        // reads as 0 to the lane that fetches from it)
+        const uint64_t up = (uint64_t)__shfl_up((long long)colS, 1, 64);
+        const uint64_t dn = (uint64_t)__shfl_down((long long)colS, 1, 64);
+        const uint64_t Lc = lane > 0 ? up : 0ull, Rc = lane < 63 ? dn : 0ull;
+        const uint64_t H = colS | Lc | Rc;
+        uint32_t cN = wcol ? (uint32_t)__popcll((H | (H << 1) | (H >> 1)) & ~colS & hmask) : 0u;
+        uint32_t cS = (uint32_t)__popcll(colS);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             cS += (uint32_t)__shfl_xor((int)cS, o, 64);
@@ -720,20 +694,6 @@ __global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
             a.dsig[(size_t)b * 32 + p] = sig;
         }
         cnt_above = cS;
-    }
-    // the same masks transposed: this lane's column, bit y = bit p of row y
-    uint64_t colS = 0;
-    for (int p = P - 1; p >= 0; p--) {
-        uint32_t c_lo = 0, c_hi = 0;
-#pragma unroll
-        for (int y = 0; y < 32; y++) {
-            c_lo |= __builtin_amdgcn_ubfe(col[y], (uint32_t)p, 1u) << y;
-            c_hi |= __builtin_amdgcn_ubfe(col[y + 32], (uint32_t)p, 1u) << y;
-        }
-        const uint64_t colB = ((uint64_t)c_hi << 32) | c_lo;
-        colS |= colB;
-        BT[(size_t)p * 64 + lane] = colB;
-        ST[(size_t)p * 64 + lane] = colS;
     }
 }
 
@@ -1006,7 +966,7 @@ GpuEncoder::~GpuEncoder() {
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwtab, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
-                     &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d, &cmcensus};
+                     &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -1244,6 +1204,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     const char *rep = getenv("JP2HIP_REPEAT_STAGE");
     const int nrep_dwt = rep && !strcmp(rep, "dwt") ? 2 : 1, nrep_quant = rep && !strcmp(rep, "quant") ? 2 : 1;
     const int nrep_cm = rep && !strcmp(rep, "cm") ? 2 : 1, nrep_mq = rep && !strcmp(rep, "mq") ? 2 : 1;
+    const int nrep_pcrd = rep && !strcmp(rep, "pcrd") ? 2 : 1;
     if (plan.rc.levels == 0) {
         // S1+S2 only: no decomposition
         IngestArgs ia;
@@ -1298,9 +1259,12 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.dref = (int64_t *)dref.ptr;
     qa.dsig = (int64_t *)dsig.ptr;
     qa.est = (uint32_t *)est.ptr;
+    qa.max_mb = 1;
+    for (int i = 0; i < nb; i++) qa.max_mb = std::max(qa.max_mb, (int)plan.blocks[i].Mb);
+    const size_t qlds = (size_t)qa.max_mb * 64 * sizeof(uint64_t);
     for (int r = 0; nb && r < nrep_quant; r++) {
-        if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, dim3(nb), dim3(64), 0, stream, qa);
-        else hipLaunchKernelGGL(k_quant<false>, dim3(nb), dim3(64), 0, stream, qa);
+        if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, dim3(nb), dim3(64), qlds, stream, qa);
+        else hipLaunchKernelGGL(k_quant<false>, dim3(nb), dim3(64), qlds, stream, qa);
     }
     HIPCHECK(hipGetLastError());
     // S4b: slope prediction -> lowest coded plane per block
@@ -1392,12 +1356,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ca.counts = (uint4 *)counts.ptr;
     ca.dspp = (int64_t *)dspp.ptr;
     ca.lossless = plan.rc.reversible;
-    ca.census = nullptr;
-    if (dd) {
-        if (!ensure<unsigned long long>(cmcensus, 8, err)) return false;
-        HIPCHECK(hipMemsetAsync(cmcensus.ptr, 0, 8 * sizeof(unsigned long long), stream));
-        ca.census = (unsigned long long *)cmcensus.ptr;
-    }
     for (int r = 0; r < nrep_cm; r++) launch_t1_cm(ca, stream);
     HIPCHECK(hipGetLastError());
     // MQ lane order: blocks by decreasing decision count
@@ -1449,6 +1407,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     for (int r = 0; r < nrep_mq; r++) launch_t1_mq(ma, stream);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[4], stream));
+    for (int rp = 0; rp < nrep_pcrd; rp++) {
     // S6a hulls
     HullArgs ha;
     ha.nblocks = nb;
@@ -1502,6 +1461,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
         HIPCHECK(hipcub::DeviceScan::InclusiveSum(cubtmp.ptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
     }
+    }  // nrep_pcrd
     HIPCHECK(hipEventRecord(ev[5], stream));
     profiled = profile;
     if (dd) {
@@ -1515,9 +1475,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!dump(dd, "dists.bin", dists, (size_t)nb * kMaxPasses * 8, err)) return false;
         if (!dump(dd, "dref.bin", dref, (size_t)nb * 32 * 8, err)) return false;
         if (!dump(dd, "dsig.bin", dsig, (size_t)nb * 32 * 8, err)) return false;
+        if (!dump(dd, "est.bin", est, (size_t)nb * 32 * 4, err)) return false;
+        if (!dump(dd, "pmin.bin", pmin, nb, err)) return false;
         if (!dump(dd, "bp.bin", bp, plan.bp_words * 8, err)) return false;
         if (!dump(dd, "mqdbg.bin", dbgbuf, (size_t)nb * 4 * 8, err)) return false;
-        if (!dump(dd, "cmcensus.bin", cmcensus, 8 * 8, err)) return false;
     }
     // no host wait: tier-1 totals and the overflow flag reach the host with
     // the first tier-2 summary (t2_size), stage times via collect_profile()
@@ -1662,6 +1623,7 @@ bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart
     if (!ensure<RateState>(rstate, 1, err)) return false;
     if (!h_rs) HIPCHECK(hipHostMalloc((void **)&h_rs, sizeof(RateState), hipHostMallocDefault));
     RateState *d = (RateState *)rstate.ptr;
+    static const bool rep_t2 = getenv("JP2HIP_REPEAT_STAGE") && !strcmp(getenv("JP2HIP_REPEAT_STAGE"), "t2");
     const int *halt = &d->halt;
     HIPCHECK(hipEventRecord(ev[6], stream));
     if (restart) hipLaunchKernelGGL(k_rate_init, dim3(1), dim3(1), 0, stream, d, init, L, (int64_t *)budget.ptr);
@@ -1671,6 +1633,7 @@ bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart
                            (uint64_t *)thr.ptr + kMaxLayers, halt);
         if (!apply_thresholds(plan, halt, err)) return false;
         t2_size_launch(plan, true, halt);
+        if (rep_t2) t2_size_launch(plan, true, halt);  // experiment knob (JP2HIP_REPEAT_STAGE=t2)
         hipLaunchKernelGGL(k_rate_step, dim3(1), dim3(1), 0, stream, d, (const T2Summary *)t2sum.ptr, L,
                            (int64_t *)budget.ptr);
     }

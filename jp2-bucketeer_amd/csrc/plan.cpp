@@ -258,7 +258,7 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
                                         uint64_t cap = ((uint64_t)bd.w * bd.h * (q.Mb + 1)) / 2 + 1024;
                                         cap = (cap + 15) & ~(uint64_t)15;
                                         bd.out_cap = (uint32_t)cap;
-                                        bpw += (uint64_t)(4 * q.Mb + 2) * 64;  // row masks, then column masks
+                                        bpw += (uint64_t)(2 * q.Mb + 1) * 64;  // column masks (kernels.hip k_quant)
                                         smw += (uint64_t)64 * bd.h;
                                         ob += cap;
                                         P.blocks.push_back(bd);
@@ -344,7 +344,7 @@ void make_subplan(const Plan &full, int tr0, int tr1, Plan &S) {
             b.out_off -= f.out_off;
         }
         const BlockDesc &l = S.blocks.back();
-        S.bp_words = l.bp_off + (uint64_t)(4 * l.Mb + 2) * 64;
+        S.bp_words = l.bp_off + (uint64_t)(2 * l.Mb + 1) * 64;
         S.sm_words = l.sm_off + (uint64_t)64 * l.h;
         S.out_bytes = l.out_off + l.out_cap;
     }

@@ -1,13 +1,14 @@
 // t1.hip -- EBCOT tier-1 (ISO/IEC 15444-1 Annex D) and the MQ coder (Annex C)
 // for gfx950, split in two kernels so the serial part is as short as possible:
 //
-//   k_t1_cm  context modelling, one lane per (code-block, bit-plane).
-//            Significance lives in 64-bit row masks (bit c = column c); a
-//            stripe (4 rows) is modelled with whole-row bit operations.  The
+//   k_t1_cm3 context modelling, one wave per (code-block, bit-plane),
+//            lane = column.  Significance lives in 64-bit column masks (bit
+//            r = row r), so the neighbourhood and context rules run
+//            bit-sliced for the whole column at once.  The
 //            state at the start of plane p is known from the bit-planes
 //            (S[p+1] = OR of planes above p), so planes are independent:
 //              - SPP membership is the least fixed point of the causal
-//                neighbourhood rule (iterated on the stripe's masks);
+//                neighbourhood rule (iterated on the whole masks);
 //              - MRP neighbours all see the post-SPP state S[p+1] | N;
 //              - CUP neighbours see S[p] (already visited) or S[p+1] | N
 //                (not yet visited): closed form, no sample-serial state.
@@ -38,43 +39,6 @@ enum { CX_RL = 17, CX_UNI = 18, CX_PAD = 19 };
 // validity test.
 constexpr uint8_t kPadDecision = CX_PAD << 1;
 
-// zero-coding context (Table D.1) from the 8-neighbour pattern
-// bits: UL U UR L R DL D DR
-__device__ __forceinline__ int zc_ctx(int band, int pat) {
-    int UL = pat & 1, U = (pat >> 1) & 1, UR = (pat >> 2) & 1, Lf = (pat >> 3) & 1;
-    int Rt = (pat >> 4) & 1, DL = (pat >> 5) & 1, D = (pat >> 6) & 1, DR = (pat >> 7) & 1;
-    int h = Lf + Rt, v = U + D, dg = UL + UR + DL + DR;
-    if (band == 1) { int t = h; h = v; v = t; }
-    if (band == 3) {
-        int hv = h + v;
-        if (dg >= 3) return 8;
-        if (dg == 2) return hv >= 1 ? 7 : 6;
-        if (dg == 1) return hv >= 2 ? 5 : (hv == 1 ? 4 : 3);
-        return hv >= 2 ? 2 : (hv == 1 ? 1 : 0);
-    }
-    if (h == 2) return 8;
-    if (h == 1) return v >= 1 ? 7 : (dg >= 1 ? 6 : 5);
-    if (v == 2) return 4;
-    if (v == 1) return 3;
-    if (dg >= 2) return 2;
-    return dg == 1 ? 1 : 0;
-}
-
-// sign-coding context (Tables D.2/D.3): pattern Lsig Lneg Rsig Rneg Usig Uneg
-// Dsig Dneg -> (ctx << 1) | xorbit
-__device__ __forceinline__ int sc_lut(int pat) {
-    auto contrib = [](int sig, int neg) { return sig ? (neg ? -1 : 1) : 0; };
-    int hc = contrib(pat & 1, (pat >> 1) & 1) + contrib((pat >> 2) & 1, (pat >> 3) & 1);
-    int vc = contrib((pat >> 4) & 1, (pat >> 5) & 1) + contrib((pat >> 6) & 1, (pat >> 7) & 1);
-    hc = hc < -1 ? -1 : (hc > 1 ? 1 : hc);
-    vc = vc < -1 ? -1 : (vc > 1 ? 1 : vc);
-    int ctx, xr;
-    if (hc == 1) { xr = 0; ctx = vc == 1 ? 13 : (vc == 0 ? 12 : 11); }
-    else if (hc == 0) { xr = vc == -1; ctx = vc == 0 ? 9 : 10; }
-    else { xr = 1; ctx = vc == 1 ? 11 : (vc == 0 ? 12 : 13); }
-    return (ctx << 1) | xr;
-}
-
 __device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m >> c) & 1u; }
 
 // bytes reserved per (block, plane) for the three passes' decisions:
@@ -83,33 +47,6 @@ __device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m
 // 16-byte chunk past the end of a pass)
 __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
     return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
-}
-
-// 3-bit window of mask m around column c: bit0 = column c-1, bit1 = c,
-// bit2 = c+1 (columns outside 0..63 read as 0)
-__device__ __forceinline__ uint32_t win3(uint64_t m, int c) {
-    return (uint32_t)(c == 0 ? (m << 1) : (m >> (c - 1))) & 7u;
-}
-
-// Zero-coding pattern (bits UL U UR L R DL D DR) of the sample at column c
-// from the "visited" (b) and "not yet visited" (a) masks of the rows above,
-// at and below it.
-__device__ __forceinline__ uint32_t pat8(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
-                                         uint64_t DNb, uint64_t DNa, int c) {
-    const uint32_t ub = win3(UPb, c), ua = win3(UPa, c), mb = win3(MIDb, c), ma = win3(MIDa, c);
-    const uint32_t db = win3(DNb, c), da = win3(DNa, c);
-    return (ub & 3u) | (ua & 4u) | ((mb & 1u) << 3) | ((ma & 4u) << 2) | ((db & 1u) << 5) | ((da & 6u) << 5);
-}
-// Sign-coding pattern Lsig Lneg Rsig Rneg Usig Uneg Dsig Dneg.
-__device__ __forceinline__ uint32_t pats(uint64_t UPb, uint64_t MIDb, uint64_t MIDa, uint64_t DNa, uint64_t sgU,
-                                         uint64_t sgM, uint64_t sgD, int c) {
-    const uint32_t mb = win3(MIDb, c), ma = win3(MIDa, c), sm = win3(sgM, c);
-    return (mb & 1u) | ((sm & 1u) << 1) | ((ma & 4u)) | ((sm & 4u) << 1) | (bit(UPb, c) << 4) |
-           (bit(sgU, c) << 5) | (bit(DNa, c) << 6) | (bit(sgD, c) << 7);
-}
-__device__ __forceinline__ uint64_t nbhd(uint64_t UPb, uint64_t UPa, uint64_t MIDb, uint64_t MIDa,
-                                         uint64_t DNb, uint64_t DNa) {
-    return (UPb << 1) | UPb | (UPa >> 1) | (MIDb << 1) | (MIDa >> 1) | (DNb << 1) | DNa | (DNa >> 1);
 }
 
 // A lane's decisions inside one stripe (<= 10), as bytes (context << 1) | d.
@@ -144,291 +81,11 @@ __device__ __forceinline__ int flush_stripe(uint8_t *out, int base, const LaneDe
     return total;
 }
 
-// The item's bit-plane rows live in VGPRs, one row per lane (lane r holds
-// row r of B[p], S[p], S[p+1], S[p+2], the sign plane and the new-significance
-// masks N); a stripe reads the rows it needs with v_readlane into SGPRs, so
-// the per-stripe mask algebra is scalar and no memory access sits inside the
-// stripe loops.
-struct RowV {
-    uint32_t lo, hi;
-};
-__device__ __forceinline__ RowV rowv(uint64_t v) { return RowV{(uint32_t)v, (uint32_t)(v >> 32)}; }
-// row r (wave-uniform) of a lane-distributed mask; 0 outside [0, h)
-__device__ __forceinline__ uint64_t row(const RowV &v, int r, int h) {
-    if (r < 0 || r >= h) return 0ull;
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v.hi, r) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)v.lo, r);
-}
-__device__ __forceinline__ void set_row(RowV &v, int r, uint64_t m, int lane) {
-    v.lo = lane == r ? (uint32_t)m : v.lo;
-    v.hi = lane == r ? (uint32_t)(m >> 32) : v.hi;
-}
-
-#define ROWS6(dst, src)                                            \
-    _Pragma("unroll") for (int i = 0; i < 6; i++) dst[i] = row(src, r0 - 1 + i, h);
-
-// Context modelling: one wavefront per (code-block, bit-plane) item, lane =
-// column.  The stripe's significance state is a handful of 64-bit row masks,
-// wave-uniform (SGPRs, SALU); each lane forms the contexts of its own
-// column's <= 4 samples from them, and the stripe's decisions are laid out in
-// scan order (column-major) by a wave prefix sum.
-//   SPP: membership is the least fixed point of the causal neighbourhood
-//        rule over the stripe's masks (new significance N feeds the samples
-//        visited after it);
-//   MRP: neighbours see the post-SPP state S[p+1] | N;
-//   CUP: visited neighbours see S[p], the others S[p+1] | N (closed form).
-// Signs come from the sign plane; the SPP distortion decrease is summed once
-// per item from N and the sign-magnitude words.
 constexpr int kCmWaves = 4;  // items per workgroup
-__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
-    __shared__ uint8_t lzc[4 * 256];
-    __shared__ uint8_t lsc[256];
-    // the grid covers the largest possible list; workgroups past the real
-    // item count (known on the device only) leave at once
-    if ((int)blockIdx.x * kCmWaves >= *a.nitems) return;
-    for (int i = threadIdx.x; i < 1024; i += 64 * kCmWaves) lzc[i] = (uint8_t)zc_ctx(i >> 8, i & 255);
-    for (int i = threadIdx.x; i < 256; i += 64 * kCmWaves) lsc[i] = (uint8_t)sc_lut(i);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gi = blockIdx.x * kCmWaves + wv;
-    if (gi >= *a.nitems) return;
-    const int2 item = a.items[gi];
-    const int b = item.x, p = item.y;
-    const BlockDesc d = a.blocks[b];
-    const int P = a.P[b];
-    const int k = P - 1 - p;  // plane index counted from the block's top plane
-    const bool lossless = a.lossless != 0;
-    const int w = d.w, h = d.h, Mb = d.Mb;
-    const int c = lane;
-    const uint64_t V = (w >= 64) ? ~0ull : ((1ull << w) - 1ull);
-    const uint64_t *BP = a.bp + d.bp_off;
-    const uint64_t *SP = BP + (size_t)Mb * 64;
-    const uint64_t *SGp = BP + (size_t)2 * Mb * 64;
-    const uint8_t *zl = lzc + d.band * 256;
-    const int nstripes = (h + 3) >> 2;
-    const bool has1 = p + 1 < P, has2 = p + 2 < P;
-    // one coalesced load per plane row array; lane r keeps row r
-    const bool inr = lane < h;
-    const RowV Bv = rowv(inr ? BP[(size_t)p * 64 + lane] : 0ull);
-    const RowV S0v = rowv(inr ? SP[(size_t)p * 64 + lane] : 0ull);
-    const RowV S1v = rowv(inr && has1 ? SP[(size_t)(p + 1) * 64 + lane] : 0ull);
-    const RowV S2v = rowv(inr && has2 ? SP[(size_t)(p + 2) * 64 + lane] : 0ull);
-    const RowV SGv = rowv(inr ? SGp[lane] : 0ull);
-    RowV Nv = {0u, 0u};
-    // quiet stripes: rows (bit r) with anything significant at planes >= p
-    // (M0) and > p (M1).  A stripe whose 6-row window r0-1 .. r0+4 is empty
-    // in M1 has no SPP candidate (unless the stripe above just gained
-    // significance) and no refinement; one empty in M0 codes only run-length
-    // "0" decisions in the cleanup pass -- both without the mask algebra.
-    const uint64_t M0 = __ballot(inr && (S0v.lo | S0v.hi) != 0u);
-    const uint64_t M1 = __ballot(inr && (S1v.lo | S1v.hi) != 0u);
-    auto win6 = [](uint64_t M, int r0) { return r0 == 0 ? (M & 0x1Full) : ((M >> (r0 - 1)) & 0x3Full); };
-    uint8_t *out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
-    int64_t dspp = 0;
-    int n_spp = 0, n_mrp = 0, pos = 0;
-    const bool spp = p < P - 1;
-    uint64_t tc0 = a.census ? clock64() : 0, tc1 = tc0, tc2 = tc0;
-    if (spp) {
-        // ---------------- significance propagation ----------------
-        uint64_t nprev = 0;
-        for (int s = 0; s < nstripes; s++) {
-            const int r0 = s * 4, nr = min(4, h - r0);
-            if (nprev == 0 && win6(M1, r0) == 0) continue;  // quiet: no candidate, N stays 0
-            uint64_t s1[6], sg[6], bt[4], n[4] = {0, 0, 0, 0}, mem[4];
-            ROWS6(s1, S1v);
-            ROWS6(sg, SGv);
-#pragma unroll
-            for (int q = 0; q < 4; q++) bt[q] = row(Bv, r0 + q, h);
-            const uint64_t bfprev = (r0 > 0) ? (s1[0] | nprev) : 0ull;
-            for (;;) {
-                bool changed = false;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (q >= nr) { mem[q] = 0; continue; }
-                    uint64_t UPb = (q == 0) ? bfprev : (s1[q] | n[q - 1]);
-                    uint64_t UPa = (q == 0) ? bfprev : s1[q];
-                    uint64_t MIDb = s1[q + 1] | n[q], MIDa = s1[q + 1];
-                    uint64_t DNb = (q == 3) ? s1[5] : (s1[q + 2] | n[q + 1]);
-                    uint64_t DNa = s1[q + 2];
-                    mem[q] = ~s1[q + 1] & V & nbhd(UPb, UPa, MIDb, MIDa, DNb, DNa);
-                    uint64_t nn = mem[q] & bt[q];
-                    if (nn != n[q]) { n[q] = nn; changed = true; }
-                }
-                if (!changed) break;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (q < nr) set_row(Nv, r0 + q, n[q], lane);
-            nprev = n[3];
-            LaneDec e{0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (q >= nr || !bit(mem[q], c)) continue;
-                uint64_t UPb = (q == 0) ? bfprev : (s1[q] | n[q - 1]);
-                uint64_t UPa = (q == 0) ? bfprev : s1[q];
-                uint64_t MIDb = s1[q + 1] | n[q], MIDa = s1[q + 1];
-                uint64_t DNb = (q == 3) ? s1[5] : (s1[q + 2] | n[q + 1]);
-                uint64_t DNa = s1[q + 2];
-                const uint32_t bv = bit(bt[q], c);
-                e.put(zl[pat8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
-                if (bv) {
-                    const uint32_t sp = lsc[pats(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
-                    e.put(sp >> 1, bit(sg[q + 1], c) ^ (sp & 1u));
-                }
-            }
-            pos += flush_stripe(out, pos, e, lane);
-        }
-        n_spp = pos;
-        pos = pad_pass(out, pos, lane);
-        if (a.census) tc1 = clock64();
-        const int mrp0 = pos;
-        // ---------------- magnitude refinement ----------------
-        for (int s = 0; s < nstripes; s++) {
-            const int r0 = s * 4, nr = min(4, h - r0);
-            if (((M1 >> r0) & 0xFull) == 0) continue;  // nothing to refine
-            uint64_t post[6], bt[4], mem[4], fr[4];
-#pragma unroll
-            for (int i = 0; i < 6; i++) post[i] = row(S1v, r0 - 1 + i, h) | row(Nv, r0 - 1 + i, h);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                bt[q] = row(Bv, r0 + q, h);
-                const uint64_t s1q = row(S1v, r0 + q, h);
-                mem[q] = s1q & V;
-                fr[q] = s1q & ~row(S2v, r0 + q, h);
-            }
-            LaneDec e{0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (q >= nr || !bit(mem[q], c)) continue;
-                uint32_t ctx = 16;
-                if (bit(fr[q], c)) ctx = pat8(post[q], post[q], post[q + 1], post[q + 1], post[q + 2], post[q + 2], c) ? 15 : 14;
-                e.put(ctx, bit(bt[q], c));
-            }
-            pos += flush_stripe(out, pos, e, lane);
-        }
-        n_mrp = pos - mrp0;
-        pos = pad_pass(out, pos, lane);
-    }
-    if (a.census) tc2 = clock64();
-    const int cup0 = pos;
-    // ---------------- cleanup ----------------
-    for (int s = 0; s < nstripes; s++) {
-        const int r0 = s * 4, nr = min(4, h - r0);
-        if (nr == 4 && win6(M0, r0) == 0) {
-            // quiet: every column is one run-length decision "0"
-            if (lane < w) out[pos + lane] = (uint8_t)(CX_RL << 1);
-            pos += w;
-            continue;
-        }
-        uint64_t s1[6], post[6], s0[6], sg[6], bt[4], mem[4];
-        ROWS6(s1, S1v);
-#pragma unroll
-        for (int i = 0; i < 6; i++) post[i] = s1[i] | row(Nv, r0 - 1 + i, h);
-        ROWS6(s0, S0v);
-        ROWS6(sg, SGv);
-#pragma unroll
-        for (int q = 0; q < 4; q++) bt[q] = row(Bv, r0 + q, h);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (q >= nr) { mem[q] = 0; continue; }
-            uint64_t c_spp = 0;
-            if (spp) {  // SPP membership with the final new-significance masks
-                uint64_t UPb = post[q], UPa = (q == 0) ? post[0] : s1[q];
-                uint64_t MIDb = post[q + 1], MIDa = s1[q + 1];
-                uint64_t DNb = (q == 3) ? s1[5] : post[q + 2];
-                uint64_t DNa = s1[q + 2];
-                c_spp = ~s1[q + 1] & V & nbhd(UPb, UPa, MIDb, MIDa, DNb, DNa);
-            }
-            mem[q] = ~s1[q + 1] & ~c_spp & V;
-        }
-        uint64_t rl = 0;
-        if (nr == 4) {
-            uint64_t z = (s0[0] << 1) | s0[0] | (s0[0] >> 1) | ((s0[1] | s0[2] | s0[3] | s0[4]) << 1) |
-                         ((post[1] | post[2] | post[3] | post[4]) >> 1) | (post[5] << 1) | post[5] |
-                         (post[5] >> 1);
-            rl = mem[0] & mem[1] & mem[2] & mem[3] & ~z;
-        }
-        LaneDec e{0, 0, 0};
-        int qstart = 0;
-        if (bit(rl, c)) {
-            int r = 4;
-#pragma unroll
-            for (int q = 3; q >= 0; q--)
-                if (bit(bt[q], c)) r = q;
-            if (r == 4) {
-                e.put(CX_RL, 0);
-                qstart = 4;
-            } else {
-                e.put(CX_RL, 1);
-                e.put(CX_UNI, (uint32_t)r >> 1);
-                e.put(CX_UNI, (uint32_t)r & 1u);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (q != r) continue;
-                    const uint32_t sp = lsc[pats(s0[q], s0[q + 1], post[q + 1], post[q + 2], sg[q], sg[q + 1], sg[q + 2], c)];
-                    e.put(sp >> 1, bit(sg[q + 1], c) ^ (sp & 1u));
-                }
-                qstart = r + 1;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (q < qstart || q >= nr || !bit(mem[q], c)) continue;
-            uint64_t UPb = s0[q], UPa = (q == 0) ? s0[0] : post[q];
-            uint64_t MIDb = s0[q + 1], MIDa = post[q + 1];
-            uint64_t DNb = (q == 3) ? post[5] : s0[q + 2];
-            uint64_t DNa = post[q + 2];
-            const uint32_t bv = bit(bt[q], c);
-            e.put(zl[pat8(UPb, UPa, MIDb, MIDa, DNb, DNa, c)], bv);
-            if (bv) {
-                const uint32_t sp = lsc[pats(UPb, MIDb, MIDa, DNa, sg[q], sg[q + 1], sg[q + 2], c)];
-                e.put(sp >> 1, bit(sg[q + 1], c) ^ (sp & 1u));
-            }
-        }
-        pos += flush_stripe(out, pos, e, lane);
-    }
-    const int n_cup = pos - cup0;
-    pad_pass(out, pos, lane);
-    if (a.census && lane == 0) {  // debug: shader cycles per pass, summed over items
-        const uint64_t tc3 = clock64();
-        atomicAdd(&a.census[0], (unsigned long long)(spp ? tc1 - tc0 : 0));
-        atomicAdd(&a.census[1], (unsigned long long)(spp ? tc2 - tc1 : 0));
-        atomicAdd(&a.census[2], (unsigned long long)(tc3 - tc2));
-        atomicAdd(&a.census[3], 1ull);
-        atomicAdd(&a.census[4], (unsigned long long)n_spp);
-        atomicAdd(&a.census[5], (unsigned long long)n_mrp);
-        atomicAdd(&a.census[6], (unsigned long long)n_cup);
-    }
-    if (spp) {
-        // SPP distortion decrease: lane r sums its row's newly significant
-        // samples (the sign-magnitude words are read only here)
-        const uint64_t nrow = ((uint64_t)Nv.hi << 32) | Nv.lo;
-        if (nrow) {
-            const int32_t *SMr = a.sm + d.sm_off + (size_t)lane * 64;
-            uint64_t m = nrow;
-            while (m) {
-                const int cc = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                dspp += dist_gain((uint32_t)SMr[cc] & 0x7FFFFFFFu, p, lossless);
-            }
-        }
-    }
-    dspp = wave_sum64(dspp);
-    if (lane == 0) {
-        uint4 cnt;  // decisions per pass; pass streams start at 16-byte boundaries
-        cnt.x = (uint32_t)n_spp;
-        cnt.y = (uint32_t)n_mrp;
-        cnt.z = (uint32_t)n_cup;
-        cnt.w = 0;
-        a.counts[(size_t)b * 32 + k] = cnt;
-        a.dspp[(size_t)b * 32 + k] = dspp;
-    }
-}
 
 // --------------------------------------------------------------------------
-// Context modelling on column masks (k_t1_cm2; the default).  Same items,
-// same decision streams as k_t1_cm, computed in the transposed layout: lane
+// Context modelling on column masks (k_t1_cm2; k_t1_cm3 below is the default).
+// One wavefront per (code-block, bit-plane) item, in the transposed layout: lane
 // c holds column c of every mask as a 64-bit word (bit r = row r; k_quant
 // writes them), so a vertical neighbour is a bit shift inside the lane and a
 // horizontal one is the next lane.  The neighbourhood and context rules then
@@ -436,7 +93,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm(T1CmArgs a) {
 // context number as four masks), instead of once per sample; per stripe a
 // lane only picks its four rows' bits and writes its decision bytes.
 //
-// Causal states, as in k_t1_cm: a neighbour already visited in the scan
+// Causal states: a neighbour already visited in the scan
 // (stripe by stripe, column by column, top to bottom) is seen in the state
 // Vb, one not yet visited in Va -- SPP: Vb = S[p+1] | N, Va = S[p+1];
 // CUP: Vb = S[p], Va = S[p+1] | N.  For row r, column c: (r-1, c), (r, c-1),
@@ -565,7 +222,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm2(T1CmArgs a) {
     const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
     const bool vl = lane < w;
     const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;  // this column's rows
-    const uint64_t *CT = a.bp + d.bp_off + (size_t)(2 * Mb + 1) * 64;      // column masks
+    const uint64_t *CT = a.bp + d.bp_off;  // column masks (k_quant)
     const uint64_t B = vl ? CT[(size_t)p * 64 + lane] : 0ull;
     const uint64_t S0 = vl ? CT[(size_t)(Mb + p) * 64 + lane] : 0ull;
     const uint64_t S1 = (vl && p + 1 < P) ? CT[(size_t)(Mb + p + 1) * 64 + lane] : 0ull;
@@ -854,7 +511,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
         const bool vl = lane < w;
         const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;
-        const uint64_t *CT = a.bp + d.bp_off + (size_t)(2 * Mb + 1) * 64;
+        const uint64_t *CT = a.bp + d.bp_off;
         const uint64_t B = vl ? CT[(size_t)p * 64 + lane] : 0ull;
         const uint64_t S0 = vl ? CT[(size_t)(Mb + p) * 64 + lane] : 0ull;
         const uint64_t S1 = (vl && p + 1 < P) ? CT[(size_t)(Mb + p + 1) * 64 + lane] : 0ull;
@@ -1145,7 +802,7 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 }
 
 // One lane codes one code-block.  The block's passes are segments of the
-// decision streams (each 16-byte aligned, see k_t1_cm); the lane walks them
+// decision streams (each 16-byte aligned, see k_t1_cm3); the lane walks them
 // with ONE data-driven loop -- a chunk of up to 16 decisions per iteration;
 // the segment switch and the per-pass rate record are data, not control
 // flow -- so all lanes of a wave execute the same instruction stream
@@ -1344,9 +1001,8 @@ void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, c
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (!a.max_items) return;
     const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
-    static const char *v = getenv("JP2HIP_CM");  // experiment knob: "rows" / "2" = earlier variants
-    if (v && !strcmp(v, "rows")) hipLaunchKernelGGL(k_t1_cm, g, dim3(64 * kCmWaves), 0, st, a);
-    else if (v && !strcmp(v, "2")) hipLaunchKernelGGL(k_t1_cm2, g, dim3(64 * kCmWaves), 0, st, a);
+    static const char *v = getenv("JP2HIP_CM");  // experiment knob: "2" = the per-sample-branch variant
+    if (v && !strcmp(v, "2")) hipLaunchKernelGGL(k_t1_cm2, g, dim3(64 * kCmWaves), 0, st, a);
     else hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,

@@ -34,6 +34,3 @@ for q in (0, 1, 2, 10, 100, 300, 1000):
     sel = wv == q
     if sel.any():
         print("wave", q, "dec max", dec[m][sel].max(), "min", dec[m][sel].min(), "wall us max", wall[m][sel].max() / 100.0)
-cm = np.fromfile(os.path.join(d, "cmcensus.bin"), dtype=np.uint64)
-print("k_t1_cm census: items", cm[3], "cycles SPP/MRP/CUP", cm[0], cm[1], cm[2],
-      "share", np.round(cm[:3] / cm[:3].sum(), 3), "decisions SPP/MRP/CUP", cm[4], cm[5], cm[6])

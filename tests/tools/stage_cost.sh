@@ -4,8 +4,8 @@
 set -o pipefail
 o=gpurun_out/${1:-stage}
 mkdir -p $o
-B="python bench.py --no-cpu-baseline --no-lossless --steps 48"
+B="python bench.py --no-cpu-baseline --no-lossless --steps 8"
 timeout -k 10 200 $B > $o/base.json 2> $o/base.err || exit 1
-for st in mq cm quant dwt; do
+for st in mq cm quant dwt pcrd t2; do
   JP2HIP_REPEAT_STAGE=$st timeout -k 10 200 $B > $o/$st.json 2> $o/$st.err || exit 1
 done
