@@ -51,6 +51,10 @@ def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # single-box rehearsal of the N-rank path: every rank on one GPU
+    # (JP2HIP_BENCH_DEVICE=0, with JP2HIP_BENCH_BACKEND=gloo)
+    if os.environ.get("JP2HIP_BENCH_DEVICE"):
+        local = int(os.environ["JP2HIP_BENCH_DEVICE"])
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("JP2HIP_BENCH_BACKEND", "nccl")
@@ -68,6 +72,16 @@ def barrier_max(world, value, device):
                      device=device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allreduce_sum(world, value, device):
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.int64, device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
 
 
 def barrier(world):
@@ -303,7 +317,7 @@ def run(args):
         # byte per MQ decision and writes the MQ code bytes (the per-pass
         # counts / distortions it also reads are < 1 %)
         mq_alg = avg_all["mq_decisions"] + avg_all["t1_bytes"]
-        ach = mq_alg / (avg_all["t1_mq_ms"] * 1e-3) / 1e9
+        ach = mq_alg / (avg_all["t1_mq_ms"] * 1e-3) / 1e9 if avg_all["t1_mq_ms"] > 0 else 0.0
         dwt_alg = dwt_bytes_per_px(C, 1, L) * npx
         dwt_alone = float(np.mean([x["dwt_ms"] for x in alone]))
         traffic, traffic_src = pmc_traffic(dom)
@@ -416,6 +430,10 @@ def run_c4(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # single-box rehearsal of the N-rank path: every rank on one GPU
+    # (JP2HIP_BENCH_DEVICE=0, with JP2HIP_BENCH_BACKEND=gloo)
+    if os.environ.get("JP2HIP_BENCH_DEVICE"):
+        local = int(os.environ["JP2HIP_BENCH_DEVICE"])
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="gloo")
@@ -516,6 +534,10 @@ def run_c5(args):
     dt_max = barrier_max(world, dt, device)
     npx = C5["w"] * C5["h"]
     value = npx / 1e6 * args.steps / dt_max
+    # the parts tile the file: their sizes add up to its length on every rank
+    parts_total = allreduce_sum(world, len(part), device)
+    if parts_total != flen:
+        raise SystemExit(f"C5: parts add up to {parts_total} bytes, file length {flen}")
     if rank != 0:
         return None
     avg = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
@@ -529,7 +551,8 @@ def run_c5(args):
                                "tile-split across ranks (bands of tile rows, RCCL all-reduce of PCRD sums)",
                    "image": "40000x30000x1 u16", "parallelism": f"tile-split x{world}",
                    "file_bytes": int(flen), "bpp": round(8 * flen / npx, 4),
-                   "rank0_rows": list(rows), "rank0_part_bytes": len(part)},
+                   "rank0_rows": list(rows), "rank0_part_bytes": len(part), "parts_total_bytes": parts_total,
+                   "backend": os.environ.get("JP2HIP_BENCH_BACKEND", "nccl") if world > 1 else None},
         "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),

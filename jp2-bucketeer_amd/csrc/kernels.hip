@@ -540,15 +540,20 @@ struct QuantArgs {
     uint8_t *P;
     int64_t *dref, *dsig;  // [block][32]
     uint32_t *est;         // [block][32] predicted coded size of plane p, 1/16 bit
-    int max_mb;            // largest Mb of the plan (LDS: max_mb * 512 bytes)
+    int max_mb;            // largest Mb of the plan (LDS: max_mb * 512 bytes per wave)
+    int nblocks;
 };
 
+constexpr int kQuantWaves = 4;  // code-blocks (waves) per workgroup
 template <bool REV>
-__global__ void __launch_bounds__(64) k_quant(QuantArgs a) {
-    extern __shared__ uint64_t planes[];  // [plane][lane], a.max_mb planes
-    int b = blockIdx.x;
+__global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
+    extern __shared__ uint64_t lds_planes[];  // [wave][plane][lane], a.max_mb planes per wave
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x * kQuantWaves + wv;
+    if (b >= a.nblocks) return;
+    uint64_t *planes = lds_planes + (size_t)wv * a.max_mb * 64;
     BlockDesc d = a.blocks[b];
-    int lane = threadIdx.x;
+    int lane = threadIdx.x & 63;
     bool act = lane < d.w;
     const int32_t *src = (const int32_t *)a.coef + (size_t)d.tc * a.plane_w * a.plane_h +
                          (size_t)d.y0 * a.plane_w + d.x0 + (act ? lane : 0);
@@ -1259,12 +1264,14 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.dref = (int64_t *)dref.ptr;
     qa.dsig = (int64_t *)dsig.ptr;
     qa.est = (uint32_t *)est.ptr;
+    qa.nblocks = nb;
     qa.max_mb = 1;
     for (int i = 0; i < nb; i++) qa.max_mb = std::max(qa.max_mb, (int)plan.blocks[i].Mb);
     const size_t qlds = (size_t)qa.max_mb * 64 * sizeof(uint64_t);
     for (int r = 0; nb && r < nrep_quant; r++) {
-        if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, dim3(nb), dim3(64), qlds, stream, qa);
-        else hipLaunchKernelGGL(k_quant<false>, dim3(nb), dim3(64), qlds, stream, qa);
+        const dim3 gq((nb + kQuantWaves - 1) / kQuantWaves), bq(64 * kQuantWaves);
+        if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, gq, bq, qlds * kQuantWaves, stream, qa);
+        else hipLaunchKernelGGL(k_quant<false>, gq, bq, qlds * kQuantWaves, stream, qa);
     }
     HIPCHECK(hipGetLastError());
     // S4b: slope prediction -> lowest coded plane per block
@@ -1396,6 +1403,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         ma.lanes = std::max(1, std::min(64, e ? atoi(e) : 64));
     }
     ma.dbg = nullptr;
+
     if (!ensure<unsigned long long>(mqspan, 2, err)) return false;
     HIPCHECK(hipMemsetAsync(mqspan.ptr, 0xFF, sizeof(unsigned long long), stream));
     HIPCHECK(hipMemsetAsync((unsigned long long *)mqspan.ptr + 1, 0, sizeof(unsigned long long), stream));
@@ -1405,6 +1413,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         ma.dbg = (int64_t *)dbgbuf.ptr;
     }
     for (int r = 0; r < nrep_mq; r++) launch_t1_mq(ma, stream);
+
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[4], stream));
     for (int rp = 0; rp < nrep_pcrd; rp++) {

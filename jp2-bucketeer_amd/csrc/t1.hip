@@ -823,6 +823,7 @@ __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     __shared__ uint32_t cxs[20 * 64];  // 19 contexts + CX_PAD, lane-interleaved
     __shared__ uint32_t mqt[48];
     __shared__ uint32_t rings[64 * 17];  // 68 bytes per lane: 64-byte ring + dummy slot
+
     if (threadIdx.x == 0) atomicMin(&a.span[0], (unsigned long long)wall_clock64());
     const int lane = threadIdx.x;
     if (lane < 47)
