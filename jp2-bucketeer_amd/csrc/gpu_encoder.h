@@ -22,6 +22,29 @@ struct StageTimes {
 
 struct T2Args;  // t2_device.hip
 
+// compressed strips / tiles -> uncompressed staging copy (kernels.hip, lzw.hip)
+struct UnpackArgs {
+    const uint8_t *src;
+    const uint64_t *off, *cnt;  // per strip (tile): byte offset and compressed size
+    int nstrips, per_plane, rps, h;
+    uint64_t row_bytes, stride;  // decoded row and strip stride (bytes)
+    uint64_t unit_bytes;         // tiles: every unit decodes to this many bytes
+    uint8_t *dst;
+    const int *only;  // k_unlzw: decode only strips with only[s] != 0 (nullptr: all)
+    int *err;
+};
+__host__ __device__ inline uint64_t strip_out_bytes(const UnpackArgs &a, int s) {
+    if (a.unit_bytes) return a.unit_bytes;
+    const int y0 = (s % a.per_plane) * a.rps;
+    return (uint64_t)(a.rps < a.h - y0 ? a.rps : a.h - y0) * a.row_bytes;
+}
+// LZW strips, segment-parallel (lzw.hip): lzw_slices() lays out each
+// strip's segment slots (returns their total), the caller uploads `slice` to
+// the start of `scratch` (lzw_scratch_bytes); false on a launch error
+uint64_t lzw_slices(const uint64_t *strip_bytes, int nstrips, std::vector<uint64_t> &slice);
+size_t lzw_scratch_bytes(int nstrips, uint64_t segs);
+bool launch_lzw(const UnpackArgs &u, uint64_t segs, void *scratch, hipStream_t st);
+
 // tier-1 kernels (t1.hip)
 struct T1CmArgs {
     const int2 *items;   // (block, plane)
@@ -168,7 +191,7 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        est, hist, kcut, pmin, mqspan, stage, soff, lzwtab, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
         dbgbuf, t1ord, t1flags, t1pos, slotbytes, nitems_d;
     // device tier-2 (t2_device.hip)
     DevBuf hdist, rstate;

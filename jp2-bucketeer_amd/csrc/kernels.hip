@@ -113,22 +113,6 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
 // staging buffer, so ingest then reads an uncompressed layout.  Horizontal
 // differencing (Predictor 2) is undone afterwards, one lane per row.
 // --------------------------------------------------------------------------
-struct UnpackArgs {
-    const uint8_t *src;
-    const uint64_t *off, *cnt;  // per strip (tile): byte offset and compressed size
-    int nstrips, per_plane, rps, h;
-    uint64_t row_bytes, stride;  // decoded row and strip stride (bytes)
-    uint64_t unit_bytes;         // tiles: every unit decodes to this many bytes
-    uint8_t *dst;
-    uint32_t *tab;  // unused (the LZW string table lives in LDS)
-    int *err;
-};
-
-__device__ __forceinline__ uint64_t strip_out_bytes(const UnpackArgs &a, int s) {
-    if (a.unit_bytes) return a.unit_bytes;
-    const int y0 = (s % a.per_plane) * a.rps;
-    return (uint64_t)min(a.rps, a.h - y0) * a.row_bytes;
-}
 
 // LZW, MSB-first codes of 9..12 bits with TIFF's early width change; the
 // string of table entry k is (start, length) inside the strip's own output
@@ -141,7 +125,7 @@ __device__ __forceinline__ uint64_t strip_out_bytes(const UnpackArgs &a, int s) 
 __global__ void __launch_bounds__(64) k_unlzw(UnpackArgs a) {
     __shared__ uint2 tab[4096];
     const int s = blockIdx.x;
-    if (s >= a.nstrips || threadIdx.x) return;
+    if (s >= a.nstrips || threadIdx.x || (a.only && !a.only[s])) return;
     const uint8_t *in = a.src + a.off[s];
     const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
@@ -968,7 +952,7 @@ GpuEncoder::~GpuEncoder() {
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
                      &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
-                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwtab, &untiled,
+                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
                      &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d};
@@ -1094,9 +1078,21 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
         ua.stride = stride;
         ua.unit_bytes = tiled ? (uint64_t)unit_h * row_bytes : 0;
         ua.dst = (uint8_t *)stage.ptr;
-        ua.tab = nullptr;
+        ua.only = nullptr;
         ua.err = (int *)this->err.ptr;
-        if (lay.compression == 5) hipLaunchKernelGGL(k_unlzw, dim3(ns), dim3(1), 0, stream, ua);
+        if (lay.compression == 5 && getenv("JP2HIP_LZW_SERIAL")) {  // experiment knob: one lane per strip
+            hipLaunchKernelGGL(k_unlzw, dim3(ns), dim3(1), 0, stream, ua);
+        } else if (lay.compression == 5) {  // segment-parallel (lzw.hip)
+            std::vector<uint64_t> slice;
+            const uint64_t segs = lzw_slices(lay.strip_bytes, ns, slice);
+            if (!ensure<uint8_t>(lzwseg, lzw_scratch_bytes(ns, segs), err) ||
+                !h2d(lzwseg.ptr, slice.data(), sizeof(uint64_t) * ns, err))
+                return false;
+            if (!launch_lzw(ua, segs, lzwseg.ptr, stream)) {
+                err = std::string("LZW launch failed: ") + hipGetErrorString(hipGetLastError());
+                return false;
+            }
+        }
         else if (lay.compression == 8 || lay.compression == 32946)
             hipLaunchKernelGGL(k_inflate, dim3(ns), dim3(1), 0, stream, ua);
         else hipLaunchKernelGGL(k_unpackbits, dim3(ns), dim3(64), 0, stream, ua);
