@@ -85,9 +85,56 @@ def synth_gray16_rows(row0, row1, w, seed=5, band=512):
     return out
 
 
+def lzw_encode(data: bytes, clear_every: int | None = None, clear_when_full: bool = True) -> bytes:
+    """TIFF 6.0 LZW (MSB-first, early width change) of one strip -- test
+    fixture generator for encoder variants libtiff does not produce: a Clear
+    every `clear_every` codes (libtiff clears only when the dictionary is
+    full; libtiff decodes both, checked against Pillow in test_oracle.py).
+    clear_when_full=False writes no Clear at all, a stream libtiff rejects."""
+    def width(k):  # the k-th code after a Clear (the decoder's rule)
+        return 9 if k < 254 else 10 if k < 766 else 11 if k < 1790 else 12
+
+    acc, nacc, out = 0, 0, bytearray()
+
+    def put(code, w):
+        nonlocal acc, nacc
+        acc = (acc << w) | code
+        nacc += w
+        while nacc >= 8:
+            nacc -= 8
+            out.append((acc >> nacc) & 0xFF)
+        acc &= (1 << nacc) - 1
+
+    table, k = {}, 0
+    put(256, 9)
+    cur = b""
+    for byte in data:
+        nxt = cur + bytes([byte])
+        if not cur or nxt in table:
+            cur = nxt
+            continue
+        put(cur[0] if len(cur) == 1 else table[cur], width(k))
+        if 258 + k <= 4095:
+            table[nxt] = 258 + k
+        k += 1
+        full = 258 + k > 4095
+        if (clear_every and k >= clear_every) or (full and clear_when_full):
+            put(256, width(k))
+            table, k = {}, 0
+        cur = bytes([byte])
+    if cur:
+        put(cur[0] if len(cur) == 1 else table[cur], width(k))
+        k += 1
+    put(257, width(k))
+    if nacc:
+        out.append((acc << (8 - nacc)) & 0xFF)
+    return bytes(out)
+
+
 def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=False,
-               alpha=None) -> bytes:
-    """Uncompressed baseline TIFF (strips), 8/16-bit, 1-4 samples."""
+               alpha=None, strip_codec=None, compression=1) -> bytes:
+    """Baseline TIFF (strips), 8/16-bit, 1-4 samples; uncompressed, or each
+    strip passed through `strip_codec` (then tagged `compression`)."""
     if img.ndim == 2:
         img = img[..., None]
     h, w, nc = img.shape
@@ -101,6 +148,8 @@ def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=Fals
         for s in range(nstrip):
             blk = np.ascontiguousarray(pl[s * rps:(s + 1) * rps])
             strips.append(blk.astype(blk.dtype.newbyteorder(e)).tobytes())
+    if strip_codec is not None:
+        strips = [strip_codec(x) for x in strips]
     ntags = 11 + (1 if nc in (2, 4) else 0)
     ifd_off = 8
     ifd_size = 2 + 12 * ntags + 4
@@ -148,7 +197,7 @@ def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=Fals
         tag(258, 3, 2, (bits, bits))
     else:
         tag(258, 3, nc, bps_off, inline=False)
-    tag(259, 3, 1, 1)
+    tag(259, 3, 1, compression)
     tag(262, 3, 1, 2 if nc >= 3 else 1)
     tag(273, 4, nst, offs[0] if nst == 1 else so_off, inline=(nst == 1))
     tag(277, 3, 1, nc)

@@ -268,6 +268,20 @@ def test_compressed_strip_longer_than_needed_is_cut(encoder, comp):
     assert got == want
 
 
+@pytest.mark.parametrize("clear_every", [700, 3000, 1])
+def test_lzw_encoder_variants_same_output(encoder, clear_every):
+    """LZW strips from an encoder that clears early (every 700 / 3000 codes:
+    more, shorter segments) or after every code (more segments than the
+    segment tables hold: the serial decoder takes the strip) decode to the
+    same pixels as libtiff's strips (tests/imaging.py lzw_encode)."""
+    img = im.synth_rgb8(300, 400, seed=11)
+    data = im.tiff_bytes(img, rows_per_strip=64, compression=5,
+                         strip_codec=lambda x: im.lzw_encode(x, clear_every=clear_every))
+    got, _ = encoder.encode_tiff(data, jp2hip.LOSSY)
+    want, _ = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSY)
+    assert got == want
+
+
 def test_old_style_lzw_rejected_by_name(encoder):
     img = im.synth_rgb8(32, 32, seed=1)
     data = bytearray(im.tiff_bytes_compressed(img, "tiff_lzw", rows_per_strip=32))

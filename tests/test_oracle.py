@@ -186,3 +186,15 @@ def test_oracle_slope_prediction_inactive_for_lossless():
     a = ol.encode(img, ol.recipe(True, format=0, slope_skip=1))
     b = ol.encode(img, ol.recipe(True, format=0, slope_skip=0))
     assert a == b
+
+
+@pytest.mark.parametrize("clear_every", [1, 700, 3000, None])
+def test_lzw_fixture_encoder_decodes_in_libtiff(clear_every):
+    """The LZW encoder variants the GPU tests feed (imaging.lzw_encode) are
+    valid TIFF LZW: Pillow's libtiff decodes them to the source pixels."""
+    import io
+    from PIL import Image
+    img = im.synth_rgb8(150, 200, seed=5)
+    data = im.tiff_bytes(img, rows_per_strip=64, compression=5,
+                         strip_codec=lambda x: im.lzw_encode(x, clear_every=clear_every))
+    assert np.array_equal(np.array(Image.open(io.BytesIO(data))), img)
