@@ -372,7 +372,8 @@ def run(args):
                              "alone": {"stage_ms": round(dwt_alone, 4),
                                        "achieved": round(dwt_alg / (dwt_alone * 1e-3) / 1e9, 2),
                                        "frac": round(dwt_alg / (dwt_alone * 1e-3) / HBM_PEAK, 5)}},
-            "t1_counters": {"k_t1_mq": sq_counters("k_t1_mq"), "k_t1_cm": sq_counters("k_t1_cm")},
+            "t1_counters": {"k_t1_mq": sq_counters("k_t1_mq"), "k_t1_cm3": sq_counters("k_t1_cm3"),
+                            "k_quant": sq_counters("k_quant")},
             "stages_ms": {k: round(avg[k], 4) for k in ("ingest_ms", "dwt_ms", "quant_ms", "t1_cm_ms",
                                                         "t1_mq_ms", "pcrd_ms", "d2h_ms", "t2_ms",
                                                         "total_ms")},

@@ -351,7 +351,7 @@ __device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const ui
 // and the output reaches HBM from the window in 16-byte stores every 4 KB
 // (per-byte global stores would make every input refill wait on them).
 __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
-    constexpr int LB = 10, DB = 8;
+    constexpr int LB = 12, DB = 9;
     constexpr uint32_t WM = 32767;
     __shared__ uint16_t lcnt[16], lsym[288], dcnt[16], dsym[32], lfast[1 << LB], dfast[1 << DB];
     __shared__ uint8_t lens[320];
@@ -525,6 +525,7 @@ struct QuantArgs {
     int64_t *dref, *dsig;  // [block][32]
     uint32_t *est;         // [block][32] predicted coded size of plane p, 1/16 bit
     int max_mb;            // largest Mb of the plan (LDS: max_mb * 512 bytes per wave)
+    int keep_sm;           // write the sign-magnitude copy of every block (debug dumps)
     int nblocks;
 };
 
@@ -542,6 +543,9 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     const int32_t *src = (const int32_t *)a.coef + (size_t)d.tc * a.plane_w * a.plane_h +
                          (size_t)d.y0 * a.plane_w + d.x0 + (act ? lane : 0);
     int32_t *sm = a.sm + d.sm_off + lane;
+    // the sign-magnitude copy is read only by the 64-bit distortion path of
+    // planes above 23 (below) and by the debug dumps
+    const bool keep_sm = a.keep_sm || d.Mb > 24;
     uint32_t vmax = 0;
     uint32_t lim = (1u << d.Mb) - 1u;
     // the lane's column stays in registers (sign | magnitude; 0 outside the
@@ -565,7 +569,7 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
         }
         v = act ? min(v, lim) : 0u;
         col[y] = act ? (s << 31) | v : 0u;
-        sm[y * 64] = (int32_t)col[y];
+        if (keep_sm) sm[y * 64] = (int32_t)col[y];
         vmax = max(vmax, v);
     }
 #pragma unroll
@@ -1261,6 +1265,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.dsig = (int64_t *)dsig.ptr;
     qa.est = (uint32_t *)est.ptr;
     qa.nblocks = nb;
+    qa.keep_sm = dd != nullptr;
     qa.max_mb = 1;
     for (int i = 0; i < nb; i++) qa.max_mb = std::max(qa.max_mb, (int)plan.blocks[i].Mb);
     const size_t qlds = (size_t)qa.max_mb * 64 * sizeof(uint64_t);

@@ -39,7 +39,6 @@ enum { CX_RL = 17, CX_UNI = 18, CX_PAD = 19 };
 // validity test.
 constexpr uint8_t kPadDecision = CX_PAD << 1;
 
-__device__ __forceinline__ uint32_t bit(uint64_t m, int c) { return (uint32_t)(m >> c) & 1u; }
 
 // bytes reserved per (block, plane) for the three passes' decisions:
 // at most w*h coding decisions + w*h sign decisions + 3 per run-length column
@@ -49,43 +48,11 @@ __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
     return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
 }
 
-// A lane's decisions inside one stripe (<= 10), as bytes (context << 1) | d.
-struct LaneDec {
-    uint64_t lo, hi;
-    int n;
-    __device__ __forceinline__ void put(uint32_t cx, uint32_t d) {
-        const uint64_t byte = (uint64_t)((cx << 1) | d);
-        if (n < 8) lo |= byte << (n * 8);
-        else hi |= byte << ((n - 8) * 8);
-        n++;
-    }
-};
-
-// Pass end: neutral decisions up to the next 16-byte boundary.
-__device__ __forceinline__ int pad_pass(uint8_t *out, int pos, int lane) {
-    const int end = (pos + 15) & ~15;
-    if (lane < end - pos) out[pos + lane] = kPadDecision;
-    return end;
-}
-
-// Stripe hand-off: the lanes' decisions go out in column order (lane c =
-// column c): exclusive prefix of the per-lane counts over the wave, then
-// each lane stores its bytes.  Returns the stripe's decision count.
-__device__ __forceinline__ int flush_stripe(uint8_t *out, int base, const LaneDec &e, int lane) {
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t b0 = __ballot(e.n & 1), b1 = __ballot(e.n & 2), b2 = __ballot(e.n & 4), b3 = __ballot(e.n & 8);
-    const int excl = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt) + 8 * __popcll(b3 & lt);
-    const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3);
-    uint8_t *o = out + base + excl;
-    for (int i = 0; i < e.n; i++) o[i] = (uint8_t)(i < 8 ? (e.lo >> (i * 8)) : (e.hi >> ((i - 8) * 8)));
-    return total;
-}
-
 constexpr int kCmWaves = 4;  // items per workgroup
 
 // --------------------------------------------------------------------------
-// Context modelling on column masks (k_t1_cm2; k_t1_cm3 below is the default).
-// One wavefront per (code-block, bit-plane) item, in the transposed layout: lane
+// Context modelling on column masks.  One wavefront per (code-block,
+// bit-plane) item, in the transposed layout: lane
 // c holds column c of every mask as a 64-bit word (bit r = row r; k_quant
 // writes them), so a vertical neighbour is a bit shift inside the lane and a
 // horizontal one is the next lane.  The neighbourhood and context rules then
@@ -203,175 +170,9 @@ __device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, u
     return c;
 }
 
-// per stripe: a mask's bits of rows 4s .. 4s+3 at bits 0..3
-__device__ __forceinline__ uint32_t nib4(uint64_t m, int sh) { return (uint32_t)(m >> sh) & 0xFu; }
-__device__ __forceinline__ uint32_t bitq(uint32_t x, int q) { return (x >> q) & 1u; }
-
-__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm2(T1CmArgs a) {
-    if ((int)blockIdx.x * kCmWaves >= *a.nitems) return;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gi = blockIdx.x * kCmWaves + wv;
-    if (gi >= *a.nitems) return;
-    const int2 item = a.items[gi];
-    const int b = item.x, p = item.y;
-    const BlockDesc d = a.blocks[b];
-    const int P = a.P[b];
-    const int k = P - 1 - p;
-    const bool lossless = a.lossless != 0;
-    const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
-    const bool vl = lane < w;
-    const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;  // this column's rows
-    const uint64_t *CT = a.bp + d.bp_off;  // column masks (k_quant)
-    const uint64_t B = vl ? CT[(size_t)p * 64 + lane] : 0ull;
-    const uint64_t S0 = vl ? CT[(size_t)(Mb + p) * 64 + lane] : 0ull;
-    const uint64_t S1 = (vl && p + 1 < P) ? CT[(size_t)(Mb + p + 1) * 64 + lane] : 0ull;
-    const uint64_t S2 = (vl && p + 2 < P) ? CT[(size_t)(Mb + p + 2) * 64 + lane] : 0ull;
-    const uint64_t SG = vl ? CT[(size_t)2 * Mb * 64 + lane] : 0ull;
-    const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
-    const int nstripes = (h + 3) >> 2;
-    uint8_t *out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
-    int n_spp = 0, n_mrp = 0, pos = 0;
-    const bool spp = p < P - 1;
-    const uint64_t LS1 = col_left(S1, lane), RS1 = col_right(S1, lane);
-    uint64_t N = 0, memS = 0;
-    if (spp) {
-        // ---- significance propagation: least fixed point of the causal rule ----
-        for (;;) {
-            const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
-            const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
-            const uint64_t cand = ~S1 & VR & (nb.UL | nb.U | nb.UR | nb.L | nb.R | nb.DL | nb.D | nb.DR);
-            const uint64_t Nn = cand & B;
-            if (!__any(Nn != N)) {
-                memS = cand;
-                break;
-            }
-            N = Nn;
-        }
-        const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
-        const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
-        const Ctx4 z = zc_masks(band, nb);
-        // sign: L (visited) in Vb, R (not) in Va = S1, U in Vb, D in S1
-        const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
-        for (int s = 0; s < nstripes; s++) {
-            const int sh = s * 4;
-            const uint32_t mem = nib4(memS, sh);
-            LaneDec e{0, 0, 0};
-            if (mem) {
-                const uint32_t bb = nib4(B, sh), z0 = nib4(z.b0, sh), z1 = nib4(z.b1, sh), z2 = nib4(z.b2, sh),
-                               z3 = nib4(z.b3, sh), c0 = nib4(sc.b0, sh), c1 = nib4(sc.b1, sh),
-                               c2 = nib4(sc.b2, sh), xr = nib4(sc.xr, sh), sg = nib4(SG, sh);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (!bitq(mem, q)) continue;
-                    const uint32_t bv = bitq(bb, q);
-                    e.put(bitq(z0, q) | (bitq(z1, q) << 1) | (bitq(z2, q) << 2) | (bitq(z3, q) << 3), bv);
-                    if (bv) e.put(8u | bitq(c0, q) | (bitq(c1, q) << 1) | (bitq(c2, q) << 2), bitq(sg ^ xr, q));
-                }
-            }
-            if (__any(e.n)) pos += flush_stripe(out, pos, e, lane);
-        }
-        n_spp = pos;
-        pos = pad_pass(out, pos, lane);
-        const int mrp0 = pos;
-        // ---- magnitude refinement: neighbours in the post-SPP state ----
-        const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
-        const uint64_t anyn = (Pst << 1) | (Pst >> 1) | LP | RP | (LP << 1) | (RP << 1) | (LP >> 1) | (RP >> 1);
-        const uint64_t memM = S1 & VR, fr = S1 & ~S2;
-        for (int s = 0; s < nstripes; s++) {
-            const int sh = s * 4;
-            const uint32_t mem = nib4(memM, sh);
-            LaneDec e{0, 0, 0};
-            if (mem) {
-                const uint32_t bb = nib4(B, sh), f = nib4(fr, sh), an = nib4(anyn, sh);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (!bitq(mem, q)) continue;
-                    const uint32_t ctx = bitq(f, q) ? (bitq(an, q) ? 15u : 14u) : 16u;
-                    e.put(ctx, bitq(bb, q));
-                }
-            }
-            if (__any(e.n)) pos += flush_stripe(out, pos, e, lane);
-        }
-        n_mrp = pos - mrp0;
-        pos = pad_pass(out, pos, lane);
-    }
-    const int cup0 = pos;
-    // ---- cleanup: visited neighbours in S[p], the others post-SPP ----
-    {
-        const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
-        const uint64_t LS0 = col_left(S0, lane), RS0 = col_right(S0, lane);
-        const Nbr8 nb = nbr8(S0, Pst, LS0, RS0, LP, RP);
-        const Ctx4 z = zc_masks(band, nb);
-        const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
-        const uint64_t memC = ~S1 & ~memS & VR;
-        // run-length: four members and no significant neighbour -- left
-        // column (visited) in S[p], right column post-SPP, the row above in
-        // S[p], the row below post-SPP
-        const uint64_t side = LS0 | RP, above = S0 | LS0 | RS0, below = Pst | LP | RP;
-        for (int s = 0; s < nstripes; s++) {
-            const int sh = s * 4, nr = min(4, h - sh);
-            const uint32_t mem = nib4(memC, sh);
-            LaneDec e{0, 0, 0};
-            if (mem) {
-                const uint32_t bb = nib4(B, sh), z0 = nib4(z.b0, sh), z1 = nib4(z.b1, sh), z2 = nib4(z.b2, sh),
-                               z3 = nib4(z.b3, sh), c0 = nib4(sc.b0, sh), c1 = nib4(sc.b1, sh),
-                               c2 = nib4(sc.b2, sh), xr = nib4(sc.xr, sh), sg = nib4(SG, sh);
-                int qstart = 0;
-                const bool rl = nr == 4 && mem == 0xFu && nib4(side, sh) == 0 &&
-                                (sh == 0 || ((above >> (sh - 1)) & 1ull) == 0) &&
-                                (sh + 4 >= 64 || ((below >> (sh + 4)) & 1ull) == 0);
-                if (rl) {
-                    if (bb == 0) {
-                        e.put(CX_RL, 0);
-                        qstart = 4;
-                    } else {
-                        const int r = __builtin_ctz(bb);
-                        e.put(CX_RL, 1);
-                        e.put(CX_UNI, (uint32_t)r >> 1);
-                        e.put(CX_UNI, (uint32_t)r & 1u);
-                        e.put(8u | bitq(c0, r) | (bitq(c1, r) << 1) | (bitq(c2, r) << 2), bitq(sg ^ xr, r));
-                        qstart = r + 1;
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (q < qstart || !bitq(mem, q)) continue;
-                    const uint32_t bv = bitq(bb, q);
-                    e.put(bitq(z0, q) | (bitq(z1, q) << 1) | (bitq(z2, q) << 2) | (bitq(z3, q) << 3), bv);
-                    if (bv) e.put(8u | bitq(c0, q) | (bitq(c1, q) << 1) | (bitq(c2, q) << 2), bitq(sg ^ xr, q));
-                }
-            }
-            if (__any(e.n)) pos += flush_stripe(out, pos, e, lane);
-        }
-    }
-    const int n_cup = pos - cup0;
-    pad_pass(out, pos, lane);
-    int64_t dspp = 0;
-    if (spp && N) {  // SPP distortion decrease: this column's newly significant samples
-        const int32_t *SMc = a.sm + d.sm_off + lane;
-        uint64_t m = N;
-        while (m) {
-            const int r = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1;
-            dspp += dist_gain((uint32_t)SMc[(size_t)r * 64] & 0x7FFFFFFFu, p, lossless);
-        }
-    }
-    dspp = wave_sum64(dspp);
-    if (lane == 0) {
-        uint4 cnt;
-        cnt.x = (uint32_t)n_spp;
-        cnt.y = (uint32_t)n_mrp;
-        cnt.z = (uint32_t)n_cup;
-        cnt.w = 0;
-        a.counts[(size_t)b * 32 + k] = cnt;
-        a.dspp[(size_t)b * 32 + k] = dspp;
-    }
-}
 
 // --------------------------------------------------------------------------
-// k_t1_cm3 (the default): the masks and contexts of k_t1_cm2, with a
-// branch-free stripe step and LDS-staged output.
+// k_t1_cm3: the stripe step, branch-free, and LDS-staged output.
 //
 // Per stripe a lane (column) builds its four rows' decision bytes at once,
 // one byte per row in a dword: the zero-coding byte (ctx << 1 | bit) and the
@@ -380,7 +181,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm2(T1CmArgs a) {
 // member samples' bytes are compacted in scan order by two v_perm_b32 whose
 // selectors come from a 256-entry table indexed by (members | members with a
 // 1 bit << 4) -- no per-sample branch.  The wave's lanes place their <= 12
-// bytes at an exclusive prefix of the counts (ballots + mbcnt) in a 2 KB LDS
+// bytes at an exclusive prefix of the counts (DPP wave scan) in a 2 KB LDS
 // ring per wave, OR-ing whole dwords (the ring is zero where nothing has
 // been written, and a lane's bytes are zero-padded, so neighbours' partial
 // dwords merge); every full KiB leaves the ring in one 16-byte store per lane.
@@ -642,17 +443,21 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         }
         const int n_cup = g.pos - cup0;
         ring_pass_end(g, lane);
-        int64_t dspp = 0;
-        if (spp && N) {  // SPP distortion decrease: this column's newly significant samples
-            const int32_t *SMc = a.sm + d.sm_off + lane;
-            uint64_t mm = N;
-            while (mm) {
-                const int rr = __ffsll((unsigned long long)mm) - 1;
-                mm &= mm - 1;
-                dspp += dist_gain((uint32_t)SMc[(size_t)rr * 64] & 0x7FFFFFFFu, p, lossless);
-            }
+        // SPP distortion decrease: the newly significant samples N have top bit
+        // p, each gains 2^p (12 v + 6d - 9 2^p) (d = 1 lossy, 0 lossless; 4 at
+        // lossless p = 0), and sum_N v = 2^p |N| + sum_{q<p} 2^q |N & B[q]|
+        // from the column masks of the lower planes (dist_gain, exact)
+        int64_t nN = 0, sv = 0;
+        if (spp && __any(N != 0ull)) {
+            nN = __popcll(N);
+            sv = nN << p;
+            for (int q = 0; q < p; q++)
+                if (vl) sv += (int64_t)__popcll(N & CT[(size_t)q * 64 + lane]) << q;
         }
-        dspp = wave_sum64(dspp);
+        nN = wave_sum64(nN);
+        sv = wave_sum64(sv);
+        const int64_t dspp = (lossless && p == 0) ? 4 * nN
+                                                  : ((12 * sv + (6 * (lossless ? 0 : 1) - 9 * ((int64_t)1 << p)) * nN) << p);
         if (lane == 0) {
             uint4 cnt;
             cnt.x = (uint32_t)n_spp;
@@ -1002,9 +807,7 @@ void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, c
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (!a.max_items) return;
     const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
-    static const char *v = getenv("JP2HIP_CM");  // experiment knob: "2" = the per-sample-branch variant
-    if (v && !strcmp(v, "2")) hipLaunchKernelGGL(k_t1_cm2, g, dim3(64 * kCmWaves), 0, st, a);
-    else hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
+    hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
                     int32_t *vals, hipStream_t st) {
