@@ -562,8 +562,23 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : NC) * bps;
     const int gx0 = (t % a.ntx) * a.tile_w, gy0 = a.row0 + (t / a.ntx) * a.tile_h;
     const bool mct = a.mct && NC >= 3;
-    // strip walk: the strip and row-in-strip of the next row to fetch
-    int strip = (gy0 + s) / a.rps, ly = gy0 + s - strip * a.rps;
+    // byte offset of every streamed row (per component plane when planar),
+    // looked up once: a row fetch is then plain loads with no dependent
+    // global read in front of them, so they stay in flight across the
+    // lifting of the previous rows
+    __shared__ uint64_t rowtab[(kStreamBand + 2 * 4) * NC];
+    {
+        const int ncp = a.planar == 2 ? NC : 1;
+        for (int i = tid; i < (e - s) * ncp; i += kDwtThreads) {
+            const int r = i / ncp, c = i - r * ncp;
+            const int gy = gy0 + s + r;
+            const int strip = gy / a.rps;
+            rowtab[i] = a.strip_off[a.planar == 2 ? (size_t)c * a.spp_strips + strip : (size_t)strip] +
+                        (size_t)(gy - strip * a.rps) * row_bytes;
+        }
+        __syncthreads();
+    }
+    int rnext = 0;  // next row to fetch, counted from s
     int32_t w[CPT][NC][NWIN];
 #pragma unroll
     for (int j = 0; j < CPT; j++)
@@ -574,16 +589,15 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     // raw (level-shifted) samples of the next row pair, fetched one
     // iteration ahead so the loads are in flight during the lifting
     int32_t pf[2][CPT][NC];
+    // raw sample bits only (a u8, or the u16 as stored): the level shift and
+    // byte order wait for place(), so nothing uses a load until the next
+    // iteration
     auto fetch = [&](int q) {  // the next row (s, s+1, ...) into pf[q]
+        const int ncp = a.planar == 2 ? NC : 1;
         uint64_t ro[NC];
 #pragma unroll
-        for (int c = 0; c < NC; c++)
-            ro[c] = a.strip_off[a.planar == 2 ? (size_t)c * a.spp_strips + strip : (size_t)strip] +
-                    (size_t)ly * row_bytes;
-        if (++ly == a.rps) {
-            ly = 0;
-            strip++;
-        }
+        for (int c = 0; c < NC; c++) ro[c] = rowtab[rnext * ncp + (a.planar == 2 ? c : 0)];
+        rnext++;
 #pragma unroll
         for (int j = 0; j < CPT; j++) {
             const int x = min(tid + j * kDwtThreads, W - 1);  // columns past W repeat the last one
@@ -591,17 +605,20 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
 #pragma unroll
             for (int c = 0; c < NC; c++) {
                 const uint8_t *p8 = a.tif + (a.planar == 2 ? ro[c] : ro[0] + (size_t)c * bps) + xo;
-                int32_t v;
-                if (a.bits == 8) v = (int32_t)p8[0];
-                else v = a.big_endian ? (((int32_t)p8[0] << 8) | p8[1]) : (p8[0] | ((int32_t)p8[1] << 8));
-                pf[q][j][c] = v - off;
+                pf[q][j][c] = a.bits == 8 ? (int32_t)p8[0] : (int32_t)*(const uint16_t *)p8;
             }
         }
     };
     auto place = [&](int q, int slot) {  // colour transform, into window slot `slot`
 #pragma unroll
         for (int j = 0; j < CPT; j++) {
-            const int32_t *smp = pf[q][j];
+            int32_t smp[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const uint32_t r = (uint32_t)pf[q][j][c];
+                const int32_t v = (a.bits != 8 && a.big_endian) ? (int32_t)(((r & 0xFFu) << 8) | (r >> 8)) : (int32_t)r;
+                smp[c] = v - off;
+            }
 #pragma unroll
             for (int c = 0; c < NC; c++) w[j][c][slot] = REV ? smp[c] : __float_as_int((float)smp[c]);
             if constexpr (NC >= 3) if (mct) {
