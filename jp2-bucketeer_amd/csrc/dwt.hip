@@ -736,9 +736,11 @@ struct DwtTailArgs {
 
 // Levels level..levels of one tile-component, entirely in LDS.  1024 threads
 // as 8 rows x 128 columns (no index divisions; a tail level is <= 128 x 128
-// for the recipe's tiles).  Each level works in place on the previous
-// level's LL, which stays where it was computed -- element (i, j) of level
-// k's input at LDS (i << k) * ld + (j << k) -- so no compaction pass.
+// for the recipe's tiles).  Each level works on a dense copy of its input
+// (row stride = its width) and writes the LL it leaves densely into the
+// other buffer for the next level, so every access is unit- or 2-stride
+// (the in-place layout -- element (i, j) of level k at (i << k, j << k) --
+// cost 2^k-way LDS bank conflicts at every step of the deeper levels).
 constexpr int kTailThreads = 1024;
 constexpr int kTailCols = 128, kTailRows = kTailThreads / kTailCols;
 template <bool REV>
@@ -757,38 +759,39 @@ __device__ __forceinline__ void tail_lift(int32_t *x, int idx, int lidx, int rid
 
 template <bool REV>
 __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
-    __shared__ int32_t lds[kDwtLdsWords];
+    __shared__ int32_t bufA[kDwtLdsWords];      // a level's input
+    __shared__ int32_t bufB[kDwtLdsWords / 4];  // the LL it leaves
     const int tc = blockIdx.x;
     const int tx = threadIdx.x & (kTailCols - 1), ty = threadIdx.x / kTailCols;
     int sh = a.level - 1;
     int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh;
     int H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
-    const int ld = W;  // row stride of the level-`level` input
     {
         const int32_t *s = (const int32_t *)a.src + (size_t)tc * a.src_tc;
         for (int y = ty; y < H; y += kTailRows)
-            for (int x = tx; x < W; x += kTailCols) lds[y * ld + x] = s[(size_t)y * a.src_stride + x];
+            for (int x = tx; x < W; x += kTailCols) bufA[y * W + x] = s[(size_t)y * a.src_stride + x];
     }
     __syncthreads();
+    int32_t *cur = bufA, *nxt = bufB;
     int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
     const int nsteps = REV ? 2 : 4;
-    for (int lv = a.level, k = 0; lv <= a.levels; lv++, k++) {
-        const int rs = ld << k, cs = 1 << k;  // strides of this level's samples
+    for (int lv = a.level; lv <= a.levels; lv++) {
+        const int ld = W;
         // vertical lifting (odd rows first), symmetric extension at 0 / H-1
         if (H > 1)
             for (int st = 0; st < nsteps; st++) {
                 const int par = (st & 1) ? 0 : 1;
                 for (int y = par + 2 * ty; y < H; y += 2 * kTailRows) {
                     const int l = y > 0 ? y - 1 : y + 1, r = y + 1 < H ? y + 1 : y - 1;
-                    for (int x = tx; x < W; x += kTailCols) tail_lift<REV>(lds, y * rs + x * cs, l * rs + x * cs, r * rs + x * cs, st);
+                    for (int x = tx; x < W; x += kTailCols) tail_lift<REV>(cur, y * ld + x, l * ld + x, r * ld + x, st);
                 }
                 __syncthreads();
             }
         if (!REV && H > 1) {
-            float *f = (float *)lds;
+            float *f = (float *)cur;
             for (int y = ty; y < H; y += kTailRows)
                 for (int x = tx; x < W; x += kTailCols) {
-                    const int o = y * rs + x * cs;
+                    const int o = y * ld + x;
                     f[o] = (y & 1) ? f[o] * K97 : f[o] * INVK97;
                 }
             __syncthreads();
@@ -799,33 +802,35 @@ __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
                 for (int y = ty; y < H; y += kTailRows)
                     for (int x = par + 2 * tx; x < W; x += 2 * kTailCols) {
                         const int l = x > 0 ? x - 1 : x + 1, r = x + 1 < W ? x + 1 : x - 1;
-                        tail_lift<REV>(lds, y * rs + x * cs, y * rs + l * cs, y * rs + r * cs, st);
+                        tail_lift<REV>(cur, y * ld + x, y * ld + l, y * ld + r, st);
                     }
                 __syncthreads();
             }
         const int nlv = (H + 1) / 2, nlh = (W + 1) / 2;
         const bool last = lv == a.levels;
-        // high bands (and the final LL) straight to HBM; the LL of a
-        // non-final level is scaled in place (each element by its owner)
+        // high bands (and the final LL) straight to HBM; a non-final LL,
+        // scaled, densely into the other buffer
         for (int y = ty; y < H; y += kTailRows) {
             const bool ylo = (y & 1) == 0;
             int32_t *drow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
             for (int j = tx; j < W; j += kTailCols) {
                 const bool lo = j < nlh;
                 const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
-                const int o = y * rs + x * cs;
-                int32_t v = lds[o];
+                int32_t v = cur[y * ld + x];
                 if (!REV && W > 1) {
                     float f = __int_as_float(v);
                     f = lo ? f * INVK97 : f * K97;
                     v = __float_as_int(f);
                 }
-                if (lo && ylo && !last) lds[o] = v;
+                if (lo && ylo && !last) nxt[(y >> 1) * nlh + j] = v;
                 else drow[j] = v;
             }
         }
         if (last) break;
         __syncthreads();
+        int32_t *t = cur;
+        cur = nxt;
+        nxt = t;
         W = nlh;
         H = nlv;
     }
