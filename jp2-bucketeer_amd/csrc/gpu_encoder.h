@@ -98,7 +98,7 @@ void launch_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P, c
 void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, const int32_t *flags,
                      const int32_t *pos, int2 *items, int *nitems, hipStream_t st);
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
-                    int32_t *vals, hipStream_t st);
+                    int32_t *vals, unsigned long long *mq_span, hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
 uint32_t t1_plane_stream_cap(int w, int h);
 

@@ -1329,7 +1329,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         !ensure<int32_t>(t1flags, nflags, err) || !ensure<int32_t>(t1pos, nflags, err) ||
         !ensure<uint64_t>(slotbytes, nb, err) || !ensure<int>(nitems_d, 1, err))
         return false;
-    HIPCHECK(hipMemsetAsync(nitems_d.ptr, 0, sizeof(int), stream));
+    if (!nflags) HIPCHECK(hipMemsetAsync(nitems_d.ptr, 0, sizeof(int), stream));  // else k_t1_items writes it
     launch_t1_flags(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr,
                     (const BlockDesc *)blocks.ptr, (int32_t *)t1flags.ptr, (uint64_t *)slotbytes.ptr, stream);
     HIPCHECK(hipGetLastError());
@@ -1369,8 +1369,9 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     // MQ lane order: blocks by decreasing decision count
     if (!ensure<uint32_t>(ordkey, nb, err) || !ensure<uint32_t>(ordkey2, nb, err) || !ensure<int32_t>(ordval, nb, err))
         return false;
+    if (!ensure<unsigned long long>(mqspan, 2, err)) return false;
     launch_t1_keys(nb, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr, (const uint4 *)counts.ptr,
-                   (uint32_t *)ordkey.ptr, (int32_t *)ordval.ptr, stream);
+                   (uint32_t *)ordkey.ptr, (int32_t *)ordval.ptr, (unsigned long long *)mqspan.ptr, stream);
     HIPCHECK(hipGetLastError());
     if (nb) {
         size_t tb = 0;
@@ -1406,8 +1407,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ma.dbg = nullptr;
 
     if (!ensure<unsigned long long>(mqspan, 2, err)) return false;
-    HIPCHECK(hipMemsetAsync(mqspan.ptr, 0xFF, sizeof(unsigned long long), stream));
-    HIPCHECK(hipMemsetAsync((unsigned long long *)mqspan.ptr + 1, 0, sizeof(unsigned long long), stream));
     ma.span = (unsigned long long *)mqspan.ptr;
     if (dd) {
         if (!ensure<int64_t>(dbgbuf, (size_t)nb * 4, err)) return false;

@@ -752,9 +752,15 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
 // Tier-1 lane order: blocks by decreasing decision count (all passes), so the
 // lanes of a wave carry similar work.  keys = ~count: an ascending radix sort
 // yields the descending order.
+// Also resets k_t1_mq's execution-span slots (earliest start, latest end).
 __global__ void __launch_bounds__(256) k_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin,
-                                                 const uint4 *counts, uint32_t *keys, int32_t *vals) {
+                                                 const uint4 *counts, uint32_t *keys, int32_t *vals,
+                                                 unsigned long long *span) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b == 0 && span) {
+        span[0] = ~0ull;
+        span[1] = 0ull;
+    }
     if (b >= nblocks) return;
     uint32_t n = 0;
     const int pc = P[b] ? P[b] - pmin[b] : 0;
@@ -810,10 +816,9 @@ void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
-                    int32_t *vals, hipStream_t st) {
-    if (nblocks)
-        hipLaunchKernelGGL(k_t1_keys, dim3((nblocks + 255) / 256), dim3(256), 0, st, nblocks, P, pmin, counts, keys,
-                           vals);
+                    int32_t *vals, unsigned long long *span, hipStream_t st) {
+    hipLaunchKernelGGL(k_t1_keys, dim3(std::max(1, (nblocks + 255) / 256)), dim3(256), 0, st, nblocks, P, pmin,
+                       counts, keys, vals, span);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
     if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + a.lanes - 1) / a.lanes), dim3(64), 0, st, a);
