@@ -306,10 +306,12 @@ def run(args):
         avg = {k: float(np.mean([s[k] for s in flat])) for k in flat[0]}
         every = flat + all_stats
         avg_all = {k: float(np.mean([s[k] for s in every])) for k in every[0]}
-        # the dominant kernel by rocprofv3 kernel time (~50 % of all kernel
-        # time, profiles/r02/c2_kernel_stats*.csv): k_t1_mq, whose time is its
-        # own execution span (wall clock read inside the kernel, as rocprofv3
-        # measures it)
+        # the dominant kernel by rocprofv3 kernel time (~60 % of all kernel
+        # time, profiles/r02/final/kernel_stats_*.csv): k_t1_mq, timed with
+        # HIP events on its context's stream around the launch (what
+        # rocprofv3's dispatch duration measures; under load that includes
+        # waiting for CUs other images hold), averaged over every launch of
+        # this run
         dom = "k_t1_mq"
         C, L = 3, 6
         npx = img.shape[0] * img.shape[1]

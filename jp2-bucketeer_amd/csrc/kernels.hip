@@ -1504,8 +1504,13 @@ bool GpuEncoder::collect_profile(StageTimes &st, std::string &err) {
     HIPCHECK(hipEventElapsedTime(&t, ev[1], ev[2])); st.dwt = t;
     HIPCHECK(hipEventElapsedTime(&t, ev[2], ev[3])); st.quant = t;
     HIPCHECK(hipEventElapsedTime(&t, ev[10], ev[11])); st.t1_cm = t;
-    // k_t1_mq's own execution span (100 MHz wall clock, see t1.hip)
-    st.t1_mq = span[1] > span[0] ? (double)(span[1] - span[0]) * 1e-5 : 0.0;
+    // k_t1_mq from HIP events on the context's stream around its launch, as
+    // rocprofv3 times a dispatch (from when the queue reaches it: under load
+    // that includes waiting for CUs).  span[] is the kernel's own execution
+    // span (first wave start .. last lane end, 100 MHz wall clock), kept for
+    // the MQ census tool.
+    HIPCHECK(hipEventElapsedTime(&t, ev[11], ev[4])); st.t1_mq = t;
+    (void)span;
     HIPCHECK(hipEventElapsedTime(&t, ev[4], ev[5])); st.pcrd += t;
     return true;
 }
