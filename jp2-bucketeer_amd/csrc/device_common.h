@@ -54,5 +54,66 @@ __device__ __forceinline__ int64_t wave_sum64(int64_t v) {
     return v;
 }
 
+// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts, then the
+// row_bcast15 / row_bcast31 steps across rows)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t n) {
+    int v = (int)n;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return (uint32_t)v;
+}
+// exclusive scan over a workgroup of NT threads (every thread calls it);
+// wsum: NT/64 + 1 words of LDS; `tot` = the workgroup's sum
+template <int NT>
+__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t n, uint32_t *wsum, uint32_t &tot) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(n);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t w = threadIdx.x < NT / 64 ? wsum[threadIdx.x] : 0u;
+        const uint32_t wi = wave_incl_scan(w);
+        if (threadIdx.x < NT / 64) wsum[threadIdx.x] = wi - w;
+        if (threadIdx.x == NT / 64 - 1) wsum[NT / 64] = wi;
+    }
+    __syncthreads();
+    const uint32_t ex = wsum[wv] + inc - n;
+    tot = wsum[NT / 64];
+    __syncthreads();  // wsum is reused by the next call
+    return ex;
+}
+// 64-bit variants (shuffle steps; offsets that may pass 4 GiB)
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, o, 64);
+        const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), o, 64);
+        if (lane >= o) v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+template <int NT>
+__device__ __forceinline__ uint64_t wg_excl_scan64(uint64_t n, uint64_t *wsum, uint64_t &tot) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan64(n);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint64_t w = threadIdx.x < NT / 64 ? wsum[threadIdx.x] : 0ull;
+        const uint64_t wi = wave_incl_scan64(w);
+        if (threadIdx.x < NT / 64) wsum[threadIdx.x] = wi - w;
+        if (threadIdx.x == NT / 64 - 1) wsum[NT / 64] = wi;
+    }
+    __syncthreads();
+    const uint64_t ex = wsum[wv] + inc - n;
+    tot = wsum[NT / 64];
+    __syncthreads();
+    return ex;
+}
 
 }  // namespace jp2hip

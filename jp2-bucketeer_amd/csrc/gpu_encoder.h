@@ -58,6 +58,7 @@ struct T1CmArgs {
     const uint64_t *slot_off;
     uint4 *counts;    // [block][32] (end of SPP, end of MRP, end of CUP)
     int64_t *dspp;    // [block][32]
+    uint32_t *keys;   // [block] ~(decisions of all coded planes); ~0 on entry (k_t1_worklist)
     int lossless;
 };
 struct T1MqArgs {
@@ -93,12 +94,10 @@ struct DwtLaunch {
 bool launch_dwt(const DwtLaunch &p, hipStream_t st);
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st);
-void launch_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
-                     const BlockDesc *blocks, int32_t *flags, uint64_t *slot_bytes, hipStream_t st);
-void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, const int32_t *flags,
-                     const int32_t *pos, int2 *items, int *nitems, hipStream_t st);
-void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
-                    int32_t *vals, unsigned long long *mq_span, hipStream_t st);
+void launch_t1_worklist(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
+                        uint32_t *keys, int2 *items, int *nitems, hipStream_t st);
+void launch_t1_order(int nblocks, const uint32_t *keys, int32_t *order, unsigned long long *mq_span,
+                     hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
 uint32_t t1_plane_stream_cap(int w, int h);
 
@@ -191,8 +190,8 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, ordkey2, ordval, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
-        dbgbuf, t1ord, t1flags, t1pos, slotbytes, nitems_d;
+        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
+        dbgbuf, t1ord, nitems_d;
     // device tier-2 (t2_device.hip)
     DevBuf hdist, rstate;
     RateState *h_rs = nullptr;  // pinned

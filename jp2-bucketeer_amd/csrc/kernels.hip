@@ -844,14 +844,47 @@ __global__ void __launch_bounds__(256) k_hull(HullArgs a) {
 // take whole groups while the running byte total fits the budget.  Here the
 // segments of all blocks are radix-sorted once per encode (hipcub), their
 // sizes prefix-summed, and each budget is resolved by one binary search.
-__global__ void __launch_bounds__(256) k_seg_count(int nblocks, const uint8_t *nhull, int32_t *nseg) {
-    int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nblocks) nseg[b] = max(0, (int)nhull[b] - 1);
+// segment counts (hull points - 1) and their exclusive scan, one workgroup
+// (one launch for count + device scan); rounds of 32 consecutive blocks per
+// thread, their 32 byte loads in flight together
+constexpr int kSegThreads = 1024, kSegPer = 32;
+__global__ void __launch_bounds__(kSegThreads) k_seg_offsets(int nblocks, const uint8_t *nhull, int32_t *nseg,
+                                                             int32_t *segoff) {
+    __shared__ uint32_t wsum[kSegThreads / 64 + 1];
+    uint32_t base = 0;
+    for (int r0 = 0; r0 < nblocks; r0 += kSegThreads * kSegPer) {
+        const int b0 = r0 + (int)threadIdx.x * kSegPer;
+        uint8_t n[kSegPer];
+        uint32_t c = 0, tot;
+#pragma unroll
+        for (int i = 0; i < kSegPer; i++) {
+            n[i] = b0 + i < nblocks ? nhull[b0 + i] : (uint8_t)0;
+            c += n[i] ? n[i] - 1u : 0u;
+        }
+        uint32_t o = base + wg_excl_scan<kSegThreads>(c, wsum, tot);
+#pragma unroll
+        for (int i = 0; i < kSegPer; i++) {
+            if (b0 + i >= nblocks) break;
+            const int k = n[i] ? n[i] - 1 : 0;
+            nseg[b0 + i] = k;
+            segoff[b0 + i] = (int32_t)o;
+            o += k;
+        }
+        base += tot;
+    }
 }
 
+// segments of each block's hull at its offset; entries past the real count
+// (up to the bound `nbound`) get key 0 and size 0
 __global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nhull, const uint8_t *hpass,
                                                   const uint64_t *hkey, const int32_t *rates,
-                                                  const int32_t *segoff, uint64_t *keys, int64_t *vals) {
+                                                  const int32_t *segoff, const int32_t *nseg, int nbound,
+                                                  uint64_t *keys, int64_t *vals) {
+    const int total = segoff[nblocks - 1] + nseg[nblocks - 1];
+    for (int i = total + blockIdx.x * blockDim.x + threadIdx.x; i < nbound; i += gridDim.x * blockDim.x) {
+        keys[i] = 0;
+        vals[i] = 0;
+    }
     int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblocks) return;
     int nh = nhull[b];
@@ -954,12 +987,12 @@ static bool ensure(DevBuf &b, size_t count, std::string &err) {
 GpuEncoder::~GpuEncoder() {
     DevBuf *all[] = {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
-                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &ordkey2, &ordval, &segcnt, &segoff, &segkey,
+                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &segcnt, &segoff, &segkey,
                      &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
-                     &t1ord, &t1flags, &t1pos, &slotbytes, &nitems_d};
+                     &t1ord, &nitems_d};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -1186,7 +1219,14 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<int32_t>(tch, plan.ntc, err)) return false;
     if (!ensure<uint64_t>(strips, lay.nstrips, err)) return false;
 
-    if (!ensure<int32_t>(t1ord, nb, err) || !h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err))
+    // tier-1 decision streams: a fixed slot per block, room for every plane
+    // (the grid and buffers are sized by that bound anyway)
+    uint64_t stream_bound = 0;
+    for (int i = 0; i < nb; i++)
+        stream_bound += (uint64_t)plan.blocks[i].Mb * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
+    if (!ensure<int32_t>(t1ord, nb, err) || !ensure<uint64_t>(slotoff, nb, err) ||
+        !ensure<uint8_t>(stream_buf, std::max<uint64_t>(stream_bound, 1), err) ||
+        !h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err))
         return false;
     // the plan's tables stay resident while the context encodes the same
     // geometry (plan.gen; buffers only grow, so they are still in place)
@@ -1198,6 +1238,13 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
             !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err) ||
             !h2d(t1ord.ptr, plan.t1_order.data(), sizeof(int32_t) * nb, err))
             return false;
+        std::vector<uint64_t> slots(nb);
+        uint64_t o = 0;
+        for (int i = 0; i < nb; i++) {
+            slots[i] = o;
+            o += (uint64_t)plan.blocks[i].Mb * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
+        }
+        if (nb && !h2d(slotoff.ptr, slots.data(), sizeof(uint64_t) * nb, err)) return false;
         front_gen = plan.gen;
     }
     HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
@@ -1313,42 +1360,17 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     // S5: tier-1.  Items (block, plane) ordered by plane depth from the top,
     // then by block shape, so a wavefront's lanes do similar work.  The list
     // and the blocks' stream slots are built on the device (t1.hip
-    // k_t1_flags / k_t1_items) from the coded plane counts; buffers and the
+    // k_t1_worklist, one workgroup) from the coded plane counts; buffers and the
     // grid are sized by the plan's bound (every plane of every block coded).
     int kmax = 0;
-    uint64_t stream_bound = 0;
-    for (int i = 0; i < nb; i++) {
-        const BlockDesc &bd = plan.blocks[i];
-        kmax = std::max(kmax, (int)bd.Mb);
-        stream_bound += (uint64_t)bd.Mb * t1_plane_stream_cap(bd.w, bd.h);
-    }
+    for (int i = 0; i < nb; i++) kmax = std::max(kmax, (int)plan.blocks[i].Mb);
     const size_t nflags = (size_t)nb * kmax;
-    if (!ensure<int2>(items, std::max<size_t>(nflags, 1), err) || !ensure<uint64_t>(slotoff, nb, err) ||
-        !ensure<uint8_t>(stream_buf, stream_bound, err) || !ensure<uint4>(counts, (size_t)nb * 32, err) ||
-        !ensure<int64_t>(dspp, (size_t)nb * 32, err) || !ensure<int32_t>(t1ord, nb, err) ||
-        !ensure<int32_t>(t1flags, nflags, err) || !ensure<int32_t>(t1pos, nflags, err) ||
-        !ensure<uint64_t>(slotbytes, nb, err) || !ensure<int>(nitems_d, 1, err))
+    if (!ensure<int2>(items, std::max<size_t>(nflags, 1), err) || !ensure<uint4>(counts, (size_t)nb * 32, err) ||
+        !ensure<int64_t>(dspp, (size_t)nb * 32, err) || !ensure<int>(nitems_d, 1, err) ||
+        !ensure<uint32_t>(ordkey, nb, err) || !ensure<unsigned long long>(mqspan, 2, err))
         return false;
-    if (!nflags) HIPCHECK(hipMemsetAsync(nitems_d.ptr, 0, sizeof(int), stream));  // else k_t1_items writes it
-    launch_t1_flags(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr,
-                    (const BlockDesc *)blocks.ptr, (int32_t *)t1flags.ptr, (uint64_t *)slotbytes.ptr, stream);
-    HIPCHECK(hipGetLastError());
-    if (nflags) {
-        size_t tb = 0;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int32_t *)t1flags.ptr, (int32_t *)t1pos.ptr,
-                                                  (int)nflags, stream));
-        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (int32_t *)t1flags.ptr, (int32_t *)t1pos.ptr,
-                                                  (int)nflags, stream));
-        tb = 0;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (uint64_t *)slotbytes.ptr, (uint64_t *)slotoff.ptr, nb,
-                                                  stream));
-        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (uint64_t *)slotbytes.ptr, (uint64_t *)slotoff.ptr,
-                                                  nb, stream));
-    }
-    launch_t1_items(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const int32_t *)t1flags.ptr,
-                    (const int32_t *)t1pos.ptr, (int2 *)items.ptr, (int *)nitems_d.ptr, stream);
+    launch_t1_worklist(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr,
+                       (uint32_t *)ordkey.ptr, (int2 *)items.ptr, (int *)nitems_d.ptr, stream);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[10], stream));
     T1CmArgs ca;
@@ -1363,24 +1385,16 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ca.slot_off = (const uint64_t *)slotoff.ptr;
     ca.counts = (uint4 *)counts.ptr;
     ca.dspp = (int64_t *)dspp.ptr;
+    ca.keys = (uint32_t *)ordkey.ptr;
     ca.lossless = plan.rc.reversible;
-    for (int r = 0; r < nrep_cm; r++) launch_t1_cm(ca, stream);
-    HIPCHECK(hipGetLastError());
-    // MQ lane order: blocks by decreasing decision count
-    if (!ensure<uint32_t>(ordkey, nb, err) || !ensure<uint32_t>(ordkey2, nb, err) || !ensure<int32_t>(ordval, nb, err))
-        return false;
-    if (!ensure<unsigned long long>(mqspan, 2, err)) return false;
-    launch_t1_keys(nb, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr, (const uint4 *)counts.ptr,
-                   (uint32_t *)ordkey.ptr, (int32_t *)ordval.ptr, (unsigned long long *)mqspan.ptr, stream);
-    HIPCHECK(hipGetLastError());
-    if (nb) {
-        size_t tb = 0;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (uint32_t *)ordkey.ptr, (uint32_t *)ordkey2.ptr,
-                                                    (int32_t *)ordval.ptr, (int32_t *)order.ptr, nb, 0, 32, stream));
-        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp.ptr, tb, (uint32_t *)ordkey.ptr, (uint32_t *)ordkey2.ptr,
-                                                    (int32_t *)ordval.ptr, (int32_t *)order.ptr, nb, 0, 32, stream));
+    for (int r = 0; r < nrep_cm; r++) {
+        if (r) HIPCHECK(hipMemsetAsync(ordkey.ptr, 0xff, sizeof(uint32_t) * nb, stream));  // (stage-repeat knob)
+        launch_t1_cm(ca, stream);
     }
+    HIPCHECK(hipGetLastError());
+    // MQ lane order: blocks by decreasing decision count (bucketed)
+    launch_t1_order(nb, (const uint32_t *)ordkey.ptr, (int32_t *)order.ptr, (unsigned long long *)mqspan.ptr, stream);
+    HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[11], stream));
     T1MqArgs ma;
     ma.blocks = (const BlockDesc *)blocks.ptr;
@@ -1432,14 +1446,8 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     HIPCHECK(hipGetLastError());
     // hull segments of all blocks, sorted by slope key (descending), sizes prefix-summed
     if (!ensure<int32_t>(segcnt, nb, err) || !ensure<int32_t>(segoff, nb, err)) return false;
-    if (nb) hipLaunchKernelGGL(k_seg_count, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
-                               (const uint8_t *)nhull.ptr, (int32_t *)segcnt.ptr);
-    {
-        size_t tb = 0;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr, nb, stream));
-        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
-        HIPCHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp.ptr, tb, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr, nb, stream));
-    }
+    if (nb) hipLaunchKernelGGL(k_seg_offsets, dim3(1), dim3(kSegThreads), 0, stream, nb,
+                               (const uint8_t *)nhull.ptr, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr);
     // the segment arrays have the bound's length (no host wait for the real
     // count): unused entries keep key 0 and size 0, sort after every real
     // key (slopes are > 0) and leave the prefix sums flat
@@ -1450,14 +1458,11 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         !ensure<int64_t>(segval, std::max(nseg, 1), err) || !ensure<int64_t>(segval2, std::max(nseg, 1), err) ||
         !ensure<int64_t>(segcum, std::max(nseg, 1), err) || !ensure<uint64_t>(thr, 2 * kMaxLayers, err))
         return false;
-    if (nseg > 0) {
-        HIPCHECK(hipMemsetAsync(segkey.ptr, 0, sizeof(uint64_t) * nseg, stream));
-        HIPCHECK(hipMemsetAsync(segval.ptr, 0, sizeof(int64_t) * nseg, stream));
-    }
     if (nb) hipLaunchKernelGGL(k_seg_emit, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
                                (const uint8_t *)nhull.ptr, (const uint8_t *)hpass.ptr,
                                (const uint64_t *)hkey.ptr, (const int32_t *)rates.ptr,
-                               (const int32_t *)segoff.ptr, (uint64_t *)segkey.ptr, (int64_t *)segval.ptr);
+                               (const int32_t *)segoff.ptr, (const int32_t *)segcnt.ptr, nseg,
+                               (uint64_t *)segkey.ptr, (int64_t *)segval.ptr);
     if (nseg > 0) {
         size_t tb = 0;
         HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,

@@ -466,6 +466,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
             cnt.w = 0;
             a.counts[(size_t)b * 32 + k] = cnt;
             a.dspp[(size_t)b * 32 + k] = dspp;
+            atomicSub(&a.keys[b], (uint32_t)(n_spp + n_mrp + n_cup));
         }
     }
 }
@@ -510,8 +511,10 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
     }
 }
 
-// Context state = the 32-bit table word of its current index (Qe | NMPS << 16 |
-// NLPS << 22 | SWITCH << 28) with the MPS symbol in bit 31.
+// Context state = the 32-bit word of its (table index i, MPS symbol) pair,
+// entry e = 2 i + MPS of a 94-entry table: Qe | e(NMPS) << 16 | e(NLPS) << 23
+// with the MPS symbol in bit 31, where e(NLPS) already carries the MPS flip of
+// a SWITCH state -- the next state is one table read, no bit fix-up.
 //
 // One decision, straight-line (no branch per decision on a 64-lane wave):
 // the CODEMPS/CODELPS procedures of Annex C.2 fold into one select -- the
@@ -519,7 +522,7 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
 // context moves to NMPS/NLPS exactly when renormalisation happens, and every
 // value of RENORME is computed with selects; the (at most one, common)
 // byte-out is applied by select and its byte is written to the lane's
-// 64-byte LDS ring -- to a dummy slot when nothing is emitted -- so the only
+// 64-byte LDS ring (written every step, see mq_step) -- so the only
 // per-decision branch is the rare second byte-out of one renormalisation.
 // Pass padding (CX_PAD, state 0) makes a step with Qe = 0 and d = MPS: no
 // interval change, no renormalisation, no byte -- so every step is coded.
@@ -546,9 +549,8 @@ __device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint3
     const uint32_t An = keep ? A1 : qe;  // never 0: Qe >= 1, and A1 = A >= 0x8000 for Qe = 0
     const uint32_t C0 = m.C + (keep ? qe : 0u);
     const bool ren = !isM || A1 < 0x8000u;
-    // next state: NMPS / NLPS entry; an LPS in a SWITCH state flips the MPS
-    const uint32_t tw = tab[__builtin_amdgcn_ubfe(t, isM ? 16u : 22u, 6u)] |
-                        ((isM ? t : (t ^ (t << 3))) & 0x80000000u);
+    // next state: the NMPS / NLPS entry (MPS flip included)
+    const uint32_t tw = tab[__builtin_amdgcn_ubfe(t, isM ? 16u : 23u, 7u)];
     const int n = __builtin_clz(An) - 16;  // renormalisation shifts
     const int CT = m.CT;
     const bool bo = n >= CT;  // a byte-out inside this renormalisation
@@ -559,9 +561,12 @@ __device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint3
     const uint32_t C2 = carry ? (C1 & 0x7FFFFFFu) : C1;
     const bool ff = Bc == 0xFFu;
     const uint32_t sh = ff ? 20u : 19u;
-    // byte -1 (the MQ coder's initial pending byte, never output) lands in
+    // the byte goes to slot bp whether or not it is emitted: without a
+    // byte-out the slot is the next byte's, written again when it is emitted
+    // and never flushed before (ring_flush copies whole groups below bp).
+    // Byte -1 (the MQ coder's initial pending byte, never output) lands in
     // slot 63, which byte 63 overwrites before that group is flushed
-    ring[bo ? (m.bp & 63) : 64] = (uint8_t)Bc;
+    ring[m.bp & 63] = (uint8_t)Bc;
     uint32_t Cx = bo ? (C2 & ((1u << sh) - 1u)) : C1;
     int CTx = bo ? 27 - (int)sh : CT - n;
     int rem = n - s1;
@@ -626,14 +631,17 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
 // CUs behind other images' kernels.
 __global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
     __shared__ uint32_t cxs[20 * 64];  // 19 contexts + CX_PAD, lane-interleaved
-    __shared__ uint32_t mqt[48];
-    __shared__ uint32_t rings[64 * 17];  // 68 bytes per lane: 64-byte ring + dummy slot
+    __shared__ uint32_t mqt[94];
+    __shared__ uint32_t rings[64 * 17];  // 64-byte ring per lane at a 68-byte stride (banks)
 
     if (threadIdx.x == 0) atomicMin(&a.span[0], (unsigned long long)wall_clock64());
     const int lane = threadIdx.x;
-    if (lane < 47)
-        mqt[lane] = (uint32_t)c_qe[lane] | ((uint32_t)c_nmps[lane] << 16) | ((uint32_t)c_nlps[lane] << 22) |
-                    ((uint32_t)(lane == 0 || lane == 6 || lane == 14) << 28);
+    for (int e = lane; e < 94; e += 64) {
+        const int i = e >> 1, mps = e & 1;
+        const int sw = i == 0 || i == 6 || i == 14;
+        mqt[e] = (uint32_t)c_qe[i] | ((uint32_t)(2 * c_nmps[i] + mps) << 16) |
+                 ((uint32_t)(2 * c_nlps[i] + (mps ^ sw)) << 23) | ((uint32_t)mps << 31);
+    }
     __syncthreads();
     mq_block(a, cxs, mqt, rings);
     atomicMax(&a.span[1], (unsigned long long)wall_clock64());
@@ -659,11 +667,11 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
     const int P = Pt - a.pmin[b];  // coded planes Pt-1 .. pmin (slope prediction)
     uint32_t *cx = cxs + lane;
 #pragma unroll
-    for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];
+    for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];  // entry 2 i + MPS; all start with MPS 0
     cx[CX_PAD * 64] = 0u;  // Qe 0, MPS 0: the padding decisions' no-op state
-    cx[0] = mqt[4];
-    cx[CX_RL * 64] = mqt[3];
-    cx[CX_UNI * 64] = mqt[46];
+    cx[0] = mqt[2 * 4];
+    cx[CX_RL * 64] = mqt[2 * 3];
+    cx[CX_UNI * 64] = mqt[2 * 46];
     Mq m;
     m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
     m.cap = (int)d.out_cap;
@@ -749,76 +757,188 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
     }
 }
 
-// Tier-1 lane order: blocks by decreasing decision count (all passes), so the
-// lanes of a wave carry similar work.  keys = ~count: an ascending radix sort
-// yields the descending order.
-// Also resets k_t1_mq's execution-span slots (earliest start, latest end).
-__global__ void __launch_bounds__(256) k_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin,
-                                                 const uint4 *counts, uint32_t *keys, int32_t *vals,
-                                                 unsigned long long *span) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b == 0 && span) {
+// Tier-1 lane order: blocks by decreasing decision count (all coded passes),
+// so the lanes of an MQ wave carry similar work.  The order only groups
+// blocks (it changes no output), so it is a bucket sort in one workgroup --
+// one launch instead of a device radix sort's ten: bucket = 8 * floor(log2(n
+// + 1)) + the next 3 bits of n + 1 (12.5 % wide), largest first; inside a
+// bucket the order is whatever the atomics give.  keys[b] = ~n, left by
+// k_t1_cm3 (each plane subtracts its decisions from ~0; tier-2's summary adds
+// the decisions up from them).  Also resets k_t1_mq's execution-span slots.
+constexpr int kOrderThreads = 1024, kOrderBuckets = 256;
+__device__ __forceinline__ int order_bucket(uint32_t n) {
+    const uint32_t v = n + 1u;
+    const int e = 31 - __clz(v);                                      // 0..31
+    const int f = e >= 3 ? (int)((v >> (e - 3)) & 7u) : (int)((v << (3 - e)) & 7u);
+    return kOrderBuckets - 1 - min(kOrderBuckets - 1, 8 * e + f);   // descending
+}
+__global__ void __launch_bounds__(kOrderThreads) k_t1_order(int nblocks, const uint32_t *keys, int32_t *order,
+                                                            unsigned long long *span) {
+    __shared__ uint32_t hist[kOrderBuckets];
+    const int tid = threadIdx.x;
+    if (tid == 0 && span) {
         span[0] = ~0ull;
         span[1] = 0ull;
     }
-    if (b >= nblocks) return;
-    uint32_t n = 0;
-    const int pc = P[b] ? P[b] - pmin[b] : 0;
-    for (int k = 0; k < pc; k++) {
-        const uint4 c = counts[(size_t)b * 32 + k];
-        n += c.x + c.y + c.z;
+    for (int i = tid; i < kOrderBuckets; i += kOrderThreads) hist[i] = 0;
+    __syncthreads();
+    constexpr int U = 4;  // blocks per thread per round (loads in flight)
+    for (int b0 = 0; b0 < nblocks; b0 += U * kOrderThreads) {
+        uint32_t k[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int b = b0 + u * kOrderThreads + tid;
+            k[u] = b < nblocks ? keys[b] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (b0 + u * kOrderThreads + tid < nblocks) atomicAdd(&hist[order_bucket(~k[u])], 1u);
     }
-    keys[b] = ~n;
-    vals[b] = b;
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 256 buckets, 4 per lane
+        uint32_t v[4], s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) s += (v[i] = hist[tid * 4 + i]);
+        uint32_t o = wave_incl_scan(s) - s;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            hist[tid * 4 + i] = o;
+            o += v[i];
+        }
+    }
+    __syncthreads();
+    for (int b0 = 0; b0 < nblocks; b0 += U * kOrderThreads) {
+        uint32_t k[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int b = b0 + u * kOrderThreads + tid;
+            k[u] = b < nblocks ? keys[b] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int b = b0 + u * kOrderThreads + tid;
+            if (b < nblocks) order[atomicAdd(&hist[order_bucket(~k[u])], 1u)] = b;
+        }
+    }
 }
 
 // Tier-1 work list, built on the device from the coded plane counts
-// (P - pmin): flags[k * nb + j] = block order[j] codes a plane at depth k
-// (counted from its top plane); an exclusive scan of the flags places each
-// (block, plane) item -- depth-major, then in plan order -- and slot_bytes
-// sizes each block's decision-stream slot.
-__global__ void __launch_bounds__(256) k_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P,
-                                                  const uint8_t *pmin, const BlockDesc *blocks, int32_t *flags,
-                                                  uint64_t *slot_bytes) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= nb * kmax) return;
-    const int k = i / nb, b = order[i - k * nb];
-    const int pc = P[b] - pmin[b];
-    flags[i] = k < pc ? 1 : 0;
-    if (k == 0) slot_bytes[b] = (uint64_t)pc * plane_stream_cap(blocks[b].w, blocks[b].h);
-}
-__global__ void __launch_bounds__(256) k_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P,
-                                                  const int32_t *flags, const int32_t *pos, int2 *items,
-                                                  int *nitems) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int n = nb * kmax;
-    if (i >= n) return;
-    const int k = i / nb, b = order[i - k * nb];
-    if (flags[i]) items[pos[i]] = make_int2(b, P[b] - 1 - k);
-    if (i == n - 1) *nitems = pos[i] + flags[i];
+// c = P - pmin by one workgroup (one launch instead of flags + two device
+// scans + items): the (block, plane) items, depth-major (k = planes from the
+// top), then in the plan's lane order `order`.  Pass 1 takes the per-depth
+// totals (ballots; c is kept in LDS), pass 2 walks the lane order in tiles of
+// 1024: per depth a ballot, the 16 waves' counts prefix-summed by one 16-lane
+// DPP row per depth, and every lane with c > k writes its item.  Also sets
+// keys[b] = ~0 for k_t1_cm3's decision counts.  (The stream slots are fixed
+// by the plan: every plane of a block has its slot, GpuEncoder::run_front.)
+constexpr int kListThreads = 1024, kListWaves = kListThreads / 64, kListMaxK = 64;
+constexpr int kListLdsBlocks = 73728;  // (top << 8 | c) per block in LDS up to this many blocks
+template <bool kLds>
+__global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, const int32_t *order,
+                                                              const uint8_t *P, const uint8_t *pmin, uint32_t *keys,
+                                                              int2 *items, int *nitems) {
+    __shared__ uint16_t ct[kLds ? kListLdsBlocks : 1];
+    __shared__ uint32_t wc[kListMaxK * kListWaves];  // per tile: [depth][wave] count -> item position
+    __shared__ uint32_t run[kListMaxK];              // per depth: next item position
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int b = t; b < nb; b += kListThreads) keys[b] = ~0u;
+    if (t < kListMaxK) run[t] = 0;
+    __syncthreads();
+    // pass 1: lane k of every wave counts the blocks with more than k coded planes
+    constexpr int U = 4;
+    uint32_t acc = 0;
+    for (int j0 = 0; j0 < nb; j0 += U * kListThreads) {
+        int b[U];
+        uint32_t top[U], c[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = j0 + u * kListThreads + t;
+            b[u] = j < nb ? order[j] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            top[u] = b[u] >= 0 ? P[b[u]] : 0u;
+            c[u] = b[u] >= 0 ? top[u] - pmin[b[u]] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int j = j0 + u * kListThreads + t;
+            if (kLds && j < nb) ct[j] = (uint16_t)(top[u] << 8 | c[u]);
+            for (int k = 0; k < kmax; k++) {
+                const uint64_t m = __ballot(c[u] > (uint32_t)k);
+                if (lane == k) acc += (uint32_t)__popcll(m);
+            }
+        }
+    }
+    if (lane < kmax) atomicAdd(&run[lane], acc);
+    __syncthreads();
+    if (t < 64) {  // depth bases: exclusive scan of the totals
+        const uint32_t v = t < kmax ? run[t] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (t < kmax) run[t] = inc - v;
+        if (t == 63) *nitems = (int)inc;
+    }
+    __syncthreads();
+    // pass 2: items (the next tile's lane order is loaded one tile ahead)
+    int bnext = t < nb ? order[t] : 0;
+    for (int j0 = 0; j0 < nb; j0 += kListThreads) {
+        const int j = j0 + t;
+        const int b = bnext;
+        bnext = j + kListThreads < nb ? order[j + kListThreads] : 0;
+        uint32_t top = 0, c = 0;
+        if (j < nb) {
+            if (kLds) {
+                top = ct[j] >> 8;
+                c = ct[j] & 0xffu;
+            } else {
+                top = P[b];
+                c = top - pmin[b];
+            }
+        }
+        for (int k = 0; k < kmax; k++) {
+            const uint64_t m = __ballot(c > (uint32_t)k);
+            if (lane == 0) wc[k * kListWaves + w] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        if (t < kmax * kListWaves) {  // one 16-lane row per depth: prefix over the waves
+            const uint32_t v = wc[t];
+            int s = (int)v;
+            s += __builtin_amdgcn_update_dpp(0, s, 0x111, 0xf, 0xf, false);
+            s += __builtin_amdgcn_update_dpp(0, s, 0x112, 0xf, 0xf, false);
+            s += __builtin_amdgcn_update_dpp(0, s, 0x114, 0xf, 0xf, false);
+            s += __builtin_amdgcn_update_dpp(0, s, 0x118, 0xf, 0xf, false);
+            const int k = t >> 4;
+            const uint32_t r = run[k];
+            wc[t] = r + (uint32_t)s - v;
+            if ((t & 15) == 15) run[k] = r + (uint32_t)s;
+        }
+        __syncthreads();
+        for (int k = 0; k < kmax; k++) {
+            const uint64_t m = __ballot(c > (uint32_t)k);
+            if (c > (uint32_t)k)
+                items[wc[k * kListWaves + w] + (uint32_t)__popcll(m & lt)] = make_int2(b, (int)(top - 1u - k));
+        }
+    }
 }
 
-void launch_t1_flags(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
-                     const BlockDesc *blocks, int32_t *flags, uint64_t *slot_bytes, hipStream_t st) {
-    const long n = (long)nb * kmax;
-    if (n) hipLaunchKernelGGL(k_t1_flags, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nb, kmax, order, P,
-                              pmin, blocks, flags, slot_bytes);
-}
-void launch_t1_items(int nb, int kmax, const int32_t *order, const uint8_t *P, const int32_t *flags,
-                     const int32_t *pos, int2 *items, int *nitems, hipStream_t st) {
-    const long n = (long)nb * kmax;
-    if (n) hipLaunchKernelGGL(k_t1_items, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nb, kmax, order, P,
-                              flags, pos, items, nitems);
-}
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (!a.max_items) return;
     const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
     hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
-void launch_t1_keys(int nblocks, const uint8_t *P, const uint8_t *pmin, const uint4 *counts, uint32_t *keys,
-                    int32_t *vals, unsigned long long *span, hipStream_t st) {
-    hipLaunchKernelGGL(k_t1_keys, dim3(std::max(1, (nblocks + 255) / 256)), dim3(256), 0, st, nblocks, P, pmin,
-                       counts, keys, vals, span);
+void launch_t1_worklist(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
+                        uint32_t *keys, int2 *items, int *nitems, hipStream_t st) {
+    if (kmax > kListMaxK) kmax = kListMaxK;  // (Mb <= 30, plan.cpp)
+    if (nb <= kListLdsBlocks)
+        hipLaunchKernelGGL(k_t1_worklist<true>, dim3(1), dim3(kListThreads), 0, st, nb, kmax, order, P, pmin, keys,
+                           items, nitems);
+    else
+        hipLaunchKernelGGL(k_t1_worklist<false>, dim3(1), dim3(kListThreads), 0, st, nb, kmax, order, P, pmin, keys,
+                           items, nitems);
+}
+void launch_t1_order(int nblocks, const uint32_t *keys, int32_t *order, unsigned long long *span, hipStream_t st) {
+    hipLaunchKernelGGL(k_t1_order, dim3(1), dim3(kOrderThreads), 0, st, nblocks, keys, order, span);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
     if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + a.lanes - 1) / a.lanes), dim3(64), 0, st, a);

@@ -565,7 +565,7 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt)
     hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
                        (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
                        with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
-                       (const uint32_t *)ordkey2.ptr, (T2Summary *)t2sum.ptr);
+                       (const uint32_t *)ordkey.ptr, (T2Summary *)t2sum.ptr);
 }
 
 bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,

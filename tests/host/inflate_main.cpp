@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <zlib.h>
 #define __device__
+#define __host__
 #define __forceinline__ inline
 #define __global__
 #define __launch_bounds__(x)

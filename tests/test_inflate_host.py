@@ -10,12 +10,14 @@ import pytest
 
 HERE = os.path.dirname(__file__)
 SRC = os.path.join(HERE, "..", "jp2-bucketeer_amd", "csrc", "kernels.hip")
+HDR = os.path.join(HERE, "..", "jp2-bucketeer_amd", "csrc", "gpu_encoder.h")
 CLANG = "/opt/rocm/llvm/bin/clang++"
 
 
 def _kernel_text():
+    h = open(HDR).read()
+    ua = h[h.index("struct UnpackArgs {"):h.index("// LZW strips, segment-parallel")]
     s = open(SRC).read()
-    ua = s[s.index("struct UnpackArgs {"):s.index("// LZW, MSB-first")]
     inf = s[s.index("__constant__ uint16_t kInfLenBase"):s.index("// Predictor 2: each sample adds")]
     return "namespace jp2hip {\n" + ua + inf + "}\n"
 
