@@ -898,75 +898,6 @@ __global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nh
     }
 }
 
-// Hull segments sorted by slope key, descending, in a few launches instead of
-// a device radix sort's ~21 (each launch in an encode's chain waits for CUs
-// behind the other in-flight encodes): runs of kSegRun keys sorted in LDS
-// (bitonic, one workgroup per run), then one launch per pairwise merge level
-// (merge path: each thread binary-searches where its kMergePer outputs start,
-// then merges them).  Ties keep no particular order: the threshold search
-// (k_thresh) only reads the byte sums at the ends of equal-key groups.
-constexpr int kSegRun = 4096, kSegRunThreads = 1024, kMergeThreads = 256, kMergePer = 8;
-__global__ void __launch_bounds__(kSegRunThreads) k_seg_runs(int n, const uint64_t *ik, const int64_t *iv,
-                                                             uint64_t *ok, int64_t *ov) {
-    __shared__ uint64_t lk[kSegRun];
-    __shared__ int64_t lv[kSegRun];
-    const int r0 = blockIdx.x * kSegRun;
-    if (r0 >= n) return;
-    const int len = min(kSegRun, n - r0);
-    int m = 2;
-    while (m < len) m <<= 1;
-    for (int i = threadIdx.x; i < m; i += kSegRunThreads) {
-        lk[i] = i < len ? ik[r0 + i] : 0ull;  // padding key 0 sorts last
-        lv[i] = i < len ? iv[r0 + i] : 0ll;
-    }
-    __syncthreads();
-    for (int kk = 2; kk <= m; kk <<= 1)
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < m; i += kSegRunThreads) {
-                const int q = i ^ j;
-                if (q > i) {
-                    const uint64_t a = lk[i], b = lk[q];
-                    if ((i & kk) == 0 ? a < b : a > b) {
-                        lk[i] = b;
-                        lk[q] = a;
-                        const int64_t t = lv[i];
-                        lv[i] = lv[q];
-                        lv[q] = t;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    for (int i = threadIdx.x; i < len; i += kSegRunThreads) {
-        ok[r0 + i] = lk[i];
-        ov[r0 + i] = lv[i];
-    }
-}
-__global__ void __launch_bounds__(kMergeThreads) k_seg_merge(int n, int run, const uint64_t *sk, const int64_t *sv,
-                                                             uint64_t *dk, int64_t *dv) {
-    const int64_t o0 = ((int64_t)blockIdx.x * kMergeThreads + threadIdx.x) * kMergePer;
-    if (o0 >= n) return;
-    const int x = (int)(o0 / (2 * run)) * 2 * run;  // this pair of runs (2 run is a multiple of kMergePer)
-    const int la = min(run, n - x), lb = max(0, min(run, n - x - la));
-    const uint64_t *ak = sk + x, *bk = ak + la;
-    const int64_t *av = sv + x, *bv = av + la;
-    const int d = (int)o0 - x, e = min(d + kMergePer, la + lb);
-    int lo = max(0, d - lb), hi = min(d, la);
-    while (lo < hi) {  // outputs before d: A[0, i) and B[0, d - i); first i with A[i] < B[d-1-i]
-        const int mid = (lo + hi) >> 1;
-        if (ak[mid] >= bk[d - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    int i = lo, j = d - lo;
-    for (int o = d; o < e; o++) {
-        const bool takeA = j >= lb || (i < la && ak[i] >= bk[j]);
-        dk[x + o] = takeA ? ak[i] : bk[j];
-        dv[x + o] = takeA ? av[i] : bv[j];
-        i += takeA ? 1 : 0;
-        j += takeA ? 0 : 1;
-    }
-}
-
 // one thread per layer: threshold key K (UINT64_MAX = nothing fits), and Kc,
 // the Kdu-Layer-Info slope: one above the first key not taken, 0 if every
 // segment is taken (= the tile-split bisection's K'; oracle select_threshold)
@@ -1533,25 +1464,13 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
                                (const int32_t *)segoff.ptr, (const int32_t *)segcnt.ptr, nseg,
                                (uint64_t *)segkey.ptr, (int64_t *)segval.ptr);
     if (nseg > 0) {
-        // sort: runs, then merge levels ping-ponging (segkey, segval) <->
-        // (segkey2, segval2); the runs go where the last level ends in
-        // (segkey2, segval2)
-        int levels = 0;
-        for (int64_t r = kSegRun; r < nseg; r *= 2) levels++;
-        uint64_t *Ak = (uint64_t *)segkey.ptr, *Bk = (uint64_t *)segkey2.ptr;
-        int64_t *Av = (int64_t *)segval.ptr, *Bv = (int64_t *)segval2.ptr;
-        const bool runs_in_B = (levels % 2) == 0;
-        hipLaunchKernelGGL(k_seg_runs, dim3((nseg + kSegRun - 1) / kSegRun), dim3(kSegRunThreads), 0, stream, nseg, Ak,
-                           Av, runs_in_B ? Bk : Ak, runs_in_B ? Bv : Av);
-        bool inB = runs_in_B;
-        const int mg = (int)(((int64_t)nseg + kMergeThreads * kMergePer - 1) / (kMergeThreads * kMergePer));
-        for (int64_t r = kSegRun; r < nseg; r *= 2) {
-            hipLaunchKernelGGL(k_seg_merge, dim3(mg), dim3(kMergeThreads), 0, stream, nseg, (int)r, inB ? Bk : Ak,
-                               inB ? Bv : Av, inB ? Ak : Bk, inB ? Av : Bv);
-            inB = !inB;
-        }
-        HIPCHECK(hipGetLastError());
         size_t tb = 0;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,
+                                                              (int64_t *)segval.ptr, (int64_t *)segval2.ptr, nseg, 0, 64, stream));
+        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
+        HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(cubtmp.ptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,
+                                                              (int64_t *)segval.ptr, (int64_t *)segval2.ptr, nseg, 0, 64, stream));
+        tb = 0;
         HIPCHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
         if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
         HIPCHECK(hipcub::DeviceScan::InclusiveSum(cubtmp.ptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
