@@ -552,25 +552,38 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     // block) for the bit-plane and distortion passes: the coefficients are
     // read from HBM once.  Rows past the block end are a wave-uniform exit;
     // lanes past its width read column 0 and keep 0.
+    // The row loads of each half block (32 rows) are issued before any is
+    // used (rows past the block end re-read its last row and are zeroed
+    // below): a load under a per-row branch was waited for before the next
+    // one issued.
     uint32_t col[64];
+    const int hm1 = d.h - 1;
 #pragma unroll
-    for (int y = 0; y < 64; y++) {
-        col[y] = 0;
-        if (y >= d.h) continue;
-        const int32_t raw = src[(size_t)y * a.plane_w];
-        uint32_t v, s;
-        if constexpr (REV) {
-            s = raw < 0;
-            v = (uint32_t)(raw < 0 ? -raw : raw);
-        } else {
-            const float cf = __int_as_float(raw);
-            s = cf < 0.0f;
-            v = (uint32_t)floorf(fabsf(cf) * d.inv_delta);
+    for (int y0 = 0; y0 < 64; y0 += 32) {
+#pragma unroll
+        for (int y = y0; y < y0 + 32; y++) col[y] = (uint32_t)src[(size_t)min(y, hm1) * a.plane_w];
+#pragma unroll
+        for (int y = y0; y < y0 + 32; y++) {
+            const int32_t raw = (int32_t)col[y];
+            uint32_t v, s;
+            if constexpr (REV) {
+                s = raw < 0;
+                v = (uint32_t)(raw < 0 ? -raw : raw);
+            } else {
+                const float cf = __int_as_float(raw);
+                s = cf < 0.0f;
+                v = (uint32_t)floorf(fabsf(cf) * d.inv_delta);
+            }
+            const bool in = act && y < d.h;
+            v = in ? min(v, lim) : 0u;
+            col[y] = in ? (s << 31) | v : 0u;
+            vmax = max(vmax, v);
         }
-        v = act ? min(v, lim) : 0u;
-        col[y] = act ? (s << 31) | v : 0u;
-        if (keep_sm) sm[y * 64] = (int32_t)col[y];
-        vmax = max(vmax, v);
+    }
+    if (keep_sm) {
+#pragma unroll
+        for (int y = 0; y < 64; y++)
+            if (y < d.h) sm[y * 64] = (int32_t)col[y];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
