@@ -387,10 +387,15 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     // ---- vertical: one column per thread, in registers ----
     for (int x = tid; x < W; x += kDwtThreads) {
         int32_t v[NR];
+        // every row load issues before any is used: rows outside the band
+        // read a clamped (valid) row and are zeroed after (a load under a
+        // per-row branch was waited for before the next one issued)
+#pragma unroll
+        for (int i = 0; i < NR; i++) v[i] = band_load<REV, INGEST>(a, tc, min(max(y0 + i, 0), H - 1), x);
 #pragma unroll
         for (int i = 0; i < NR; i++) {
             const int y = y0 + i;
-            v[i] = (y >= 0 && y < H) ? band_load<REV, INGEST>(a, tc, y, x) : 0;
+            v[i] = (y >= 0 && y < H) ? v[i] : 0;
         }
         if (H > 1) {
             lift_regs<REV, NR>(v, y0, H);

@@ -313,11 +313,18 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         const bool vl = lane < w;
         const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;
         const uint64_t *CT = a.bp + d.bp_off;
-        const uint64_t B = vl ? CT[(size_t)p * 64 + lane] : 0ull;
-        const uint64_t S0 = vl ? CT[(size_t)(Mb + p) * 64 + lane] : 0ull;
-        const uint64_t S1 = (vl && p + 1 < P) ? CT[(size_t)(Mb + p + 1) * 64 + lane] : 0ull;
-        const uint64_t S2 = (vl && p + 2 < P) ? CT[(size_t)(Mb + p + 2) * 64 + lane] : 0ull;
-        const uint64_t SG = vl ? CT[(size_t)2 * Mb * 64 + lane] : 0ull;
+        // the five mask loads issue together (no load under a branch; rows
+        // past S[Mb-1] read the sign row and are dropped by the selects)
+        const uint64_t Bl = CT[(size_t)p * 64 + lane];
+        const uint64_t S0l = CT[(size_t)(Mb + p) * 64 + lane];
+        const uint64_t S1l = CT[(size_t)min(Mb + p + 1, 2 * Mb) * 64 + lane];
+        const uint64_t S2l = CT[(size_t)min(Mb + p + 2, 2 * Mb) * 64 + lane];
+        const uint64_t SGl = CT[(size_t)2 * Mb * 64 + lane];
+        const uint64_t B = vl ? Bl : 0ull;
+        const uint64_t S0 = vl ? S0l : 0ull;
+        const uint64_t S1 = (vl && p + 1 < P) ? S1l : 0ull;
+        const uint64_t S2 = (vl && p + 2 < P) ? S2l : 0ull;
+        const uint64_t SG = vl ? SGl : 0ull;
         const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
         const int nstripes = (h + 3) >> 2;
         g.out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
@@ -451,8 +458,10 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         if (spp && __any(N != 0ull)) {
             nN = __popcll(N);
             sv = nN << p;
-            for (int q = 0; q < p; q++)
-                if (vl) sv += (int64_t)__popcll(N & CT[(size_t)q * 64 + lane]) << q;
+            // (N is 0 on lanes past the block width: no lane test, so the
+            // unrolled loads issue together)
+#pragma unroll 4
+            for (int q = 0; q < p; q++) sv += (int64_t)__popcll(N & CT[(size_t)q * 64 + lane]) << q;
         }
         nN = wave_sum64(nN);
         sv = wave_sum64(sv);
