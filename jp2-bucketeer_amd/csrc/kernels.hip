@@ -744,9 +744,14 @@ __global__ void __launch_bounds__(256) k_plane_hist(PredictArgs a) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // block * 32 + plane
     if (i < (size_t)a.nblocks * 32) {
         const int b = (int)(i >> 5), p = (int)(i & 31);
-        if (p < a.P[b]) {
-            const int k = plane_bin(a.dref[i] + a.dsig[i], a.weight[b], a.est[i]);
-            if (k >= 0) atomicAdd(&lh[k], (unsigned long long)a.est[i]);
+        // every load issues at once (a load under the p < P branch waited for P)
+        const int Pb = a.P[b];
+        const int64_t dd = a.dref[i] + a.dsig[i];
+        const double wb = a.weight[b];
+        const uint32_t e = a.est[i];
+        if (p < Pb) {
+            const int k = plane_bin(dd, wb, e);
+            if (k >= 0) atomicAdd(&lh[k], (unsigned long long)e);
         }
     }
     __syncthreads();

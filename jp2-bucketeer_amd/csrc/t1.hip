@@ -795,10 +795,7 @@ __global__ void __launch_bounds__(kOrderThreads) k_t1_order(int nblocks, const u
     for (int b0 = 0; b0 < nblocks; b0 += U * kOrderThreads) {
         uint32_t k[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int b = b0 + u * kOrderThreads + tid;
-            k[u] = b < nblocks ? keys[b] : 0u;
-        }
+        for (int u = 0; u < U; u++) k[u] = keys[min(b0 + u * kOrderThreads + tid, nblocks - 1)];
 #pragma unroll
         for (int u = 0; u < U; u++)
             if (b0 + u * kOrderThreads + tid < nblocks) atomicAdd(&hist[order_bucket(~k[u])], 1u);
@@ -819,10 +816,7 @@ __global__ void __launch_bounds__(kOrderThreads) k_t1_order(int nblocks, const u
     for (int b0 = 0; b0 < nblocks; b0 += U * kOrderThreads) {
         uint32_t k[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int b = b0 + u * kOrderThreads + tid;
-            k[u] = b < nblocks ? keys[b] : 0u;
-        }
+        for (int u = 0; u < U; u++) k[u] = keys[min(b0 + u * kOrderThreads + tid, nblocks - 1)];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int b = b0 + u * kOrderThreads + tid;
@@ -860,15 +854,15 @@ __global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, 
     for (int j0 = 0; j0 < nb; j0 += U * kListThreads) {
         int b[U];
         uint32_t top[U], c[U];
+        // (loads at clamped indices, no load under a branch: they issue together)
+#pragma unroll
+        for (int u = 0; u < U; u++) b[u] = order[min(j0 + u * kListThreads + t, nb - 1)];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int j = j0 + u * kListThreads + t;
-            b[u] = j < nb ? order[j] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            top[u] = b[u] >= 0 ? P[b[u]] : 0u;
-            c[u] = b[u] >= 0 ? top[u] - pmin[b[u]] : 0u;
+            const bool in = j0 + u * kListThreads + t < nb;
+            const uint32_t pt = P[b[u]], pm = pmin[b[u]];
+            top[u] = in ? pt : 0u;
+            c[u] = in ? pt - pm : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -890,19 +884,22 @@ __global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, 
     }
     __syncthreads();
     // pass 2: items (the next tile's lane order is loaded one tile ahead)
-    int bnext = t < nb ? order[t] : 0;
+    int bnext = order[min(t, nb - 1)];
     for (int j0 = 0; j0 < nb; j0 += kListThreads) {
         const int j = j0 + t;
         const int b = bnext;
-        bnext = j + kListThreads < nb ? order[j + kListThreads] : 0;
+        bnext = order[min(j + kListThreads, nb - 1)];
         uint32_t top = 0, c = 0;
-        if (j < nb) {
-            if (kLds) {
+        if (kLds) {
+            if (j < nb) {
                 top = ct[j] >> 8;
                 c = ct[j] & 0xffu;
-            } else {
-                top = P[b];
-                c = top - pmin[b];
+            }
+        } else {
+            const uint32_t pt = P[b], pm = pmin[b];
+            if (j < nb) {
+                top = pt;
+                c = pt - pm;
             }
         }
         for (int k = 0; k < kmax; k++) {
@@ -938,6 +935,7 @@ void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
 }
 void launch_t1_worklist(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
                         uint32_t *keys, int2 *items, int *nitems, hipStream_t st) {
+    if (nb <= 0) return;                      // (no blocks: no tier-1 launch reads the list)
     if (kmax > kListMaxK) kmax = kListMaxK;  // (Mb <= 30, plan.cpp)
     if (nb <= kListLdsBlocks)
         hipLaunchKernelGGL(k_t1_worklist<true>, dim3(1), dim3(kListThreads), 0, st, nb, kmax, order, P, pmin, keys,
@@ -947,6 +945,7 @@ void launch_t1_worklist(int nb, int kmax, const int32_t *order, const uint8_t *P
                            items, nitems);
 }
 void launch_t1_order(int nblocks, const uint32_t *keys, int32_t *order, unsigned long long *span, hipStream_t st) {
+    if (nblocks <= 0) return;
     hipLaunchKernelGGL(k_t1_order, dim3(1), dim3(kOrderThreads), 0, st, nblocks, keys, order, span);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
