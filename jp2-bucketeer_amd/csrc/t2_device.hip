@@ -355,12 +355,15 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
         hdr += a.tp_hdr[t];
     }
     // per-layer packet bytes (layers in groups of 8 through shared memory)
-    const size_t npk = (size_t)a.nprec * a.L;
     for (int l0 = 0; l0 < a.L; l0 += 8) {
         int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (size_t i = tid; i < npk; i += 256) {
-            const int l = (int)(i % a.L);
-            if (l >= l0 && l < l0 + 8) v[l - l0] += a.pk_len[i];
+        // precinct-major: a thread's 8 layer loads at clamped indices, issued together
+        for (int pq = tid; pq < a.nprec; pq += 256) {
+            uint32_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) x[k] = a.pk_len[(size_t)pq * a.L + min(l0 + k, a.L - 1)];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] += l0 + k < a.L ? x[k] : 0u;
         }
         for (int k = 0; k < 8; k++) lay[tid][k] = v[k];
         __syncthreads();
@@ -374,11 +377,25 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
     // tier-1 totals (ndec_key: ~decisions per block, the MQ lane-order keys)
     int64_t tb = 0, tp = 0, nd = 0;
     int skipped = 0;
-    for (int b = tid; b < nblocks; b += 256) {
-        tb += lengths[b];
-        tp += npasses[b];
-        nd += ~ndec_key[b];
-        skipped |= pmin[b] > 0;
+    for (int b0 = 0; b0 < nblocks; b0 += 4 * 256) {  // 4 blocks' loads in flight per thread
+        int32_t ln[4];
+        uint32_t np[4], kk[4], pm[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int b = min(b0 + u * 256 + tid, nblocks - 1);
+            ln[u] = lengths[b];
+            np[u] = npasses[b];
+            kk[u] = ndec_key[b];
+            pm[u] = pmin[b];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (b0 + u * 256 + tid < nblocks) {
+                tb += ln[u];
+                tp += np[u];
+                nd += ~kk[u];
+                skipped |= pm[u] > 0;
+            }
     }
     lay[tid][1] = nd;
     part[tid] = (uint64_t)tb;
