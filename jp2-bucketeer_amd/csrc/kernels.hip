@@ -836,19 +836,46 @@ __global__ void __launch_bounds__(256) k_hull(HullArgs a) {
     hp[0] = 0;
     hk[0] = 0;
     hd[0] = 0;
+    // the stack's top entry (key, cumulative distortion, rate at its pass)
+    // also lives in registers, so only a pop reads the stack back; the next
+    // pass's rate and distortion are loaded one pass ahead
+    uint64_t tk = 0;
+    int64_t td = 0;
+    int32_t tr = 0;
     int64_t Dn = 0;
+    int32_t Rnx = np ? R[0] : 0;
+    int64_t Dnx = np ? Dd[0] : 0;
     for (int n = 1; n <= np; n++) {
-        Dn += Dd[n - 1];
+        const int32_t Rn = Rnx;
+        Dn += Dnx;
+        if (n < np) {
+            Rnx = R[n];
+            Dnx = Dd[n];
+        }
         for (;;) {
-            int hh = hp[nh - 1];
-            int64_t dD = Dn - hd[nh - 1];
-            int32_t dR = R[n - 1] - (hh ? R[hh - 1] : 0);
+            const int64_t dD = Dn - td;
+            const int32_t dR = Rn - tr;
+            bool pop = false;
+            double s = 0.0;
             if (dD <= 0) break;
-            if (dR <= 0) { nh--; continue; }
-            double s = (double)dD * wgt / (double)dR;
-            if (nh >= 2 && s >= __longlong_as_double((long long)hk[nh - 1])) { nh--; continue; }
+            if (dR <= 0) pop = true;
+            else {
+                s = (double)dD * wgt / (double)dR;
+                pop = nh >= 2 && s >= __longlong_as_double((long long)tk);
+            }
+            if (pop) {
+                nh--;
+                const int hh = hp[nh - 1];
+                tk = hk[nh - 1];
+                td = hd[nh - 1];
+                tr = hh ? R[hh - 1] : 0;
+                continue;
+            }
+            tk = (uint64_t)__double_as_longlong(s);
+            td = Dn;
+            tr = Rn;
             hp[nh] = (uint8_t)n;
-            hk[nh] = (uint64_t)__double_as_longlong(s);
+            hk[nh] = tk;
             hd[nh] = Dn;
             nh++;
             break;
