@@ -901,19 +901,44 @@ __global__ void __launch_bounds__(kSegThreads) k_seg_offsets(int nblocks, const 
         const int b0 = r0 + (int)threadIdx.x * kSegPer;
         uint8_t n[kSegPer];
         uint32_t c = 0, tot;
+        const bool whole = b0 + kSegPer <= nblocks;  // 16-byte loads / stores (b0 is 32-aligned)
+        if (whole) {
+            const uint4 v0 = *(const uint4 *)(nhull + b0), v1 = *(const uint4 *)(nhull + b0 + 16);
+            const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int i = 0; i < kSegPer; i++) n[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        } else {
+#pragma unroll
+            for (int i = 0; i < kSegPer; i++) n[i] = nhull[min(b0 + i, nblocks - 1)];
+#pragma unroll
+            for (int i = 0; i < kSegPer; i++)
+                if (b0 + i >= nblocks) n[i] = 0;
+        }
+        int32_t k[kSegPer], off[kSegPer];
 #pragma unroll
         for (int i = 0; i < kSegPer; i++) {
-            n[i] = b0 + i < nblocks ? nhull[b0 + i] : (uint8_t)0;
-            c += n[i] ? n[i] - 1u : 0u;
+            k[i] = n[i] ? n[i] - 1 : 0;
+            c += (uint32_t)k[i];
         }
         uint32_t o = base + wg_excl_scan<kSegThreads>(c, wsum, tot);
 #pragma unroll
         for (int i = 0; i < kSegPer; i++) {
-            if (b0 + i >= nblocks) break;
-            const int k = n[i] ? n[i] - 1 : 0;
-            nseg[b0 + i] = k;
-            segoff[b0 + i] = (int32_t)o;
-            o += k;
+            off[i] = (int32_t)o;
+            o += (uint32_t)k[i];
+        }
+        if (whole) {
+#pragma unroll
+            for (int i = 0; i < kSegPer; i += 4) {
+                *(int4 *)(nseg + b0 + i) = make_int4(k[i], k[i + 1], k[i + 2], k[i + 3]);
+                *(int4 *)(segoff + b0 + i) = make_int4(off[i], off[i + 1], off[i + 2], off[i + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kSegPer; i++)
+                if (b0 + i < nblocks) {
+                    nseg[b0 + i] = k[i];
+                    segoff[b0 + i] = off[i];
+                }
         }
         base += tot;
     }
