@@ -836,6 +836,12 @@ __global__ void __launch_bounds__(kOrderThreads) k_t1_order(int nblocks, const u
 // by the plan: every plane of a block has its slot, GpuEncoder::run_front.)
 constexpr int kListThreads = 1024, kListWaves = kListThreads / 64, kListMaxK = 64;
 constexpr int kListLdsBlocks = 73728;  // (top << 8 | c) per block in LDS up to this many blocks
+// the wave's largest coded plane count, at most kmax (wave-uniform)
+__device__ __forceinline__ int wave_max_planes(uint32_t c, int kmax) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c = max(c, (uint32_t)__shfl_xor((int)c, o, 64));
+    return min(__builtin_amdgcn_readfirstlane((int)c), kmax);
+}
 template <bool kLds>
 __global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, const int32_t *order,
                                                               const uint8_t *P, const uint8_t *pmin, uint32_t *keys,
@@ -868,7 +874,8 @@ __global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, 
         for (int u = 0; u < U; u++) {
             const int j = j0 + u * kListThreads + t;
             if (kLds && j < nb) ct[j] = (uint16_t)(top[u] << 8 | c[u]);
-            for (int k = 0; k < kmax; k++) {
+            const int kw = wave_max_planes(c[u], kmax);
+            for (int k = 0; k < kw; k++) {
                 const uint64_t m = __ballot(c[u] > (uint32_t)k);
                 if (lane == k) acc += (uint32_t)__popcll(m);
             }
@@ -902,10 +909,13 @@ __global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, 
                 c = pt - pm;
             }
         }
-        for (int k = 0; k < kmax; k++) {
+        // depths up to the wave's deepest block; the rest of its column is 0
+        const int kw = wave_max_planes(c, kmax);
+        for (int k = 0; k < kw; k++) {
             const uint64_t m = __ballot(c > (uint32_t)k);
             if (lane == 0) wc[k * kListWaves + w] = (uint32_t)__popcll(m);
         }
+        if (lane >= kw && lane < kmax) wc[lane * kListWaves + w] = 0u;
         __syncthreads();
         if (t < kmax * kListWaves) {  // one 16-lane row per depth: prefix over the waves
             const uint32_t v = wc[t];
@@ -920,7 +930,7 @@ __global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, 
             if ((t & 15) == 15) run[k] = r + (uint32_t)s;
         }
         __syncthreads();
-        for (int k = 0; k < kmax; k++) {
+        for (int k = 0; k < kw; k++) {
             const uint64_t m = __ballot(c > (uint32_t)k);
             if (c > (uint32_t)k)
                 items[wc[k * kListWaves + w] + (uint32_t)__popcll(m & lt)] = make_int2(b, (int)(top - 1u - k));
