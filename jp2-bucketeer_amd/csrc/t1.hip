@@ -626,7 +626,7 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 // the segment switch and the per-pass rate record are data, not control
 // flow -- so all lanes of a wave execute the same instruction stream
 // whatever pass each is in.  Blocks are ordered by decision count
-// (k_t1_keys + radix sort), so the lanes of a wave finish together.
+// (k_t1_order, a one-workgroup bucket sort), so the lanes of a wave finish together.
 //
 // Segment s of a block with P coded planes: s = 0 is the top plane's cleanup
 // pass; s >= 1 is pass (s+2)%3 (0 SPP, 1 MRP, 2 CUP) of plane k = (s+2)/3,
