@@ -116,4 +116,33 @@ __device__ __forceinline__ uint64_t wg_excl_scan64(uint64_t n, uint64_t *wsum, u
     return ex;
 }
 
+// Files each block's coded planes in k_t1_cm3's per-depth work lists
+// (T1ItemArgs, gpu_encoder.h); called by every lane of a thread-per-block
+// kernel (`valid` false past the last block), one atomic per wave and depth.
+template <typename ItemArgs>
+__device__ __forceinline__ void emit_t1_items(const ItemArgs &a, int b, bool valid, int P, int pmin) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = valid ? (uint32_t)(P - pmin) : 0u;
+    if (valid) {
+        a.acc[b] = (unsigned long long)c << 40;
+        if (P == 0) {
+            a.npasses[b] = 0;
+            a.lengths[b] = 0;
+        }
+    }
+    uint32_t cw = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cw = max(cw, (uint32_t)__shfl_xor((int)cw, o, 64));
+    const int kw = min(__builtin_amdgcn_readfirstlane((int)cw), a.kmax);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int k = 0; k < kw; k++) {
+        const uint64_t m = __ballot(c > (uint32_t)k);
+        const int leader = __builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&a.dfill[k], (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        if (c > (uint32_t)k) a.dlist[(size_t)k * a.nb + base + (uint32_t)__popcll(m & lt)] = b;
+    }
+}
+
 }  // namespace jp2hip

@@ -852,10 +852,8 @@ static void launch_band(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a
     hipLaunchKernelGGL((k_dwt_band<REV, INGEST, RB>), g, dim3(kDwtThreads), lds, st, a);
 }
 template <bool REV, bool INGEST>
-static void launch_band_rb(int RB, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
-    if (RB == 32) launch_band<REV, INGEST, 32>(g, lds, st, a);
-    else if (RB == 16) launch_band<REV, INGEST, 16>(g, lds, st, a);
-    else launch_band<REV, INGEST, 8>(g, lds, st, a);
+static void launch_band_rb(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    launch_band<REV, INGEST, 8>(g, lds, st, a);
 }
 
 template <bool REV, int NC>
@@ -940,12 +938,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             else hipLaunchKernelGGL(k_dwt_tail<false>, dim3(p.ntc), dim3(kTailThreads), 0, st, t);
             return hipGetLastError() == hipSuccess;
         }
-        // kept rows per workgroup: 16, or 8 for rows wider than 2048
-        int R = 8;  // kept rows per workgroup (8: more workgroups in flight; 16/32 measured slower)
-        if (const char *e = getenv("JP2HIP_DWT_RB")) {  // experiment knob
-            const int r = atoi(e);
-            if ((r == 8 || r == 16 || r == 32) && (size_t)r * maxW <= (size_t)kDwtLdsWordsWide) R = r;
-        }
+        const int R = 8;  // kept rows per workgroup (more workgroups in flight; 16 / 32 measured slower)
         a.level = lv;
         a.R = R;
         a.src = scratch[(lv - 1) & 1];
@@ -961,26 +954,24 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
         constexpr int kRb1 = 8;
         const size_t lds1 = ((size_t)p.nc * kRb1 * lds_row_stride(maxW) + kPadL + kPadR) * 4;
         const int cpt = maxW <= kDwtThreads ? 1 : (maxW <= 2 * kDwtThreads ? 2 : 4);
-        if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && maxW <= 4 * kDwtThreads &&
-            !getenv("JP2HIP_DWT_L1_WINDOW") && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
+        if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && maxW <= 4 * kDwtThreads) {
             // streaming vertical pass (k_dwt_l1s), bands of kStreamBand rows,
-            // horizontal batches of 4 rows (8: JP2HIP_DWT_L1_RB=8)
-            const char *rbe = getenv("JP2HIP_DWT_L1_RB");
-            a.R = (rbe && atoi(rbe) == 8) ? 8 : 4;
+            // horizontal batches of 4 rows
+            a.R = 4;
             const size_t lds_s = ((size_t)p.nc * a.R * lds_row_stride(maxW) + kPadL + kPadR) * 4;
             dim3 g1((maxH + kStreamBand - 1) / kStreamBand, p.ntc / p.nc);
             if (p.reversible) launch_l1s<true>(p.nc, cpt, g1, lds_s, st, a);
             else launch_l1s<false>(p.nc, cpt, g1, lds_s, st, a);
-        } else if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && !getenv("JP2HIP_DWT_PER_COMPONENT")) {
+        } else if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4) {
             dim3 g1((maxH + kRb1 - 1) / kRb1, p.ntc / p.nc);
             if (p.reversible) launch_l1<true>(p.nc, g1, lds1, st, a);
             else launch_l1<false>(p.nc, g1, lds1, st, a);
         } else if (lv == 1) {
-            if (p.reversible) launch_band_rb<true, true>(R, g, lds, st, a);
-            else launch_band_rb<false, true>(R, g, lds, st, a);
+            if (p.reversible) launch_band_rb<true, true>(g, lds, st, a);
+            else launch_band_rb<false, true>(g, lds, st, a);
         } else {
-            if (p.reversible) launch_band_rb<true, false>(R, g, lds, st, a);
-            else launch_band_rb<false, false>(R, g, lds, st, a);
+            if (p.reversible) launch_band_rb<true, false>(g, lds, st, a);
+            else launch_band_rb<false, false>(g, lds, st, a);
         }
         if (hipGetLastError() != hipSuccess) return false;
     }

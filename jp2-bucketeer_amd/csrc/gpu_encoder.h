@@ -46,10 +46,26 @@ size_t lzw_scratch_bytes(int nstrips, uint64_t segs);
 bool launch_lzw(const UnpackArgs &u, uint64_t segs, void *scratch, hipStream_t st);
 
 // tier-1 kernels (t1.hip)
+constexpr int kOrderBuckets = 256;  // MQ lane-order buckets (decision count, 12.5 % wide)
+// Work lists of k_t1_cm3, filled once the coded planes are known
+// (emit_t1_items: k_plane_pmin, or k_t1_items without slope prediction):
+// list k holds the blocks with more than k coded planes (item = plane k from
+// the top of that block), in no particular order.
+struct T1ItemArgs {
+    int nb, kmax;               // kmax: largest Mb of the plan (<= 64)
+    const uint8_t *P;
+    uint8_t *pmin;              // k_t1_items writes 0 (every plane coded)
+    uint32_t *dfill;            // [64] list fills (zeroed by k_quant)
+    int32_t *dlist;             // [kmax][nb]
+    unsigned long long *acc;    // [nb] (coded planes << 40): k_t1_cm3 counts planes down, decisions up
+    uint8_t *npasses;           // blocks without a coded plane: 0 passes, 0 bytes (k_t1_mq never sees them)
+    int32_t *lengths;
+};
 struct T1CmArgs {
-    const int2 *items;   // (block, plane)
-    const int *nitems;   // item count (device); the grid covers max_items
-    int max_items;
+    const uint32_t *dfill;  // per-depth list fills
+    const int32_t *dlist;
+    int nb, kmax;
+    int max_items;          // bound on the items (nb * kmax): the grid
     const BlockDesc *blocks;
     const uint64_t *bp;
     const int32_t *sm;
@@ -58,12 +74,15 @@ struct T1CmArgs {
     const uint64_t *slot_off;
     uint4 *counts;    // [block][32] (end of SPP, end of MRP, end of CUP)
     int64_t *dspp;    // [block][32]
-    uint32_t *keys;   // [block] ~(decisions of all coded planes); ~0 on entry (k_t1_worklist)
+    unsigned long long *acc;  // [block] (planes left << 40) | decisions so far
+    uint32_t *bfill;          // [256] MQ lane-order bucket fills (zeroed by k_quant)
+    int32_t *bslots;          // [256][nb] blocks per bucket
     int lossless;
 };
 struct T1MqArgs {
     const BlockDesc *blocks;
-    const int32_t *order;
+    const uint32_t *bfill;   // lane order: bucket fills and members (k_t1_cm3)
+    const int32_t *bslots;
     int nblocks;
     const uint8_t *P;
     const uint8_t *pmin;  // lowest coded plane (slope prediction; 0 = all)
@@ -77,8 +96,7 @@ struct T1MqArgs {
     uint8_t *npasses;
     int32_t *lengths;
     int *err;
-    int lanes;  // blocks per wavefront (1..64)
-    unsigned long long *span;  // [2] execution span in 100 MHz ticks (min start, max end)
+    unsigned long long *span;  // [2] execution span in 100 MHz ticks (~min start, max end)
     int64_t *dbg;  // optional per-block census [block][4] (debug)
 };
 // fused ingest + DWT (dwt.hip)
@@ -94,10 +112,7 @@ struct DwtLaunch {
 bool launch_dwt(const DwtLaunch &p, hipStream_t st);
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st);
-void launch_t1_worklist(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
-                        uint32_t *keys, int2 *items, int *nitems, hipStream_t st);
-void launch_t1_order(int nblocks, const uint32_t *keys, int32_t *order, unsigned long long *mq_span,
-                     hipStream_t st);
+void launch_t1_items(const T1ItemArgs &a, hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
 uint32_t t1_plane_stream_cap(int w, int h);
 
@@ -168,6 +183,7 @@ class GpuEncoder {
     // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
     bool apply_thresholds(const Plan &plan, const int *halt, std::string &err);
+    void select_launch(const Plan &plan, const int *halt);
     T2Args t2_args(const Plan &plan) const;
     void t2_size_launch(const Plan &plan, bool with_kc, const int *halt);
     bool host_wait(std::string &err);
@@ -190,21 +206,27 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, segkey2, llbuf0, llbuf1, ordkey, segval, segval2, segcum, thr, cubtmp, items, slotoff, stream_buf, counts, dspp,
-        dbgbuf, t1ord, nitems_d;
+        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, llbuf0, llbuf1, ordkey, segval, thr, items,
+        slotoff, stream_buf, counts, dspp, dbgbuf, t1fill;
+    // PCRD selection (k_hull / k_select): slope-bin histogram, ticket + list
+    // fills, candidate lists
+    DevBuf pcrd_hb, pcrd_hc, sel_ctl, sel_key, sel_size;
     // device tier-2 (t2_device.hip)
     DevBuf hdist, rstate;
-    RateState *h_rs = nullptr;  // pinned
+    RateState *h_rs = nullptr;      // host-mapped: rate state, then the T2Summary (k_rate_step)
+    RateState *d_rs_out = nullptr;  // its device address
     DevBuf t2prec, t2tp, t2tt, t2lblock, t2incl, t2pklen, t2pkoff, t2tplen, t2tphdr, t2tpoff, t2blkdst, t2out, t2sum;
     int t2_nprec = 0, t2_ntp = 0;
     uint64_t front_gen = 0, t2_gen = 0;  // plan generation whose tables are resident
     T2Summary *h_sum = nullptr;
     int64_t *h_tot = nullptr;  // pinned [8]: t1 total, -, k_t1_mq span[2], unpack error, segment tail[2]
     bool profiled = false;
-    int nseg = 0;  // segment arrays' length: the bound sum(3 Mb - 2), zero-key padded
+    int nseg = 0;  // hull segments at most: the bound sum(3 Mb - 2)
     uint8_t *h_packed = nullptr;
     size_t h_packed_cap = 0;
     std::vector<int64_t> h_hist;
+    std::vector<uint64_t> strips_host;  // strip offsets last uploaded to `strips`
+    const void *strips_dev = nullptr;
 };
 
 }  // namespace jp2hip

@@ -18,6 +18,12 @@ constexpr int kMaxPasses = 96;    // 3*32-2 rounded up; per-block pass table str
 constexpr int kSlopeBins = 1024;
 constexpr int kSlopeBinBase = (1023 - 64) << 3;
 constexpr int kSkipMargin = 12;
+// PCRD threshold selection (kernels.hip k_hull / k_select): hull segment bytes
+// histogrammed over 1/32-octave bins of the slope key (bits 47..62 of the
+// IEEE double, 2^-64 .. 2^64, clamped at both ends); the exact threshold is
+// then resolved inside the one bin where a layer's budget falls
+constexpr int kPcrdBins = 4096;
+constexpr int kPcrdBinBase = (1023 - 64) << 5;
 constexpr int kMaxLayers = 32;
 constexpr int kMaxLevels = 12;
 

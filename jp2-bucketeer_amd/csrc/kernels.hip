@@ -14,9 +14,9 @@
 // Floating point: built with -ffp-contract=off; every 9/7 / ICT expression is
 // written in the same order as the oracle so the lossy path is bit-exact.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -527,6 +527,10 @@ struct QuantArgs {
     int max_mb;            // largest Mb of the plan (LDS: max_mb * 512 bytes per wave)
     int keep_sm;           // write the sign-magnitude copy of every block (debug dumps)
     int nblocks;
+    // per-encode counters of later kernels, zeroed here by workgroup 0 (no
+    // memset launch): dword spans
+    uint32_t *zero[8];
+    uint32_t nzero[8];
 };
 
 constexpr int kQuantWaves = 4;  // code-blocks (waves) per workgroup
@@ -535,6 +539,10 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     extern __shared__ uint64_t lds_planes[];  // [wave][plane][lane], a.max_mb planes per wave
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.x * kQuantWaves + wv;
+    if (blockIdx.x == 0)
+#pragma unroll
+        for (int z = 0; z < 8; z++)
+            for (uint32_t i = threadIdx.x; i < a.nzero[z]; i += 64 * kQuantWaves) a.zero[z][i] = 0u;
     if (b >= a.nblocks) return;
     uint64_t *planes = lds_planes + (size_t)wv * a.max_mb * 64;
     BlockDesc d = a.blocks[b];
@@ -788,24 +796,30 @@ __global__ void __launch_bounds__(64) k_plane_cut(const unsigned long long *hist
     if (lane == 0) *kcut = cnt - kSkipMargin;
 }
 
-__global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a) {
+// the lowest coded plane of each block, then its items in tier-1's work lists
+__global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a, T1ItemArgs ia) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.nblocks) return;
-    const int P = a.P[b];
-    const int kc = *a.kcut;
-    const double wgt = a.weight[b];
+    const bool in = b < a.nblocks;
+    const int P = in ? a.P[b] : 0;
     int pmin = P > 0 ? P - 1 : 0;
-    for (int p = 0; p < P; p++) {
-        const size_t i = (size_t)b * 32 + p;
-        if (plane_bin(a.dref[i] + a.dsig[i], wgt, a.est[i]) >= kc) { pmin = p; break; }
+    if (in) {
+        const int kc = *a.kcut;
+        const double wgt = a.weight[b];
+        for (int p = 0; p < P; p++) {
+            const size_t i = (size_t)b * 32 + p;
+            if (plane_bin(a.dref[i] + a.dsig[i], wgt, a.est[i]) >= kc) { pmin = p; break; }
+        }
+        a.pmin[b] = (uint8_t)pmin;
     }
-    a.pmin[b] = (uint8_t)pmin;
+    emit_t1_items(ia, b, in, P, pmin);
 }
 
 // --------------------------------------------------------------------------
-// S6: PCRD-opt.  Hull per block (thread per block), then one workgroup
-// finds, for every layer at once, the smallest slope key whose total rate
-// fits the layer budget (63-step bisection over the key space).
+// S6: PCRD-opt.  Hull per block (thread per block, k_hull), which also
+// histograms every hull segment's bytes over kPcrdBins slope-key bins; then
+// k_select finds each layer's threshold: the bin its budget falls in from the
+// histogram, the exact key inside that bin by a radix select over the
+// segments of that bin only (no sort of all segments).
 // --------------------------------------------------------------------------
 struct HullArgs {
     int nblocks;
@@ -817,11 +831,17 @@ struct HullArgs {
     uint8_t *hpass;   // [block][kMaxPasses+1]
     uint64_t *hkey;   // [block][kMaxPasses+1]
     int64_t *hdist;   // [block][kMaxPasses+1] cumulative distortion at each hull point
+    unsigned long long *hbytes;  // [kPcrdBins] segment bytes per slope bin (zeroed by k_quant)
+    uint32_t *hcount;            // [kPcrdBins] segments per slope bin
 };
 
-__global__ void __launch_bounds__(256) k_hull(HullArgs a) {
-    int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.nblocks) return;
+// slope-key bin: monotone in the key (positive doubles order like their bits)
+__device__ __forceinline__ int pcrd_bin(uint64_t key) {
+    const int b = (int)(key >> 47) - kPcrdBinBase;
+    return b < 0 ? 0 : (b >= kPcrdBins ? kPcrdBins - 1 : b);
+}
+
+__device__ __forceinline__ void hull_one(const HullArgs &a, int b, unsigned long long *lb, uint32_t *lc) {
     int np = a.npasses[b];
     const int32_t *R = a.rates + (size_t)b * kMaxPasses;
     const int64_t *Dd = a.dists + (size_t)b * kMaxPasses;
@@ -882,16 +902,239 @@ __global__ void __launch_bounds__(256) k_hull(HullArgs a) {
         }
     }
     a.nhull[b] = (uint8_t)nh;
+    // the hull's segments into the workgroup's slope-bin histogram
+    int32_t r0 = 0;
+    for (int i = 1; i < nh; i++) {
+        const int32_t r1 = R[hp[i] - 1];
+        const int bn = pcrd_bin(hk[i]);
+        atomicAdd(&lb[bn], (unsigned long long)(r1 - r0));
+        atomicAdd(&lc[bn], 1u);
+        r0 = r1;
+    }
 }
+
+constexpr int kHullThreads = 256;
+__global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
+    __shared__ unsigned long long lb[kPcrdBins];
+    __shared__ uint32_t lc[kPcrdBins];
+    for (int i = threadIdx.x; i < kPcrdBins; i += kHullThreads) {
+        lb[i] = 0;
+        lc[i] = 0;
+    }
+    __syncthreads();
+    const int b = blockIdx.x * kHullThreads + threadIdx.x;
+    if (b < a.nblocks) hull_one(a, b, lb, lc);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kPcrdBins; i += kHullThreads)
+        if (lc[i]) {
+            atomicAdd(&a.hbytes[i], lb[i]);
+            atomicAdd(&a.hcount[i], lc[i]);
+        }
+}
+
 
 // Layer thresholds.  The oracle's rule (oracle/jp2_oracle.c select_threshold)
 // is: walk hull segments in decreasing slope-key order, group equal keys, and
-// take whole groups while the running byte total fits the budget.  Here the
-// segments of all blocks are radix-sorted once per encode (hipcub), their
-// sizes prefix-summed, and each budget is resolved by one binary search.
-// segment counts (hull points - 1) and their exclusive scan, one workgroup
-// (one launch for count + device scan); rounds of 32 consecutive blocks per
-// thread, their 32 byte loads in flight together
+// take whole groups while the running byte total fits the budget.  With
+// S(k) = bytes of the segments whose key >= k (non-increasing), that takes
+// exactly the keys >= K' = min { k : S(k) <= budget } (split.cpp), and K' is
+// one above the first key not taken -- the rule's Kc (Kdu-Layer-Info).
+//
+// k_select finds K' per layer in one launch, no sort:
+//  1. every workgroup: suffix sums of the k_hull bin histogram; per layer the
+//     bin b whose segments straddle the budget (S over the bins above b fits,
+//     with b's bytes it does not);
+//  2. every workgroup, thread per code-block: the hull segments whose key falls
+//     in one of those bins are appended to that bin's candidate list;
+//  3. the last workgroup to arrive (agent-scope release / acquire ticket,
+//     cdna_hip_programming.md Guideline 16) resolves each layer by a radix
+//     select over its bin's candidates, 8 bits a round from the top: the largest
+//     key v with (bytes above the bin) + (candidate bytes with key >= v) >
+//     budget is the first key not taken, K' = v + 1.
+// The ticket and list fill counters are zeroed by k_quant and left zero by
+// the last workgroup for the next launch (the device rate loop runs several).
+struct SelectArgs {
+    const int *halt;  // device rate loop: nothing to do once it has stopped
+    int nblocks, layers;
+    const uint8_t *nhull, *hpass;
+    const uint64_t *hkey;
+    const int32_t *rates;
+    const unsigned long long *hbytes;
+    const uint32_t *hcount;
+    const int64_t *budget;
+    uint64_t *lkey;   // candidate lists, capacity >= every hull segment
+    uint32_t *lsize;
+    uint32_t *ctl;    // [0] arrival ticket, [1 + i] fill of list i
+    uint64_t *K, *Kc;
+};
+
+constexpr int kSelThreads = 1024, kSelGroup = 8;
+__global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
+    __shared__ unsigned long long sfx[kPcrdBins];  // S(bin): bytes of the bins >= bin
+    __shared__ int8_t binmap[kPcrdBins];           // bin -> candidate list (-1: none)
+    __shared__ uint64_t wsum[kSelThreads / 64 + 1];
+    __shared__ int lbin[kMaxLayers], lli[kMaxLayers];
+    __shared__ int64_t lneed[kMaxLayers];          // budget - bytes above the bin
+    __shared__ int list_bin[kMaxLayers];
+    __shared__ uint32_t list_off[kMaxLayers + 1];
+    __shared__ int nlist, last;
+    __shared__ unsigned long long rh[kSelGroup][256];
+    __shared__ unsigned long long rpre[kMaxLayers], racc[kMaxLayers];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, L = a.layers;
+    if (a.halt && *a.halt) return;
+    // 1. suffix sums, 4 bins per thread
+    {
+        uint64_t v[4], s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) s += (v[i] = a.hbytes[4 * tid + i]);
+        uint64_t tot;
+        const uint64_t pre = wg_excl_scan64<kSelThreads>(s, wsum, tot);
+        uint64_t S = tot - pre;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            sfx[4 * tid + i] = S;
+            S -= v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) binmap[4 * tid + i] = -1;
+    }
+    __syncthreads();
+    if (tid < L) {
+        // (a negative budget takes nothing, as 0 does: every segment has bytes)
+        const int64_t T = a.budget[tid] < 0 ? 0 : a.budget[tid];
+        int b = -1;
+        if ((int64_t)sfx[0] > T) {  // the largest bin b with S(b) > T
+            int lo = 0, hi = kPcrdBins - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if ((int64_t)sfx[mid] > T) lo = mid;
+                else hi = mid - 1;
+            }
+            b = lo;
+        }
+        lbin[tid] = b;
+        lneed[tid] = b < 0 ? 0 : T - (int64_t)(b + 1 < kPcrdBins ? sfx[b + 1] : 0ull);
+    }
+    __syncthreads();
+    if (tid == 0) {  // one candidate list per distinct bin
+        int n = 0;
+        uint32_t o = 0;
+        for (int l = 0; l < L; l++) {
+            if (lbin[l] < 0) continue;
+            int i = 0;
+            while (i < n && list_bin[i] != lbin[l]) i++;
+            if (i == n) {
+                list_bin[n] = lbin[l];
+                list_off[n] = o;
+                o += a.hcount[lbin[l]];
+                binmap[lbin[l]] = (int8_t)n;
+                n++;
+            }
+            lli[l] = i;
+        }
+        list_off[n] = o;
+        nlist = n;
+    }
+    __syncthreads();
+    // 2. candidates of those bins, thread per code-block
+    if (nlist > 0)
+        for (int b = blockIdx.x * kSelThreads + tid; b < a.nblocks; b += gridDim.x * kSelThreads) {
+            const int nh = a.nhull[b];
+            const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
+            const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
+            const int32_t *R = a.rates + (size_t)b * kMaxPasses;
+            for (int i = 1; i < nh; i++) {
+                const uint64_t key = hk[i];
+                const int li = binmap[pcrd_bin(key)];
+                if (li >= 0) {
+                    const int32_t r1 = R[hp[i] - 1];
+                    const uint32_t at = list_off[li] + atomicAdd(&a.ctl[1 + li], 1u);
+                    a.lkey[at] = key;
+                    a.lsize[at] = (uint32_t)(r1 - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
+                }
+            }
+        }
+    // 3. publish (release, ticket); the last workgroup acquires and resolves
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int g0 = 0; g0 < L; g0 += kSelGroup) {
+        const int ng = min(kSelGroup, L - g0);
+        if (tid < ng) {
+            rpre[g0 + tid] = 0;
+            racc[g0 + tid] = 0;
+        }
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            for (int i = tid; i < kSelGroup * 256; i += kSelThreads) (&rh[0][0])[i] = 0;
+            __syncthreads();
+            for (int j = 0; j < ng; j++) {
+                const int l = g0 + j;
+                if (lbin[l] < 0) continue;
+                const int li = lli[l];
+                const uint64_t pre = rpre[l];
+                for (uint32_t i = list_off[li] + tid; i < list_off[li + 1]; i += kSelThreads) {
+                    const uint64_t key = a.lkey[i];
+                    if (shift == 56 || (key >> (shift + 8)) == (pre >> (shift + 8)))
+                        atomicAdd(&rh[j][(key >> shift) & 255u], (unsigned long long)a.lsize[i]);
+                }
+            }
+            __syncthreads();
+            if (wv < ng && lbin[g0 + wv] >= 0) {  // one wave per layer picks the digit
+                const int l = g0 + wv;
+                uint64_t v[4], s = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) s += (v[k] = rh[wv][4 * lane + k]);
+                const uint64_t inc = wave_incl_scan64(s);
+                const unsigned long long tot = (unsigned long long)__shfl((long long)inc, 63, 64);
+                const int64_t need = lneed[l] - (int64_t)racc[l];
+                // S_d = bytes of digits >= d; the largest d with S_d > need
+                unsigned long long Sd = tot - inc;  // digits above this lane's four
+                int dk = -1;
+                unsigned long long Sabove = 0;
+#pragma unroll
+                for (int k = 3; k >= 0; k--) {
+                    const unsigned long long up = Sd;
+                    Sd += v[k];
+                    if (dk < 0 && (int64_t)Sd > need) {
+                        dk = k;
+                        Sabove = up;
+                    }
+                }
+                const uint64_t m = __ballot(dk >= 0);
+                const int src = 63 - __builtin_clzll(m);  // (m != 0: the bin's bytes exceed need)
+                if (lane == src) {
+                    rpre[l] |= (uint64_t)(4 * lane + dk) << shift;
+                    racc[l] += Sabove;
+                }
+            }
+            __syncthreads();
+        }
+        if (tid < ng) {
+            const int l = g0 + tid;
+            const uint64_t k = lbin[l] < 0 ? 0ull : rpre[l] + 1;
+            a.K[l] = k;
+            a.Kc[l] = k;
+        }
+        __syncthreads();
+    }
+    if (tid <= nlist) a.ctl[tid] = 0u;  // ticket and fill counters, for the next launch
+}
+
+// Split path only (GpuEncoder::segments): every hull segment listed
+// (key, bytes), for the host-side exact exchange.  Segment counts (hull
+// points - 1) and their exclusive scan, one workgroup; rounds of 32
+// consecutive blocks per thread, their 32 byte loads in flight together
 constexpr int kSegThreads = 1024, kSegPer = 32;
 __global__ void __launch_bounds__(kSegThreads) k_seg_offsets(int nblocks, const uint8_t *nhull, int32_t *nseg,
                                                              int32_t *segoff) {
@@ -948,13 +1191,7 @@ __global__ void __launch_bounds__(kSegThreads) k_seg_offsets(int nblocks, const 
 // (up to the bound `nbound`) get key 0 and size 0
 __global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nhull, const uint8_t *hpass,
                                                   const uint64_t *hkey, const int32_t *rates,
-                                                  const int32_t *segoff, const int32_t *nseg, int nbound,
-                                                  uint64_t *keys, int64_t *vals) {
-    const int total = segoff[nblocks - 1] + nseg[nblocks - 1];
-    for (int i = total + blockIdx.x * blockDim.x + threadIdx.x; i < nbound; i += gridDim.x * blockDim.x) {
-        keys[i] = 0;
-        vals[i] = 0;
-    }
+                                                  const int32_t *segoff, uint64_t *keys, int64_t *vals) {
     int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblocks) return;
     int nh = nhull[b];
@@ -966,35 +1203,6 @@ __global__ void __launch_bounds__(256) k_seg_emit(int nblocks, const uint8_t *nh
         keys[o + i - 1] = hk[i];
         vals[o + i - 1] = (int64_t)(R[hp[i] - 1] - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
     }
-}
-
-// one thread per layer: threshold key K (UINT64_MAX = nothing fits), and Kc,
-// the Kdu-Layer-Info slope: one above the first key not taken, 0 if every
-// segment is taken (= the tile-split bisection's K'; oracle select_threshold)
-__global__ void k_thresh(int nseg, int layers, const uint64_t *keys, const int64_t *cum,
-                         const int64_t *budget, uint64_t *K, uint64_t *Kc, const int *halt) {
-    int l = threadIdx.x;
-    if (l >= layers || (halt && *halt)) return;
-    int64_t bgt = budget[l];
-    int lo = 0, hi = nseg;  // first index with cum > bgt
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (cum[mid] <= bgt) lo = mid + 1;
-        else hi = mid;
-    }
-    int j = lo - 1;
-    if (j >= 0 && j + 1 < nseg && keys[j + 1] == keys[j]) {
-        uint64_t kj = keys[j];
-        int l2 = 0, h2 = j;  // first index whose key == kj (keys descending)
-        while (l2 < h2) {
-            int mid = (l2 + h2) >> 1;
-            if (keys[mid] > kj) l2 = mid + 1;
-            else h2 = mid;
-        }
-        j = l2 - 1;
-    }
-    K[l] = (j >= 0) ? keys[j] : 0xFFFFFFFFFFFFFFFFull;
-    Kc[l] = (j + 1 < nseg && keys[j + 1] != 0) ? keys[j + 1] + 1 : 0ull;  // key 0 = padding
 }
 
 // last hull index whose key >= K (0 = nothing); hull keys strictly decrease
@@ -1058,11 +1266,11 @@ GpuEncoder::~GpuEncoder() {
     DevBuf *all[] = {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
                      &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &segcnt, &segoff, &segkey,
-                     &segkey2, &segval, &segval2, &segcum, &thr, &cubtmp, &items, &slotoff,
+                     &segval, &thr, &items, &slotoff, &pcrd_hb, &pcrd_hc, &sel_ctl, &sel_key, &sel_size,
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
-                     &t1ord, &nitems_d};
+                     &t1fill};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -1187,9 +1395,7 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
         ua.dst = (uint8_t *)stage.ptr;
         ua.only = nullptr;
         ua.err = (int *)this->err.ptr;
-        if (lay.compression == 5 && getenv("JP2HIP_LZW_SERIAL")) {  // experiment knob: one lane per strip
-            hipLaunchKernelGGL(k_unlzw, dim3(ns), dim3(1), 0, stream, ua);
-        } else if (lay.compression == 5) {  // segment-parallel (lzw.hip)
+        if (lay.compression == 5) {  // segment-parallel (lzw.hip)
             std::vector<uint64_t> slice;
             const uint64_t segs = lzw_slices(lay.strip_bytes, ns, slice);
             if (!ensure<uint8_t>(lzwseg, lzw_scratch_bytes(ns, segs), err) ||
@@ -1294,10 +1500,16 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     uint64_t stream_bound = 0;
     for (int i = 0; i < nb; i++)
         stream_bound += (uint64_t)plan.blocks[i].Mb * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
-    if (!ensure<int32_t>(t1ord, nb, err) || !ensure<uint64_t>(slotoff, nb, err) ||
-        !ensure<uint8_t>(stream_buf, std::max<uint64_t>(stream_bound, 1), err) ||
-        !h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err))
+    if (!ensure<uint64_t>(slotoff, nb, err) || !ensure<uint8_t>(stream_buf, std::max<uint64_t>(stream_bound, 1), err))
         return false;
+    // the strip offsets: uploaded only when they differ from the last upload
+    // (repeat encodes of one layout skip the copy)
+    if (strips.ptr != strips_dev || strips_host.size() != (size_t)lay.nstrips ||
+        std::memcmp(strips_host.data(), lay.strip_offsets, sizeof(uint64_t) * lay.nstrips) != 0) {
+        if (!h2d(strips.ptr, lay.strip_offsets, sizeof(uint64_t) * lay.nstrips, err)) return false;
+        strips_host.assign(lay.strip_offsets, lay.strip_offsets + lay.nstrips);
+        strips_dev = strips.ptr;
+    }
     // the plan's tables stay resident while the context encodes the same
     // geometry (plan.gen; buffers only grow, so they are still in place)
     if (!plan.gen || plan.gen != front_gen) {
@@ -1305,8 +1517,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!h2d(blocks.ptr, plan.blocks.data(), sizeof(BlockDesc) * nb, err) ||
             !h2d(weight.ptr, plan.weight.data(), sizeof(double) * nb, err) ||
             !h2d(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, err) ||
-            !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err) ||
-            !h2d(t1ord.ptr, plan.t1_order.data(), sizeof(int32_t) * nb, err))
+            !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err))
             return false;
         std::vector<uint64_t> slots(nb);
         uint64_t o = 0;
@@ -1317,16 +1528,18 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (nb && !h2d(slotoff.ptr, slots.data(), sizeof(uint64_t) * nb, err)) return false;
         front_gen = plan.gen;
     }
-    HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
+    // (the error word is zeroed by k_quant, which every encode with blocks runs)
+    if (!nb) HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
 
     HIPCHECK(hipEventRecord(ev[0], stream));
     HIPCHECK(hipEventRecord(ev[1], stream));
+    // every stage's device buffer written to files: a debug build only
+    // (make JP2HIP_DEBUG=1), for the tools in tests/tools
+#ifdef JP2HIP_DEBUG_DUMPS
     const char *dd = getenv("JP2HIP_DUMP_DIR");
-    // experiment knob: launch one stage twice (its marginal cost under load)
-    const char *rep = getenv("JP2HIP_REPEAT_STAGE");
-    const int nrep_dwt = rep && !strcmp(rep, "dwt") ? 2 : 1, nrep_quant = rep && !strcmp(rep, "quant") ? 2 : 1;
-    const int nrep_cm = rep && !strcmp(rep, "cm") ? 2 : 1, nrep_mq = rep && !strcmp(rep, "mq") ? 2 : 1;
-    const int nrep_pcrd = rep && !strcmp(rep, "pcrd") ? 2 : 1;
+#else
+    const char *dd = nullptr;
+#endif
     if (plan.rc.levels == 0) {
         // S1+S2 only: no decomposition
         IngestArgs ia;
@@ -1361,11 +1574,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
         dl.coef = coef.ptr; dl.scratch0 = llbuf0.ptr; dl.scratch1 = llbuf1.ptr;
-        for (int r = 0; r < nrep_dwt; r++)
-            if (!launch_dwt(dl, stream)) {
-                err = std::string("DWT launch failed: ") + hipGetErrorString(hipGetLastError());
-                return false;
-            }
+        if (!launch_dwt(dl, stream)) {
+            err = std::string("DWT launch failed: ") + hipGetErrorString(hipGetLastError());
+            return false;
+        }
     }
     HIPCHECK(hipEventRecord(ev[2], stream));
     if (dd && !dump(dd, "dwt.bin", coef, plane * plan.ntc * 4, err)) return false;
@@ -1383,16 +1595,58 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.est = (uint32_t *)est.ptr;
     qa.nblocks = nb;
     qa.keep_sm = dd != nullptr;
-    qa.max_mb = 1;
-    for (int i = 0; i < nb; i++) qa.max_mb = std::max(qa.max_mb, (int)plan.blocks[i].Mb);
+    // tier-1 work lists and lane order, slope prediction, PCRD: their
+    // counters are zeroed by k_quant's first workgroup (no memset launches)
+    int kmax = 0;
+    for (int i = 0; i < nb; i++) kmax = std::max(kmax, (int)plan.blocks[i].Mb);
+    const size_t nflags = (size_t)nb * kmax;
+    if (!ensure<unsigned long long>(pcrd_hb, kPcrdBins, err) || !ensure<uint32_t>(pcrd_hc, kPcrdBins, err) ||
+        !ensure<uint32_t>(sel_ctl, kMaxLayers + 1, err) || !ensure<uint32_t>(t1fill, 64 + kOrderBuckets, err) ||
+        !ensure<int32_t>(items, std::max<size_t>(nflags, 1), err) ||
+        !ensure<int32_t>(order, (size_t)kOrderBuckets * std::max(nb, 1), err) ||
+        !ensure<uint4>(counts, (size_t)nb * 32, err) || !ensure<int64_t>(dspp, (size_t)nb * 32, err) ||
+        !ensure<unsigned long long>(ordkey, std::max(nb, 1), err) || !ensure<unsigned long long>(mqspan, 2, err))
+        return false;
+    uint32_t *dfill = (uint32_t *)t1fill.ptr, *bfill = dfill + 64;
+    std::memset(qa.zero, 0, sizeof qa.zero);
+    std::memset(qa.nzero, 0, sizeof qa.nzero);
+    qa.zero[0] = (uint32_t *)pcrd_hb.ptr;
+    qa.nzero[0] = 2 * kPcrdBins;
+    qa.zero[1] = (uint32_t *)pcrd_hc.ptr;
+    qa.nzero[1] = kPcrdBins;
+    qa.zero[2] = (uint32_t *)sel_ctl.ptr;
+    qa.nzero[2] = kMaxLayers + 1;
+    qa.zero[3] = dfill;
+    qa.nzero[3] = 64 + kOrderBuckets;
+    qa.zero[4] = (uint32_t *)mqspan.ptr;
+    qa.nzero[4] = 4;
+    qa.zero[5] = (uint32_t *)this->err.ptr;
+    qa.nzero[5] = 1;
+    if (skip_target > 0) {
+        if (!ensure<unsigned long long>(hist, kSlopeBins, err)) return false;
+        qa.zero[6] = (uint32_t *)hist.ptr;
+        qa.nzero[6] = 2 * kSlopeBins;
+    }
+    qa.max_mb = std::max(1, kmax);
     const size_t qlds = (size_t)qa.max_mb * 64 * sizeof(uint64_t);
-    for (int r = 0; nb && r < nrep_quant; r++) {
+    if (nb) {
         const dim3 gq((nb + kQuantWaves - 1) / kQuantWaves), bq(64 * kQuantWaves);
         if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, gq, bq, qlds * kQuantWaves, stream, qa);
         else hipLaunchKernelGGL(k_quant<false>, gq, bq, qlds * kQuantWaves, stream, qa);
     }
     HIPCHECK(hipGetLastError());
-    // S4b: slope prediction -> lowest coded plane per block
+    // S4b: slope prediction -> lowest coded plane per block, and the tier-1
+    // work lists: list k = the blocks with more than k coded planes
+    T1ItemArgs ia;
+    ia.nb = nb;
+    ia.kmax = kmax;
+    ia.P = (const uint8_t *)P.ptr;
+    ia.pmin = (uint8_t *)pmin.ptr;
+    ia.dfill = dfill;
+    ia.dlist = (int32_t *)items.ptr;
+    ia.acc = (unsigned long long *)ordkey.ptr;
+    ia.npasses = (uint8_t *)npasses.ptr;
+    ia.lengths = (int32_t *)lengths.ptr;
     if (skip_target > 0 && nb) {
         PredictArgs pa;
         pa.nblocks = nb;
@@ -1404,7 +1658,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         pa.hist = (unsigned long long *)hist.ptr;
         pa.kcut = (int *)kcut.ptr;
         pa.pmin = (uint8_t *)pmin.ptr;
-        HIPCHECK(hipMemsetAsync(hist.ptr, 0, sizeof(unsigned long long) * kSlopeBins, stream));
         hipLaunchKernelGGL(k_plane_hist, dim3((nb * 32 + 255) / 256), dim3(256), 0, stream, pa);
         HIPCHECK(hipGetLastError());
         if (reduce) {
@@ -1421,31 +1674,23 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         }
         hipLaunchKernelGGL(k_plane_cut, dim3(1), dim3(64), 0, stream, (const unsigned long long *)hist.ptr,
                            skip_target * 128, (int *)kcut.ptr);
-        hipLaunchKernelGGL(k_plane_pmin, dim3((nb + 255) / 256), dim3(256), 0, stream, pa);
+        hipLaunchKernelGGL(k_plane_pmin, dim3((nb + 255) / 256), dim3(256), 0, stream, pa, ia);
         HIPCHECK(hipGetLastError());
-    } else if (nb) {
-        HIPCHECK(hipMemsetAsync(pmin.ptr, 0, nb, stream));
+    } else {
+        launch_t1_items(ia, stream);
+        HIPCHECK(hipGetLastError());
     }
     HIPCHECK(hipEventRecord(ev[3], stream));
-    // S5: tier-1.  Items (block, plane) ordered by plane depth from the top,
-    // then by block shape, so a wavefront's lanes do similar work.  The list
-    // and the blocks' stream slots are built on the device (t1.hip
-    // k_t1_worklist, one workgroup) from the coded plane counts; buffers and the
-    // grid are sized by the plan's bound (every plane of every block coded).
-    int kmax = 0;
-    for (int i = 0; i < nb; i++) kmax = std::max(kmax, (int)plan.blocks[i].Mb);
-    const size_t nflags = (size_t)nb * kmax;
-    if (!ensure<int2>(items, std::max<size_t>(nflags, 1), err) || !ensure<uint4>(counts, (size_t)nb * 32, err) ||
-        !ensure<int64_t>(dspp, (size_t)nb * 32, err) || !ensure<int>(nitems_d, 1, err) ||
-        !ensure<uint32_t>(ordkey, nb, err) || !ensure<unsigned long long>(mqspan, 2, err))
-        return false;
-    launch_t1_worklist(nb, kmax, (const int32_t *)t1ord.ptr, (const uint8_t *)P.ptr, (const uint8_t *)pmin.ptr,
-                       (uint32_t *)ordkey.ptr, (int2 *)items.ptr, (int *)nitems_d.ptr, stream);
-    HIPCHECK(hipGetLastError());
+    // S5: tier-1.  k_t1_cm3 takes the items depth by depth; each block's last
+    // plane files it in its MQ lane-order bucket (decision count), which
+    // k_t1_mq reads.  Buffers and the grid are sized by the plan's bound
+    // (every plane of every block coded).
     HIPCHECK(hipEventRecord(ev[10], stream));
     T1CmArgs ca;
-    ca.items = (const int2 *)items.ptr;
-    ca.nitems = (const int *)nitems_d.ptr;
+    ca.dfill = dfill;
+    ca.dlist = (const int32_t *)items.ptr;
+    ca.nb = nb;
+    ca.kmax = kmax;
     ca.max_items = (int)nflags;
     ca.blocks = (const BlockDesc *)blocks.ptr;
     ca.bp = (const uint64_t *)bp.ptr;
@@ -1455,20 +1700,17 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ca.slot_off = (const uint64_t *)slotoff.ptr;
     ca.counts = (uint4 *)counts.ptr;
     ca.dspp = (int64_t *)dspp.ptr;
-    ca.keys = (uint32_t *)ordkey.ptr;
+    ca.acc = (unsigned long long *)ordkey.ptr;
+    ca.bfill = bfill;
+    ca.bslots = (int32_t *)order.ptr;
     ca.lossless = plan.rc.reversible;
-    for (int r = 0; r < nrep_cm; r++) {
-        if (r) HIPCHECK(hipMemsetAsync(ordkey.ptr, 0xff, sizeof(uint32_t) * nb, stream));  // (stage-repeat knob)
-        launch_t1_cm(ca, stream);
-    }
-    HIPCHECK(hipGetLastError());
-    // MQ lane order: blocks by decreasing decision count (bucketed)
-    launch_t1_order(nb, (const uint32_t *)ordkey.ptr, (int32_t *)order.ptr, (unsigned long long *)mqspan.ptr, stream);
+    launch_t1_cm(ca, stream);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[11], stream));
     T1MqArgs ma;
     ma.blocks = (const BlockDesc *)blocks.ptr;
-    ma.order = (const int32_t *)order.ptr;
+    ma.bfill = bfill;
+    ma.bslots = (const int32_t *)order.ptr;
     ma.nblocks = nb;
     ma.P = (const uint8_t *)P.ptr;
     ma.pmin = (const uint8_t *)pmin.ptr;
@@ -1484,24 +1726,17 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ma.npasses = (uint8_t *)npasses.ptr;
     ma.lengths = (int32_t *)lengths.ptr;
     ma.err = (int *)this->err.ptr;
-    {
-        const char *e = getenv("JP2HIP_MQ_LANES");
-        ma.lanes = std::max(1, std::min(64, e ? atoi(e) : 64));
-    }
     ma.dbg = nullptr;
-
-    if (!ensure<unsigned long long>(mqspan, 2, err)) return false;
     ma.span = (unsigned long long *)mqspan.ptr;
     if (dd) {
         if (!ensure<int64_t>(dbgbuf, (size_t)nb * 4, err)) return false;
         ma.dbg = (int64_t *)dbgbuf.ptr;
     }
-    for (int r = 0; r < nrep_mq; r++) launch_t1_mq(ma, stream);
+    launch_t1_mq(ma, stream);
 
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[4], stream));
-    for (int rp = 0; rp < nrep_pcrd; rp++) {
-    // S6a hulls
+    // S6a hulls + their slope-bin histogram (k_select resolves thresholds)
     HullArgs ha;
     ha.nblocks = nb;
     ha.npasses = (const uint8_t *)npasses.ptr;
@@ -1512,40 +1747,17 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ha.hpass = (uint8_t *)hpass.ptr;
     ha.hkey = (uint64_t *)hkey.ptr;
     ha.hdist = (int64_t *)hdist.ptr;
-    if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + 255) / 256), dim3(256), 0, stream, ha);
+    ha.hbytes = (unsigned long long *)pcrd_hb.ptr;
+    ha.hcount = (uint32_t *)pcrd_hc.ptr;
+    if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + kHullThreads - 1) / kHullThreads), dim3(kHullThreads), 0, stream, ha);
     HIPCHECK(hipGetLastError());
-    // hull segments of all blocks, sorted by slope key (descending), sizes prefix-summed
-    if (!ensure<int32_t>(segcnt, nb, err) || !ensure<int32_t>(segoff, nb, err)) return false;
-    if (nb) hipLaunchKernelGGL(k_seg_offsets, dim3(1), dim3(kSegThreads), 0, stream, nb,
-                               (const uint8_t *)nhull.ptr, (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr);
-    // the segment arrays have the bound's length (no host wait for the real
-    // count): unused entries keep key 0 and size 0, sort after every real
-    // key (slopes are > 0) and leave the prefix sums flat
+    // candidate lists: room for every hull segment (the bound sum(3 Mb - 2))
     int64_t nseg_bound = 0;
     for (int i = 0; i < nb; i++) nseg_bound += std::max(0, 3 * (int)plan.blocks[i].Mb - 2);
     nseg = (int)nseg_bound;
-    if (!ensure<uint64_t>(segkey, std::max(nseg, 1), err) || !ensure<uint64_t>(segkey2, std::max(nseg, 1), err) ||
-        !ensure<int64_t>(segval, std::max(nseg, 1), err) || !ensure<int64_t>(segval2, std::max(nseg, 1), err) ||
-        !ensure<int64_t>(segcum, std::max(nseg, 1), err) || !ensure<uint64_t>(thr, 2 * kMaxLayers, err))
+    if (!ensure<uint64_t>(sel_key, std::max(nseg, 1), err) || !ensure<uint32_t>(sel_size, std::max(nseg, 1), err) ||
+        !ensure<uint64_t>(thr, 2 * kMaxLayers, err))
         return false;
-    if (nb) hipLaunchKernelGGL(k_seg_emit, dim3((nb + 255) / 256), dim3(256), 0, stream, nb,
-                               (const uint8_t *)nhull.ptr, (const uint8_t *)hpass.ptr,
-                               (const uint64_t *)hkey.ptr, (const int32_t *)rates.ptr,
-                               (const int32_t *)segoff.ptr, (const int32_t *)segcnt.ptr, nseg,
-                               (uint64_t *)segkey.ptr, (int64_t *)segval.ptr);
-    if (nseg > 0) {
-        size_t tb = 0;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,
-                                                              (int64_t *)segval.ptr, (int64_t *)segval2.ptr, nseg, 0, 64, stream));
-        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
-        HIPCHECK(hipcub::DeviceRadixSort::SortPairsDescending(cubtmp.ptr, tb, (uint64_t *)segkey.ptr, (uint64_t *)segkey2.ptr,
-                                                              (int64_t *)segval.ptr, (int64_t *)segval2.ptr, nseg, 0, 64, stream));
-        tb = 0;
-        HIPCHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
-        if (!ensure<uint8_t>(cubtmp, tb, err)) return false;
-        HIPCHECK(hipcub::DeviceScan::InclusiveSum(cubtmp.ptr, tb, (int64_t *)segval2.ptr, (int64_t *)segcum.ptr, nseg, stream));
-    }
-    }  // nrep_pcrd
     HIPCHECK(hipEventRecord(ev[5], stream));
     profiled = profile;
     if (dd) {
@@ -1573,7 +1785,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
 // encode's final host wait returned).
 bool GpuEncoder::collect_profile(StageTimes &st, std::string &err) {
     if (!profiled || !h_tot) return true;
-    const uint64_t span[2] = {(uint64_t)h_tot[2], (uint64_t)h_tot[3]};  // read back by t2_emit
     float t;
     HIPCHECK(hipEventElapsedTime(&t, ev[0], ev[1])); st.ingest = t;
     HIPCHECK(hipEventElapsedTime(&t, ev[1], ev[2])); st.dwt = t;
@@ -1581,11 +1792,8 @@ bool GpuEncoder::collect_profile(StageTimes &st, std::string &err) {
     HIPCHECK(hipEventElapsedTime(&t, ev[10], ev[11])); st.t1_cm = t;
     // k_t1_mq from HIP events on the context's stream around its launch, as
     // rocprofv3 times a dispatch (from when the queue reaches it: under load
-    // that includes waiting for CUs).  span[] is the kernel's own execution
-    // span (first wave start .. last lane end, 100 MHz wall clock), kept for
-    // the MQ census tool.
+    // that includes waiting for CUs)
     HIPCHECK(hipEventElapsedTime(&t, ev[11], ev[4])); st.t1_mq = t;
-    (void)span;
     HIPCHECK(hipEventElapsedTime(&t, ev[4], ev[5])); st.pcrd += t;
     return true;
 }
@@ -1595,11 +1803,32 @@ bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets, s
     const int L = plan.rc.layers;
     if (!h2d(budget.ptr, budgets.data(), sizeof(int64_t) * L, err)) return false;
     HIPCHECK(hipEventRecord(ev[6], stream));
-    hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
-                       (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
-                       (uint64_t *)thr.ptr + kMaxLayers, (const int *)nullptr);
+    select_launch(plan, nullptr);
     HIPCHECK(hipGetLastError());
     return apply_thresholds(plan, nullptr, err);
+}
+
+// k_select for the budgets in `budget` (thresholds -> thr[0..L), Kc -> thr[kMaxLayers..))
+void GpuEncoder::select_launch(const Plan &plan, const int *halt) {
+    const int nb = (int)plan.blocks.size();
+    if (!nb) return;
+    SelectArgs sa;
+    sa.halt = halt;
+    sa.nblocks = nb;
+    sa.layers = plan.rc.layers;
+    sa.nhull = (const uint8_t *)nhull.ptr;
+    sa.hpass = (const uint8_t *)hpass.ptr;
+    sa.hkey = (const uint64_t *)hkey.ptr;
+    sa.rates = (const int32_t *)rates.ptr;
+    sa.hbytes = (const unsigned long long *)pcrd_hb.ptr;
+    sa.hcount = (const uint32_t *)pcrd_hc.ptr;
+    sa.budget = (const int64_t *)budget.ptr;
+    sa.lkey = (uint64_t *)sel_key.ptr;
+    sa.lsize = (uint32_t *)sel_size.ptr;
+    sa.ctl = (uint32_t *)sel_ctl.ptr;
+    sa.K = (uint64_t *)thr.ptr;
+    sa.Kc = (uint64_t *)thr.ptr + kMaxLayers;
+    hipLaunchKernelGGL(k_select, dim3((nb + kSelThreads - 1) / kSelThreads), dim3(kSelThreads), 0, stream, sa);
 }
 
 // lossless "-rate -": layer l's budget is total >> (L-1-l), total = every
@@ -1624,9 +1853,7 @@ bool GpuEncoder::select_lossless(const Plan &plan, std::string &err) {
     HIPCHECK(hipEventRecord(ev[6], stream));
     hipLaunchKernelGGL(k_budget_lossless, dim3(1), dim3(256), 0, stream, nb, (const int32_t *)lengths.ptr, L,
                        (int64_t *)budget.ptr);
-    hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
-                       (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
-                       (uint64_t *)thr.ptr + kMaxLayers, (const int *)nullptr);
+    select_launch(plan, nullptr);
     HIPCHECK(hipGetLastError());
     return apply_thresholds(plan, nullptr, err);
 }
@@ -1678,16 +1905,29 @@ __global__ void k_rate_init(RateState *rs, RateState init, int L, int64_t *budge
     *rs = r;
     rate_budgets(r, L, budget);
 }
-__global__ void k_rate_step(RateState *rs, const T2Summary *sum, int L, int64_t *budget) {
+// Each iteration that runs also leaves the state and the summary it decided
+// on in host-mapped memory (out_rs, out_sum): the host reads them after its
+// wait with no copy launches.
+__device__ __forceinline__ void rate_out(const RateState &r, const T2Summary *sum, RateState *out_rs,
+                                         T2Summary *out_sum) {
+    *out_rs = r;
+    *out_sum = *sum;
+}
+__global__ void k_rate_step(RateState *rs, const T2Summary *sum, int L, int64_t *budget, RateState *out_rs,
+                            T2Summary *out_sum) {
     RateState r = *rs;
     if (r.halt) return;
     if (sum->err) {  // tier-1 overflow: the host reports it
-        rs->halt = 1;
+        r.halt = 1;
+        *rs = r;
+        rate_out(r, sum, out_rs, out_sum);
         return;
     }
     if (r.it == 0 && r.skip_target > 0 && sum->skipped && sum->t1_bytes < r.skip_target) {
-        rs->safety = 1;
-        rs->halt = 1;
+        r.safety = 1;
+        r.halt = 1;
+        *rs = r;
+        rate_out(r, sum, out_rs, out_sum);
         return;
     }
     r.iters++;
@@ -1703,6 +1943,7 @@ __global__ void k_rate_step(RateState *rs, const T2Summary *sum, int L, int64_t 
         rate_budgets(r, L, budget);
     }
     *rs = r;
+    rate_out(r, sum, out_rs, out_sum);
 }
 
 bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart, int batch, bool profile,
@@ -1710,29 +1951,29 @@ bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart
     HIPCHECK(hipSetDevice(device));
     const int L = plan.rc.layers;
     if (!ensure<RateState>(rstate, 1, err)) return false;
-    if (!h_rs) HIPCHECK(hipHostMalloc((void **)&h_rs, sizeof(RateState), hipHostMallocDefault));
+    if (!h_rs) {  // host-mapped: k_rate_step writes the state and summary here
+        HIPCHECK(hipHostMalloc((void **)&h_rs, sizeof(RateState) + sizeof(T2Summary), hipHostMallocMapped));
+        HIPCHECK(hipHostGetDevicePointer((void **)&d_rs_out, h_rs, 0));
+    }
+    RateState *o_rs = d_rs_out;
+    T2Summary *o_sum = (T2Summary *)(d_rs_out + 1);
     RateState *d = (RateState *)rstate.ptr;
-    static const bool rep_t2 = getenv("JP2HIP_REPEAT_STAGE") && !strcmp(getenv("JP2HIP_REPEAT_STAGE"), "t2");
     const int *halt = &d->halt;
     HIPCHECK(hipEventRecord(ev[6], stream));
     if (restart) hipLaunchKernelGGL(k_rate_init, dim3(1), dim3(1), 0, stream, d, init, L, (int64_t *)budget.ptr);
     for (int i = 0; i < batch; i++) {
-        hipLaunchKernelGGL(k_thresh, dim3(1), dim3(64), 0, stream, nseg, L, (const uint64_t *)segkey2.ptr,
-                           (const int64_t *)segcum.ptr, (const int64_t *)budget.ptr, (uint64_t *)thr.ptr,
-                           (uint64_t *)thr.ptr + kMaxLayers, halt);
+        select_launch(plan, halt);
         if (!apply_thresholds(plan, halt, err)) return false;
         t2_size_launch(plan, true, halt);
-        if (rep_t2) t2_size_launch(plan, true, halt);  // experiment knob (JP2HIP_REPEAT_STAGE=t2)
         hipLaunchKernelGGL(k_rate_step, dim3(1), dim3(1), 0, stream, d, (const T2Summary *)t2sum.ptr, L,
-                           (int64_t *)budget.ptr);
+                           (int64_t *)budget.ptr, o_rs, o_sum);
     }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipMemcpyAsync(h_sum, t2sum.ptr, sizeof(T2Summary), hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(h_rs, d, sizeof(RateState), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipEventRecord(ev[9], stream));
     if (!host_wait(err)) return false;
-    sum = *h_sum;
-    rs = *h_rs;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    std::memcpy(&sum, h_rs + 1, sizeof sum);
+    std::memcpy(&rs, h_rs, sizeof rs);
     if (profile) {
         float t;
         HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[9]));
@@ -1770,23 +2011,46 @@ bool GpuEncoder::t1_totals(const Plan &plan, int64_t &bytes, std::string &err) {
 bool GpuEncoder::segments(const Plan &plan, std::vector<uint64_t> &keys, std::vector<int64_t> &cum,
                           std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    // the real segment count (the arrays are padded to the bound)
+    // every hull segment (key, bytes), listed on the device, sorted here by
+    // key, descending (the tile-split exchange's input; the single-image path
+    // never needs the whole order: k_select)
     const int nb = (int)plan.blocks.size();
+    keys.clear();
+    cum.clear();
+    if (!nb) return true;
+    if (!ensure<int32_t>(segcnt, nb, err) || !ensure<int32_t>(segoff, nb, err) ||
+        !ensure<uint64_t>(segkey, std::max(nseg, 1), err) || !ensure<int64_t>(segval, std::max(nseg, 1), err))
+        return false;
+    hipLaunchKernelGGL(k_seg_offsets, dim3(1), dim3(kSegThreads), 0, stream, nb, (const uint8_t *)nhull.ptr,
+                       (int32_t *)segcnt.ptr, (int32_t *)segoff.ptr);
+    hipLaunchKernelGGL(k_seg_emit, dim3((nb + 255) / 256), dim3(256), 0, stream, nb, (const uint8_t *)nhull.ptr,
+                       (const uint8_t *)hpass.ptr, (const uint64_t *)hkey.ptr, (const int32_t *)rates.ptr,
+                       (const int32_t *)segoff.ptr, (uint64_t *)segkey.ptr, (int64_t *)segval.ptr);
+    HIPCHECK(hipGetLastError());
     int32_t *tail = (int32_t *)(h_tot + 5);  // pinned
     tail[0] = tail[1] = 0;
-    if (nb) {
-        HIPCHECK(hipMemcpyAsync(&tail[0], (int32_t *)segoff.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
-        HIPCHECK(hipMemcpyAsync(&tail[1], (int32_t *)segcnt.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
-    }
+    HIPCHECK(hipMemcpyAsync(&tail[0], (int32_t *)segoff.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(&tail[1], (int32_t *)segcnt.ptr + nb - 1, 4, hipMemcpyDeviceToHost, stream));
     if (!host_wait(err)) return false;
     const int n = tail[0] + tail[1];
-    keys.resize((size_t)n);
-    cum.resize((size_t)n);
+    std::vector<uint64_t> k((size_t)n);
+    std::vector<int64_t> v((size_t)n);
     if (n > 0) {
-        HIPCHECK(hipMemcpyAsync(keys.data(), segkey2.ptr, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, stream));
-        HIPCHECK(hipMemcpyAsync(cum.data(), segcum.ptr, sizeof(int64_t) * n, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(k.data(), segkey.ptr, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(v.data(), segval.ptr, sizeof(int64_t) * n, hipMemcpyDeviceToHost, stream));
     }
     if (!host_wait(err)) return false;
+    std::vector<int> idx((size_t)n);
+    for (int i = 0; i < n; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int x, int y) { return k[x] > k[y]; });
+    keys.resize((size_t)n);
+    cum.resize((size_t)n);
+    int64_t acc = 0;
+    for (int i = 0; i < n; i++) {
+        keys[i] = k[idx[i]];
+        acc += v[idx[i]];
+        cum[i] = acc;
+    }
     return true;
 }
 

@@ -50,6 +50,21 @@ __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
 
 constexpr int kCmWaves = 4;  // items per workgroup
 
+// MQ lane order: blocks by decreasing decision count, so the lanes of an MQ
+// wave carry similar work.  The order only groups blocks (it changes no
+// output): bucket = 8 * floor(log2(n + 1)) + the next 3 bits of n + 1 (12.5 %
+// wide), largest first; inside a bucket the order is whatever the atomics
+// give.  k_t1_cm3's last plane of a block files it (bslots[bucket][i]);
+// k_t1_mq maps its lanes through the bucket fills' prefix.
+constexpr unsigned long long kAccMask = (1ull << 40) - 1ull;
+__device__ __forceinline__ int order_bucket(uint32_t n) {
+    const uint32_t v = n + 1u;
+    const int e = 31 - __clz(v);                                      // 0..31
+    const int f = e >= 3 ? (int)((v >> (e - 3)) & 7u) : (int)((v << (3 - e)) & 7u);
+    return kOrderBuckets - 1 - min(kOrderBuckets - 1, 8 * e + f);   // descending
+}
+
+
 // --------------------------------------------------------------------------
 // Context modelling on column masks.  One wavefront per (code-block,
 // bit-plane) item, in the transposed layout: lane
@@ -282,6 +297,7 @@ __device__ __forceinline__ void zc_sg_bytes(const Half &m, int sh, uint32_t &zc,
 __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
     __shared__ uint2 lut[256];
     __shared__ uint32_t rings[kCmWaves][kRingBytes / 4];
+    __shared__ uint32_t dbase[65];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // compaction selectors: entry K = members (bits 0-3) | members with a 1
@@ -298,16 +314,26 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
                             sel[4] | sel[5] << 8 | sel[6] << 16 | sel[7] << 24);
     }
     for (int i = threadIdx.x; i < kCmWaves * kRingBytes / 4; i += 64 * kCmWaves) (&rings[0][0])[i] = 0u;
+    // item = (depth k, entry) of the per-depth lists (emit_t1_items): the
+    // depth bases are an exclusive scan of the list fills
+    if (threadIdx.x < 64) {
+        const uint32_t v = threadIdx.x < (unsigned)a.kmax ? a.dfill[threadIdx.x] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        dbase[threadIdx.x + 1] = inc;
+        if (threadIdx.x == 0) dbase[0] = 0;
+    }
     __syncthreads();
-    const int nitems = *a.nitems;
+    const int nitems = (int)dbase[a.kmax];
     Ring g;
     g.r = rings[wv];
     for (int gi = blockIdx.x * kCmWaves + wv; gi < nitems; gi += gridDim.x * kCmWaves) {
-        const int2 item = a.items[gi];
-        const int b = item.x, p = item.y;
+        int k = 0;  // the depth holding item gi (wave-uniform)
+        for (int step = 32; step > 0; step >>= 1)
+            if (k + step < a.kmax && dbase[k + step] <= (uint32_t)gi) k += step;
+        const int b = a.dlist[(size_t)k * a.nb + (gi - (int)dbase[k])];
         const BlockDesc d = a.blocks[b];
         const int P = a.P[b];
-        const int k = P - 1 - p;
+        const int p = P - 1 - k;
         const bool lossless = a.lossless != 0;
         const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
         const bool vl = lane < w;
@@ -475,7 +501,16 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
             cnt.w = 0;
             a.counts[(size_t)b * 32 + k] = cnt;
             a.dspp[(size_t)b * 32 + k] = dspp;
-            atomicSub(&a.keys[b], (uint32_t)(n_spp + n_mrp + n_cup));
+            // one atomic per plane: planes left (bits 40+) down by one,
+            // decisions up; the block's last plane knows its total and files
+            // the block in its MQ lane-order bucket
+            const uint32_t nd = (uint32_t)(n_spp + n_mrp + n_cup);
+            const unsigned long long old = atomicAdd(&a.acc[b], (unsigned long long)nd - (1ull << 40));
+            if ((old >> 40) == 1ull) {
+                const uint32_t tot = (uint32_t)(old & kAccMask) + nd;
+                const int bk = order_bucket(tot);
+                a.bslots[(size_t)bk * a.nb + atomicAdd(&a.bfill[bk], 1u)] = b;
+            }
         }
     }
 }
@@ -520,21 +555,6 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
     }
 }
 
-// Context state = the 32-bit word of its (table index i, MPS symbol) pair,
-// entry e = 2 i + MPS of a 94-entry table: Qe | e(NMPS) << 16 | e(NLPS) << 23
-// with the MPS symbol in bit 31, where e(NLPS) already carries the MPS flip of
-// a SWITCH state -- the next state is one table read, no bit fix-up.
-//
-// One decision, straight-line (no branch per decision on a 64-lane wave):
-// the CODEMPS/CODELPS procedures of Annex C.2 fold into one select -- the
-// interval keeps A-Qe exactly when "MPS" xor "conditional exchange" -- the
-// context moves to NMPS/NLPS exactly when renormalisation happens, and every
-// value of RENORME is computed with selects; the (at most one, common)
-// byte-out is applied by select and its byte is written to the lane's
-// 64-byte LDS ring (written every step, see mq_step) -- so the only
-// per-decision branch is the rare second byte-out of one renormalisation.
-// Pass padding (CX_PAD, state 0) makes a step with Qe = 0 and d = MPS: no
-// interval change, no renormalisation, no byte -- so every step is coded.
 __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
     uint32_t B = m.B;
     if (B != 0xFF && m.C >= 0x8000000u) {
@@ -549,18 +569,59 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
     m.CT = ff ? 7 : 8;
 }
 
-__device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint32_t *tab, const uint32_t d,
-                                               uint8_t *ring) {
+// --------------------------------------------------------------------------
+// k_t1_mq: two waves per 64 code-blocks, a software pipeline over the MQ
+// coder's two dependency chains (Annex C.2):
+//   wave 0 (modeller) walks the blocks' decision streams with the context
+//     states and the interval register A: per decision it knows whether C
+//     gains Qe and how many bits the renormalisation shifts -- the code
+//     register's whole input -- and leaves (add | shifts << 16) in an LDS slot;
+//   wave 1 (coder) runs C, CT and the byte-outs over those words.
+// Chunks of 16 decisions per lane, double-buffered, one workgroup barrier per
+// chunk: the modeller writes chunk i + 1 while the coder codes chunk i, so a
+// decision costs the longer of the two chains, not their sum.
+//
+// Context state = the 32-bit word of its (table index i, MPS symbol) pair,
+// entry e = 2 i + MPS of a 94-entry table: Qe | e(NMPS) << 16 | e(NLPS) << 23
+// with the MPS symbol in bit 31, where e(NLPS) already carries the MPS flip of
+// a SWITCH state -- the next state is one table read, no bit fix-up.
+//
+// The CODEMPS/CODELPS procedures fold into one select -- the interval keeps
+// A - Qe exactly when "MPS" xor "conditional exchange" -- and the context
+// moves to NMPS / NLPS exactly when renormalisation happens.  Pass padding
+// (CX_PAD, state 0) makes a step with Qe = 0 and d = MPS: no interval change,
+// no shift, no byte -- so every step is coded, and lanes whose block is done
+// code padding.
+// --------------------------------------------------------------------------
+constexpr int kMqChunk = 16;
+constexpr uint32_t kPadWord = 0x01010101u * kPadDecision;
+
+// modeller: one decision; returns the context's next state, *code = the
+// coder's input word
+__device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, const uint32_t *tab, const uint32_t d,
+                                             uint32_t &code) {
     const uint32_t qe = t & 0xFFFFu;
     const bool isM = d == (t >> 31);
-    const uint32_t A1 = m.A - qe;
+    // next state: the NMPS / NLPS entry (MPS flip included), read early
+    const uint32_t tw = tab[__builtin_amdgcn_ubfe(t, isM ? 16u : 23u, 7u)];
+    const uint32_t A1 = A - qe;
     const bool keep = isM != (A1 < qe);
     const uint32_t An = keep ? A1 : qe;  // never 0: Qe >= 1, and A1 = A >= 0x8000 for Qe = 0
-    const uint32_t C0 = m.C + (keep ? qe : 0u);
     const bool ren = !isM || A1 < 0x8000u;
-    // next state: the NMPS / NLPS entry (MPS flip included)
-    const uint32_t tw = tab[__builtin_amdgcn_ubfe(t, isM ? 16u : 23u, 7u)];
-    const int n = __builtin_clz(An) - 16;  // renormalisation shifts
+    const uint32_t n = (uint32_t)__builtin_clz(An) - 16u;  // renormalisation shifts
+    A = An << n;
+    code = (keep ? qe : 0u) | (n << 16);
+    return ren ? tw : t;
+}
+
+// coder: C += add, then n shifts with their byte-outs.  The (at most one,
+// common) byte-out is applied by select and its byte written to the lane's
+// 64-byte LDS ring on every step -- so the only branch is the rare second
+// byte-out of one renormalisation.
+__device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *ring) {
+    const uint32_t add = code & 0xFFFFu;
+    const int n = (int)(code >> 16);
+    const uint32_t C0 = m.C + add;
     const int CT = m.CT;
     const bool bo = n >= CT;  // a byte-out inside this renormalisation
     const int s1 = min(n, CT);
@@ -581,7 +642,6 @@ __device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint3
     int rem = n - s1;
     m.B = bo ? (C2 >> sh) : m.B;
     m.bp += bo ? 1 : 0;
-    m.A = An << n;
     if (bo && rem >= CTx) {  // rare: a second byte-out in this renormalisation
         m.C = Cx << CTx;
         rem -= CTx;
@@ -591,7 +651,6 @@ __device__ __forceinline__ uint32_t mq_step(Mq &m, const uint32_t t, const uint3
     }
     m.C = Cx << rem;
     m.CT = CTx - rem;
-    return ren ? tw : t;
 }
 
 // Copy the lane's completed 16-byte ring groups to the code-block output.
@@ -620,91 +679,69 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
     return m.bp;
 }
 
-// One lane codes one code-block.  The block's passes are segments of the
-// decision streams (each 16-byte aligned, see k_t1_cm3); the lane walks them
-// with ONE data-driven loop -- a chunk of up to 16 decisions per iteration;
-// the segment switch and the per-pass rate record are data, not control
-// flow -- so all lanes of a wave execute the same instruction stream
-// whatever pass each is in.  Blocks are ordered by decision count
-// (k_t1_order, a one-workgroup bucket sort), so the lanes of a wave finish together.
-//
-// Segment s of a block with P coded planes: s = 0 is the top plane's cleanup
-// pass; s >= 1 is pass (s+2)%3 (0 SPP, 1 MRP, 2 CUP) of plane k = (s+2)/3,
-// planes counted from the top.
-__device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const uint32_t *mqt, uint32_t *rings);
+// LDS of one k_t1_mq workgroup
+struct MqShared {
+    uint32_t cxs[20 * 64];                 // 19 contexts + CX_PAD, lane-interleaved (modeller)
+    uint32_t mqt[94];                      // state table
+    uint32_t rings[64 * 17];               // coder: 64-byte ring per lane at a 68-byte stride (banks)
+    uint32_t bbase[kOrderBuckets + 1];     // lane order: bucket bases
+    uint32_t code[2][kMqChunk][64];        // modeller -> coder, double-buffered
+    int32_t segs[2][64];                   // passes closed before the chunk (per lane)
+    uint32_t finA[64];                     // the interval register at the end (mq_flush)
+    int32_t blk[64];                       // the lane's block, -1 none
+    int32_t more[2];                       // chunk present
+};
 
-// The launch's execution span is recorded in 100 MHz wall-clock ticks
-// (span[0] = earliest wave start, span[1] = latest lane end; vector atomics),
-// so the encoder reports the kernel's own duration -- what rocprofv3 reports
-// -- rather than an event interval that also holds time spent waiting for
-// CUs behind other images' kernels.
-__global__ void __launch_bounds__(64) k_t1_mq(T1MqArgs a) {
-    __shared__ uint32_t cxs[20 * 64];  // 19 contexts + CX_PAD, lane-interleaved
-    __shared__ uint32_t mqt[94];
-    __shared__ uint32_t rings[64 * 17];  // 64-byte ring per lane at a 68-byte stride (banks)
-
-    if (threadIdx.x == 0) atomicMin(&a.span[0], (unsigned long long)wall_clock64());
-    const int lane = threadIdx.x;
-    for (int e = lane; e < 94; e += 64) {
-        const int i = e >> 1, mps = e & 1;
-        const int sw = i == 0 || i == 6 || i == 14;
-        mqt[e] = (uint32_t)c_qe[i] | ((uint32_t)(2 * c_nmps[i] + mps) << 16) |
-                 ((uint32_t)(2 * c_nlps[i] + (mps ^ sw)) << 23) | ((uint32_t)mps << 31);
-    }
-    __syncthreads();
-    mq_block(a, cxs, mqt, rings);
-    atomicMax(&a.span[1], (unsigned long long)wall_clock64());
-}
-
-__device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const uint32_t *mqt, uint32_t *rings) {
-    const int lane = threadIdx.x;
-    uint8_t *ring = (uint8_t *)rings + lane * 68;
-    int fl = 0;  // bytes already copied from the ring
-    // only the first `lanes` lanes of each wave take a block
-    if (lane >= a.lanes) return;
-    const int gi = blockIdx.x * a.lanes + lane;
-    if (gi >= a.nblocks) return;
-    const uint64_t w0 = wall_clock64();
-    const int b = a.order[gi];
-    const BlockDesc d = a.blocks[b];
-    const int Pt = a.P[b];
-    if (Pt == 0) {
-        a.npasses[b] = 0;
-        a.lengths[b] = 0;
-        return;
-    }
-    const int P = Pt - a.pmin[b];  // coded planes Pt-1 .. pmin (slope prediction)
-    uint32_t *cx = cxs + lane;
+// Modeller (wave 0).  One lane per block walks the block's passes -- segments
+// of the decision streams, each 16-byte aligned (k_t1_cm3) -- with ONE
+// data-driven loop of 16-decision chunks; the segment switch and the per-pass
+// distortion record are data, not control flow.  Segment s of a block with P
+// coded planes: s = 0 is the top plane's cleanup pass; s >= 1 is pass
+// (s+2)%3 (0 SPP, 1 MRP, 2 CUP) of plane k = (s+2)/3, planes counted from the
+// top.  Blocks are ordered by decision count (the buckets k_t1_cm3 files
+// them in), so the lanes of a wave finish together.
+__device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
+    const int lane = threadIdx.x & 63;
+    const int b = sh.blk[lane];
+    uint32_t *cx = sh.cxs + lane;
+    const uint32_t *mqt = sh.mqt;
 #pragma unroll
     for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];  // entry 2 i + MPS; all start with MPS 0
     cx[CX_PAD * 64] = 0u;  // Qe 0, MPS 0: the padding decisions' no-op state
     cx[0] = mqt[2 * 4];
     cx[CX_RL * 64] = mqt[2 * 3];
     cx[CX_UNI * 64] = mqt[2 * 46];
-    Mq m;
-    m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
-    m.cap = (int)d.out_cap;
-    m.out = a.out + d.out_off;
-    int32_t *R = a.rates + (size_t)b * kMaxPasses;
-    int64_t *D = a.dists + (size_t)b * kMaxPasses;
-    const uint32_t cap = plane_stream_cap(d.w, d.h);
-    const uint8_t *sbase = a.stream + a.slot_off[b];
-    const uint4 *cntp = a.counts + (size_t)b * 32;
-    const int64_t *dspp = a.dspp + (size_t)b * 32;
-    const int64_t *dref = a.dref + (size_t)b * 32;
-    const int64_t *dsig = a.dsig + (size_t)b * 32;
-    const int nseg = 3 * P - 2;
-    int s = 0, k = 0, pass = 2;
-    uint4 cnt = cntp[0];
-    const uint4 *ptr = (const uint4 *)sbase;  // top plane: cleanup at offset 0
-    int left = (int)cnt.z;
-    int64_t ndec = left;
-    uint4 cur = ptr[0];
-    for (;;) {
-        // close finished segments (empty passes close at once)
+    uint32_t A = 0x8000u;
+    int nseg = 0, s = 0, k = 0, pass = 2, left = 0, Pt = 0;
+    uint32_t cap = 0;
+    const uint8_t *sbase = nullptr;
+    const uint4 *cntp = nullptr, *ptr = nullptr;
+    const int64_t *dspp = nullptr, *dref = nullptr, *dsig = nullptr;
+    int64_t *D = nullptr;
+    uint4 cnt = make_uint4(0u, 0u, 0u, 0u), cur = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
+    int64_t ndec = 0;
+    if (b >= 0) {
+        const BlockDesc d = a.blocks[b];
+        Pt = a.P[b];
+        const int P = Pt - a.pmin[b];  // coded planes Pt-1 .. pmin (slope prediction)
+        nseg = 3 * P - 2;
+        D = a.dists + (size_t)b * kMaxPasses;
+        cap = plane_stream_cap(d.w, d.h);
+        sbase = a.stream + a.slot_off[b];
+        cntp = a.counts + (size_t)b * 32;
+        dspp = a.dspp + (size_t)b * 32;
+        dref = a.dref + (size_t)b * 32;
+        dsig = a.dsig + (size_t)b * 32;
+        cnt = cntp[0];
+        ptr = (const uint4 *)sbase;  // top plane: cleanup at offset 0
+        left = (int)cnt.z;
+        ndec = left;
+        cur = ptr[0];
+    }
+    for (int it = 0;; it++) {
+        // close finished passes (empty passes close at once)
         while (left <= 0 && s < nseg) {
             const int p = Pt - 1 - k;
-            R[s] = m.bp + 3;
             D[s] = pass == 0 ? dspp[k] : (pass == 1 ? dref[p] : dsig[p] - dspp[k]);
             if (++s >= nseg) break;
             pass = pass == 2 ? 0 : pass + 1;
@@ -719,33 +756,84 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
             ndec += left;
             cur = ptr[0];
         }
-        if (s >= nseg) break;
-        // one chunk of 16 decisions (a pass's last chunk is padded); the
-        // next chunk's load is in flight behind it, and each context state
-        // is read one decision ahead
-        const uint4 nxt = ptr[1];
+        const bool active = s < nseg;
+        const int buf = it & 1;
+        sh.segs[buf][lane] = s;
+        if (!__any(active)) {
+            sh.finA[lane] = A;
+            if (lane == 0) sh.more[buf] = 0;
+            __syncthreads();
+            break;
+        }
+        if (lane == 0) sh.more[buf] = 1;
+        // one chunk of 16 decisions (a pass's last chunk is padded; a lane
+        // whose block is done codes padding); the next chunk's load is in
+        // flight behind it, and each context state is read one decision ahead
+        uint4 nxt = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
+        if (active) nxt = ptr[1];
+        if (!active) cur = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
         const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
-        const int n = min(16, left);
         uint32_t t = cx[__builtin_amdgcn_ubfe(w[0], 1, 5) * 64];
+        uint32_t *out = &sh.code[buf][0][lane];
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < kMqChunk; j++) {
             // decision byte = (context << 1) | d; context in bits 1..5
             const uint32_t cur_cx = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8 + 1, 5);
-            const uint32_t d = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 1);
+            const uint32_t dd = __builtin_amdgcn_ubfe(w[j >> 2], (j & 3) * 8, 1);
             uint32_t nxt_cx = 0, nt = 0;
-            if (j < 15) {
+            if (j < kMqChunk - 1) {
                 nxt_cx = __builtin_amdgcn_ubfe(w[(j + 1) >> 2], ((j + 1) & 3) * 8 + 1, 5);
                 nt = cx[nxt_cx * 64];
             }
-            const uint32_t tn = mq_step(m, t, mqt, d, ring);
+            uint32_t code;
+            const uint32_t tn = mq_model(A, t, mqt, dd, code);
+            out[j * 64] = code;
             cx[cur_cx * 64] = tn;
             t = (nxt_cx == cur_cx) ? tn : nt;
         }
-        ring_flush(m, ring, fl);
-        left -= n;
-        ptr++;
-        cur = nxt;
+        if (active) {
+            left -= min(16, left);
+            ptr++;
+            cur = nxt;
+        }
+        __syncthreads();  // chunk `it` ready; the coder is done with chunk it - 1
     }
+    if (a.dbg && b >= 0) a.dbg[(size_t)b * 4 + 0] = ndec;
+}
+
+// Coder (wave 1): C, CT, B and the output bytes of the same 64 blocks.
+__device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
+    const int lane = threadIdx.x & 63;
+    const int b = sh.blk[lane];
+    uint8_t *ring = (uint8_t *)sh.rings + lane * 68;
+    int fl = 0;  // bytes already copied from the ring
+    Mq m;
+    m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
+    m.cap = 0;
+    m.out = nullptr;
+    int32_t *R = nullptr;
+    if (b >= 0) {
+        const BlockDesc d = a.blocks[b];
+        m.cap = (int)d.out_cap;
+        m.out = a.out + d.out_off;
+        R = a.rates + (size_t)b * kMaxPasses;
+    }
+    int sdone = 0;
+    for (int it = 0;; it++) {
+        __syncthreads();  // chunk `it` written by the modeller
+        const int buf = it & 1;
+        // passes that ended before this chunk end at the current length
+        const int s_now = sh.segs[buf][lane];
+        for (; sdone < s_now; sdone++) R[sdone] = m.bp + 3;
+        if (!sh.more[buf]) break;
+        const uint32_t *in = &sh.code[buf][0][lane];
+#pragma unroll
+        for (int j = 0; j < kMqChunk; j++) mq_code(m, in[j * 64], ring);
+        ring_flush(m, ring, fl);
+    }
+    if (b < 0) return;
+    const int nseg = sdone;
+    m.A = sh.finA[lane];
     for (int i = fl; i < m.bp; i++)  // bytes still in the ring
         if (i < m.cap) m.out[i] = ring[i & 63];
     const int len = mq_flush(m);
@@ -758,184 +846,57 @@ __device__ __forceinline__ void mq_block(const T1MqArgs &a, uint32_t *cxs, const
     }
     a.npasses[b] = (uint8_t)nseg;
     a.lengths[b] = len;
-    if (a.dbg) {  // debug census: decisions, 100 MHz ticks, lane index
-        a.dbg[(size_t)b * 4 + 0] = ndec;
-        a.dbg[(size_t)b * 4 + 1] = 0;
-        a.dbg[(size_t)b * 4 + 2] = (int64_t)(wall_clock64() - w0);
-        a.dbg[(size_t)b * 4 + 3] = gi;
-    }
 }
 
-// Tier-1 lane order: blocks by decreasing decision count (all coded passes),
-// so the lanes of an MQ wave carry similar work.  The order only groups
-// blocks (it changes no output), so it is a bucket sort in one workgroup --
-// one launch instead of a device radix sort's ten: bucket = 8 * floor(log2(n
-// + 1)) + the next 3 bits of n + 1 (12.5 % wide), largest first; inside a
-// bucket the order is whatever the atomics give.  keys[b] = ~n, left by
-// k_t1_cm3 (each plane subtracts its decisions from ~0; tier-2's summary adds
-// the decisions up from them).  Also resets k_t1_mq's execution-span slots.
-constexpr int kOrderThreads = 1024, kOrderBuckets = 256;
-__device__ __forceinline__ int order_bucket(uint32_t n) {
-    const uint32_t v = n + 1u;
-    const int e = 31 - __clz(v);                                      // 0..31
-    const int f = e >= 3 ? (int)((v >> (e - 3)) & 7u) : (int)((v << (3 - e)) & 7u);
-    return kOrderBuckets - 1 - min(kOrderBuckets - 1, 8 * e + f);   // descending
-}
-__global__ void __launch_bounds__(kOrderThreads) k_t1_order(int nblocks, const uint32_t *keys, int32_t *order,
-                                                            unsigned long long *span) {
-    __shared__ uint32_t hist[kOrderBuckets];
-    const int tid = threadIdx.x;
-    if (tid == 0 && span) {
-        span[0] = ~0ull;
-        span[1] = 0ull;
+// The launch's execution span is recorded in 100 MHz wall-clock ticks
+// (span[0] = ~earliest wave start, span[1] = latest lane end; vector atomics
+// on words k_quant zeroed).
+__global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
+    __shared__ MqShared sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint64_t w0 = wall_clock64();
+    if (tid == 0) atomicMax(&a.span[0], ~(unsigned long long)w0);
+    for (int e = tid; e < 94; e += 128) {
+        const int i = e >> 1, mps = e & 1;
+        const int sw = i == 0 || i == 6 || i == 14;
+        sh.mqt[e] = (uint32_t)c_qe[i] | ((uint32_t)(2 * c_nmps[i] + mps) << 16) |
+                    ((uint32_t)(2 * c_nlps[i] + (mps ^ sw)) << 23) | ((uint32_t)mps << 31);
     }
-    for (int i = tid; i < kOrderBuckets; i += kOrderThreads) hist[i] = 0;
-    __syncthreads();
-    constexpr int U = 4;  // blocks per thread per round (loads in flight)
-    for (int b0 = 0; b0 < nblocks; b0 += U * kOrderThreads) {
-        uint32_t k[U];
+    if (tid < 64) {  // exclusive scan of the bucket fills, 4 per lane
+        uint32_t v[4], t = 0;
 #pragma unroll
-        for (int u = 0; u < U; u++) k[u] = keys[min(b0 + u * kOrderThreads + tid, nblocks - 1)];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (b0 + u * kOrderThreads + tid < nblocks) atomicAdd(&hist[order_bucket(~k[u])], 1u);
-    }
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 256 buckets, 4 per lane
-        uint32_t v[4], s = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) s += (v[i] = hist[tid * 4 + i]);
-        uint32_t o = wave_incl_scan(s) - s;
+        for (int i = 0; i < 4; i++) t += (v[i] = a.bfill[4 * lane + i]);
+        uint32_t o = wave_incl_scan(t) - t;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            hist[tid * 4 + i] = o;
+            sh.bbase[4 * lane + i] = o;
             o += v[i];
         }
+        if (lane == 63) sh.bbase[kOrderBuckets] = o;
     }
     __syncthreads();
-    for (int b0 = 0; b0 < nblocks; b0 += U * kOrderThreads) {
-        uint32_t k[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) k[u] = keys[min(b0 + u * kOrderThreads + tid, nblocks - 1)];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int b = b0 + u * kOrderThreads + tid;
-            if (b < nblocks) order[atomicAdd(&hist[order_bucket(~k[u])], 1u)] = b;
+    if (tid < 64) {
+        // lane-order position gi -> its bucket -> the block (blocks with no
+        // coded plane are in no bucket: emit_t1_items recorded them)
+        const int gi = blockIdx.x * 64 + lane;
+        int b = -1;
+        if (gi < (int)sh.bbase[kOrderBuckets]) {
+            int bk = 0;
+            for (int step = 128; step > 0; step >>= 1)
+                if (sh.bbase[bk + step] <= (uint32_t)gi) bk += step;
+            b = a.bslots[(size_t)bk * a.nblocks + (gi - (int)sh.bbase[bk])];
         }
-    }
-}
-
-// Tier-1 work list, built on the device from the coded plane counts
-// c = P - pmin by one workgroup (one launch instead of flags + two device
-// scans + items): the (block, plane) items, depth-major (k = planes from the
-// top), then in the plan's lane order `order`.  Pass 1 takes the per-depth
-// totals (ballots; c is kept in LDS), pass 2 walks the lane order in tiles of
-// 1024: per depth a ballot, the 16 waves' counts prefix-summed by one 16-lane
-// DPP row per depth, and every lane with c > k writes its item.  Also sets
-// keys[b] = ~0 for k_t1_cm3's decision counts.  (The stream slots are fixed
-// by the plan: every plane of a block has its slot, GpuEncoder::run_front.)
-constexpr int kListThreads = 1024, kListWaves = kListThreads / 64, kListMaxK = 64;
-constexpr int kListLdsBlocks = 73728;  // (top << 8 | c) per block in LDS up to this many blocks
-// the wave's largest coded plane count, at most kmax (wave-uniform)
-__device__ __forceinline__ int wave_max_planes(uint32_t c, int kmax) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c = max(c, (uint32_t)__shfl_xor((int)c, o, 64));
-    return min(__builtin_amdgcn_readfirstlane((int)c), kmax);
-}
-template <bool kLds>
-__global__ void __launch_bounds__(kListThreads) k_t1_worklist(int nb, int kmax, const int32_t *order,
-                                                              const uint8_t *P, const uint8_t *pmin, uint32_t *keys,
-                                                              int2 *items, int *nitems) {
-    __shared__ uint16_t ct[kLds ? kListLdsBlocks : 1];
-    __shared__ uint32_t wc[kListMaxK * kListWaves];  // per tile: [depth][wave] count -> item position
-    __shared__ uint32_t run[kListMaxK];              // per depth: next item position
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    for (int b = t; b < nb; b += kListThreads) keys[b] = ~0u;
-    if (t < kListMaxK) run[t] = 0;
-    __syncthreads();
-    // pass 1: lane k of every wave counts the blocks with more than k coded planes
-    constexpr int U = 4;
-    uint32_t acc = 0;
-    for (int j0 = 0; j0 < nb; j0 += U * kListThreads) {
-        int b[U];
-        uint32_t top[U], c[U];
-        // (loads at clamped indices, no load under a branch: they issue together)
-#pragma unroll
-        for (int u = 0; u < U; u++) b[u] = order[min(j0 + u * kListThreads + t, nb - 1)];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const bool in = j0 + u * kListThreads + t < nb;
-            const uint32_t pt = P[b[u]], pm = pmin[b[u]];
-            top[u] = in ? pt : 0u;
-            c[u] = in ? pt - pm : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int j = j0 + u * kListThreads + t;
-            if (kLds && j < nb) ct[j] = (uint16_t)(top[u] << 8 | c[u]);
-            const int kw = wave_max_planes(c[u], kmax);
-            for (int k = 0; k < kw; k++) {
-                const uint64_t m = __ballot(c[u] > (uint32_t)k);
-                if (lane == k) acc += (uint32_t)__popcll(m);
-            }
-        }
-    }
-    if (lane < kmax) atomicAdd(&run[lane], acc);
-    __syncthreads();
-    if (t < 64) {  // depth bases: exclusive scan of the totals
-        const uint32_t v = t < kmax ? run[t] : 0u;
-        const uint32_t inc = wave_incl_scan(v);
-        if (t < kmax) run[t] = inc - v;
-        if (t == 63) *nitems = (int)inc;
+        sh.blk[lane] = b;
     }
     __syncthreads();
-    // pass 2: items (the next tile's lane order is loaded one tile ahead)
-    int bnext = order[min(t, nb - 1)];
-    for (int j0 = 0; j0 < nb; j0 += kListThreads) {
-        const int j = j0 + t;
-        const int b = bnext;
-        bnext = order[min(j + kListThreads, nb - 1)];
-        uint32_t top = 0, c = 0;
-        if (kLds) {
-            if (j < nb) {
-                top = ct[j] >> 8;
-                c = ct[j] & 0xffu;
-            }
-        } else {
-            const uint32_t pt = P[b], pm = pmin[b];
-            if (j < nb) {
-                top = pt;
-                c = pt - pm;
-            }
-        }
-        // depths up to the wave's deepest block; the rest of its column is 0
-        const int kw = wave_max_planes(c, kmax);
-        for (int k = 0; k < kw; k++) {
-            const uint64_t m = __ballot(c > (uint32_t)k);
-            if (lane == 0) wc[k * kListWaves + w] = (uint32_t)__popcll(m);
-        }
-        if (lane >= kw && lane < kmax) wc[lane * kListWaves + w] = 0u;
-        __syncthreads();
-        if (t < kmax * kListWaves) {  // one 16-lane row per depth: prefix over the waves
-            const uint32_t v = wc[t];
-            int s = (int)v;
-            s += __builtin_amdgcn_update_dpp(0, s, 0x111, 0xf, 0xf, false);
-            s += __builtin_amdgcn_update_dpp(0, s, 0x112, 0xf, 0xf, false);
-            s += __builtin_amdgcn_update_dpp(0, s, 0x114, 0xf, 0xf, false);
-            s += __builtin_amdgcn_update_dpp(0, s, 0x118, 0xf, 0xf, false);
-            const int k = t >> 4;
-            const uint32_t r = run[k];
-            wc[t] = r + (uint32_t)s - v;
-            if ((t & 15) == 15) run[k] = r + (uint32_t)s;
-        }
-        __syncthreads();
-        for (int k = 0; k < kw; k++) {
-            const uint64_t m = __ballot(c > (uint32_t)k);
-            if (c > (uint32_t)k)
-                items[wc[k * kListWaves + w] + (uint32_t)__popcll(m & lt)] = make_int2(b, (int)(top - 1u - k));
-        }
+    if (tid < 64) mq_modeller(a, sh);
+    else mq_coder(a, sh);
+    if (a.dbg && tid >= 64 && sh.blk[lane] >= 0) {  // debug census: 100 MHz ticks, lane position
+        a.dbg[(size_t)sh.blk[lane] * 4 + 1] = 0;
+        a.dbg[(size_t)sh.blk[lane] * 4 + 2] = (int64_t)(wall_clock64() - w0);
+        a.dbg[(size_t)sh.blk[lane] * 4 + 3] = blockIdx.x * 64 + lane;
     }
+    if (tid == 64) atomicMax(&a.span[1], (unsigned long long)wall_clock64());
 }
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
@@ -943,23 +904,19 @@ void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
     hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
-void launch_t1_worklist(int nb, int kmax, const int32_t *order, const uint8_t *P, const uint8_t *pmin,
-                        uint32_t *keys, int2 *items, int *nitems, hipStream_t st) {
-    if (nb <= 0) return;                      // (no blocks: no tier-1 launch reads the list)
-    if (kmax > kListMaxK) kmax = kListMaxK;  // (Mb <= 30, plan.cpp)
-    if (nb <= kListLdsBlocks)
-        hipLaunchKernelGGL(k_t1_worklist<true>, dim3(1), dim3(kListThreads), 0, st, nb, kmax, order, P, pmin, keys,
-                           items, nitems);
-    else
-        hipLaunchKernelGGL(k_t1_worklist<false>, dim3(1), dim3(kListThreads), 0, st, nb, kmax, order, P, pmin, keys,
-                           items, nitems);
-}
-void launch_t1_order(int nblocks, const uint32_t *keys, int32_t *order, unsigned long long *span, hipStream_t st) {
-    if (nblocks <= 0) return;
-    hipLaunchKernelGGL(k_t1_order, dim3(1), dim3(kOrderThreads), 0, st, nblocks, keys, order, span);
-}
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
-    if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + a.lanes - 1) / a.lanes), dim3(64), 0, st, a);
+    if (a.nblocks) hipLaunchKernelGGL(k_t1_mq, dim3((a.nblocks + 63) / 64), dim3(128), 0, st, a);
+}
+// no slope prediction: every plane coded (pmin = 0), the work lists filled
+__global__ void __launch_bounds__(256) k_t1_items(T1ItemArgs a) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    const bool in = b < a.nb;
+    const int P = in ? a.P[b] : 0;
+    if (in) a.pmin[b] = 0;
+    emit_t1_items(a, b, in, P, 0);
+}
+void launch_t1_items(const T1ItemArgs &a, hipStream_t st) {
+    if (a.nb > 0) hipLaunchKernelGGL(k_t1_items, dim3((a.nb + 255) / 256), dim3(256), 0, st, a);
 }
 uint32_t t1_plane_stream_cap(int w, int h) { return plane_stream_cap(w, h); }
 

@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(64) k_t2_tparts(T2Args a) {
 // host needs (part size, header bytes, bytes per layer, tier-1 totals).
 __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
                                                   const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
-                                                  const uint64_t *kc, const uint32_t *ndec_key, T2Summary *sum) {
+                                                  const uint64_t *kc, const unsigned long long *acc, T2Summary *sum) {
     __shared__ uint64_t part[256];
     __shared__ int64_t lay[256][kMaxLayers > 8 ? 8 : kMaxLayers];
     if (a.halt && *a.halt) return;  // the whole workgroup
@@ -374,18 +374,19 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
         }
         __syncthreads();
     }
-    // tier-1 totals (ndec_key: ~decisions per block, the MQ lane-order keys)
+    // tier-1 totals (acc: decisions per block in the low 40 bits, k_t1_cm3)
     int64_t tb = 0, tp = 0, nd = 0;
     int skipped = 0;
     for (int b0 = 0; b0 < nblocks; b0 += 4 * 256) {  // 4 blocks' loads in flight per thread
         int32_t ln[4];
-        uint32_t np[4], kk[4], pm[4];
+        uint32_t np[4], pm[4];
+        unsigned long long kk[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int b = min(b0 + u * 256 + tid, nblocks - 1);
             ln[u] = lengths[b];
             np[u] = npasses[b];
-            kk[u] = ndec_key[b];
+            kk[u] = acc[b];
             pm[u] = pmin[b];
         }
 #pragma unroll
@@ -393,7 +394,7 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
             if (b0 + u * 256 + tid < nblocks) {
                 tb += ln[u];
                 tp += np[u];
-                nd += ~kk[u];
+                nd += (int64_t)(kk[u] & ((1ull << 40) - 1ull));
                 skipped |= pm[u] > 0;
             }
     }
@@ -582,7 +583,7 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt)
     hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
                        (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
                        with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
-                       (const uint32_t *)ordkey.ptr, (T2Summary *)t2sum.ptr);
+                       (const unsigned long long *)ordkey.ptr, (T2Summary *)t2sum.ptr);
 }
 
 bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,
@@ -622,8 +623,6 @@ bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, u
     // staging path, which serialises the contexts)
     if (part_bytes)
         HIPCHECK(hipMemcpyAsync(host_dst, (const uint8_t *)t2out.ptr + base, part_bytes, hipMemcpyDeviceToHost, stream));
-    if (profiled)  // k_t1_mq's execution span, for collect_profile()
-        HIPCHECK(hipMemcpyAsync(h_tot + 2, mqspan.ptr, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipEventRecord(ev[9], stream));
     if (!host_wait(err)) return false;
     if (profile) {

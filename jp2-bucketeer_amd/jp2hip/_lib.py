@@ -170,8 +170,42 @@ def tiff_layout(data: bytes):
     return lay, keep
 
 
+class Output:
+    """An encode's file bytes, left where the library wrote them (pinned host
+    memory from jp2hip's pool) instead of copied into a Python bytes object;
+    released by close() or when collected."""
+
+    def __init__(self, ptr, n: int):
+        self._p = ptr
+        self._n = n
+
+    def __len__(self):
+        return self._n
+
+    def view(self) -> memoryview:
+        if not self._p:
+            raise ValueError("released output")
+        return memoryview((c_uint8 * self._n).from_address(ctypes.addressof(self._p.contents)))
+
+    def tobytes(self) -> bytes:
+        return bytes(self.view())
+
+    def close(self):
+        if self._p:
+            lib().jp2hip_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Encoder:
-    """One libjp2hip context bound to one GPU (thread-safe, calls serialise)."""
+    """One libjp2hip context bound to one GPU (thread-safe, calls serialise).
+    The encode_* methods return the file as bytes, or with copy=False as an
+    Output over the library's buffer (no host copy of the result)."""
 
     def __init__(self, device: int = 0, host_threads: int = 0, profile: bool = False):
         cfg = Config(device, host_threads, 1 if profile else 0, 0)
@@ -191,7 +225,9 @@ class Encoder:
         except Exception:
             pass
 
-    def _take(self, out, n):
+    def _take(self, out, n, copy=True):
+        if not copy:
+            return Output(out, n.value)
         try:
             return ctypes.string_at(out, n.value)
         finally:
@@ -209,7 +245,8 @@ class Encoder:
             raise Jp2hipError(last_error())
         return self._take(out, n), st
 
-    def encode_tiff_ptr(self, h_ptr: int, nbytes: int, conversion: int, rcp: Recipe | None = None):
+    def encode_tiff_ptr(self, h_ptr: int, nbytes: int, conversion: int, rcp: Recipe | None = None,
+                        copy: bool = True):
         """encode_tiff on TIFF bytes already in host memory at h_ptr (pinned
         memory makes the H2D a plain DMA)."""
         out = POINTER(c_uint8)()
@@ -220,10 +257,10 @@ class Encoder:
                                       byref(out), byref(n), byref(st))
         if rc != 0:
             raise Jp2hipError(last_error())
-        return self._take(out, n), st
+        return self._take(out, n, copy), st
 
     def encode_device(self, d_ptr: int, nbytes: int, layout: Layout, conversion: int,
-                      rcp: Recipe | None = None):
+                      rcp: Recipe | None = None, copy: bool = True):
         out = POINTER(c_uint8)()
         n = c_size_t()
         st = Stats()
@@ -232,7 +269,7 @@ class Encoder:
                                         byref(out), byref(n), byref(st))
         if rc != 0:
             raise Jp2hipError(last_error())
-        return self._take(out, n), st
+        return self._take(out, n, copy), st
 
     def encode_device_split(self, d_ptr: int, nbytes: int, layout: Layout, conversion: int,
                             split: Split, rcp: Recipe | None = None):
