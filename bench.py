@@ -48,6 +48,8 @@ def make_image(kind: str, seed: int):
 
 
 def dist_setup(n_gpus):
+    """(world, rank, local device) of this process; for N > 1 ranks the
+    process group is up and its size checked against --gpus."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -59,7 +61,22 @@ def dist_setup(n_gpus):
         import torch.distributed as dist
         backend = os.environ.get("JP2HIP_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend=backend)
+        if dist.get_world_size() != n_gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {n_gpus}")
     return world, rank, local
+
+
+def local_device():
+    if os.environ.get("JP2HIP_BENCH_DEVICE"):
+        return int(os.environ["JP2HIP_BENCH_DEVICE"])
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def ranks_seen(world):
+    if world <= 1:
+        return 1
+    import torch.distributed as dist
+    return dist.get_world_size()
 
 
 def barrier_max(world, value, device):
@@ -345,7 +362,8 @@ def run(args):
                        "images_per_step": batch, "images_in_flight_per_gpu": nf, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "timed_span": "TIFF resident in HBM -> JPX bytes in host memory (jp2hip_encode_device; "
                                      "the file is left in the library's pinned buffer, not copied into Python)",
-                       "parallelism": f"replicas x{world}", "out_bytes": int(avg["out_bytes"]),
+                       "parallelism": f"replicas x{world}", "ranks_in_process_group": ranks_seen(world),
+                       "out_bytes": int(avg["out_bytes"]),
                        "bpp": round(8 * avg["out_bytes"] / npx, 4),
                        "single_image_latency_ms": round(1e3 * min(lat), 3),
                        "host_waits_per_encode": int(max(a["host_waits"] for a in alone)),
@@ -447,6 +465,8 @@ def run_c4(args):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     work = tempfile.mkdtemp(prefix=f"jp2hip_c4_{rank}_")
     try:
         ndistinct, rows = 4, args.steps
@@ -494,7 +514,8 @@ def run_c4(args):
                 "data": f"synthetic 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0..{ndistinct - 1}) on local disk",
                 "config": {"workload": "C4: Bucketeer batch CSV -> per-GPU native queue (read, lossless 5/3 encode, "
                                        "JPX write, stub upload, delete-after-upload), Kakadu recipe",
-                           "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"shards x{world}"}}
+                           "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"shards x{world}",
+                           "ranks_in_process_group": world}}
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
@@ -562,7 +583,8 @@ def run_c5(args):
                    "image": "40000x30000x1 u16", "parallelism": f"tile-split x{world}",
                    "file_bytes": int(flen), "bpp": round(8 * flen / npx, 4),
                    "rank0_rows": list(rows), "rank0_part_bytes": len(part), "parts_total_bytes": parts_total,
-                   "backend": os.environ.get("JP2HIP_BENCH_BACKEND", "nccl") if world > 1 else None},
+                   "backend": os.environ.get("JP2HIP_BENCH_BACKEND", "nccl") if world > 1 else None,
+                   "ranks_in_process_group": ranks_seen(world)},
         "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
@@ -572,6 +594,19 @@ def run_c5(args):
         "rate_iterations": int(avg["rate_iterations"]),
         "split_equals_single_encode": identical,
     }
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment):
+    start N rank processes through torch.distributed.run, before anything here
+    touches a GPU, and exit with their status (a child process, not an exec)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -589,6 +624,10 @@ def main():
                     help="c2: the headline (replicas); c4: CSV batch through the native per-GPU queue; "
                          "c5: one oversized image tile-split across ranks")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}")
     # one hardware queue per in-flight context plus a few for the runtime's
     # own streams: with HIP's default of 4 (exported as such on the GPU
     # boxes) the 12 contexts share 4 queues, and the kernels of a shared
@@ -615,6 +654,7 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_lossless:
             res["lossless_c3"] = lossless_c3(enc)
+            res["lossless_c4"] = lossless_c4(local_device())
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_reference_opj(img)
             res["cpu_not_a_reference"] = cpu_oracle_not_a_reference(img)
@@ -625,10 +665,14 @@ def main():
         dist.destroy_process_group()
 
 
-def lossless_c3(enc, steps=2, inflight=4):
-    """C3 (configs[2]): 10000x8000 RGB16 lossless 5/3, 1024^2 tiles -- reported
-    beside: one image alone (latency, including the Python copy of the 340 MB
-    result) and `inflight` images at once on separate contexts (throughput)."""
+def lossless_c3(enc, steps=2, inflight=4, n_each=3):
+    """C3 (configs[2]): 10000x8000 RGB16 lossless 5/3, 1024^2 tiles, the
+    conversion the reference's service runs (ImageWorkerVerticle.java:64).
+    One image alone (latency at the C call) and `inflight` images at once on
+    separate contexts (throughput): TIFF resident in HBM -> JPX bytes in host
+    memory, timed around the C calls, the file left in the library's pinned
+    buffer (no Python copy); each context's code-stream D2H overlaps the
+    other contexts' kernels."""
     import threading
 
     import torch
@@ -639,36 +683,37 @@ def lossless_c3(enc, steps=2, inflight=4):
     tif = im.tiff_bytes(img, rows_per_strip=64)
     lay, offs = jp2hip.tiff_layout(tif)
     d_src = torch.frombuffer(bytearray(tif), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
     rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
-    out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)
-    t0 = time.perf_counter()
+    out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc, copy=False)
+    out.close()
+    lat = []
     for _ in range(steps):
-        out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)
-    dt = (time.perf_counter() - t0) / steps
+        t0 = time.perf_counter()
+        out, st = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc, copy=False)
+        lat.append(time.perf_counter() - t0)
+        nbytes = len(out)
+        out.close()
     npx = img.shape[0] * img.shape[1]
-    res = {"workload": "C3: 10000x8000 RGB16 lossless 5/3, 1024^2 tiles", "mp_per_s": round(npx / 1e6 / dt, 3),
-           "ms": round(dt * 1e3, 2),
-           # the C call alone (jp2hip_encode_device wall time), without the
-           # Python copy of the ~340 MB result that "ms" includes
-           "ms_c_api": round(st.total_ms, 2), "mp_per_s_c_api": round(npx / 1e3 / st.total_ms, 3),
-           "bpp": round(8 * len(out) / npx, 4), "t1_ms": round(st.t1_ms, 3),
-           "dwt_ms": round(st.dwt_ms, 3),
+    bpp = 8 * nbytes / npx
+    res = {"workload": "C3: 10000x8000 RGB16 lossless 5/3, 1024^2 tiles", "bpp": round(bpp, 4),
+           "ms_c_api": round(1e3 * min(lat), 2), "mp_per_s_c_api": round(npx / 1e6 / min(lat), 3),
            "stages_ms": {k: round(v, 3) for k, v in st.as_dict().items() if k.endswith("_ms")}}
-    del out
     encs = [enc] + [jp2hip.Encoder(torch.cuda.current_device(), host_threads=4, profile=True)
                     for _ in range(inflight - 1)]
     for e in encs[1:]:
-        e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)  # warm-up
-    n_each = 2
+        e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc, copy=False)[0].close()
     errors = []
 
     def work(e):
         try:
             for _ in range(n_each):
-                e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)
+                o, _ = e.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc, copy=False)
+                o.close()
         except Exception as ex:
             errors.append(ex)
 
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     th = [threading.Thread(target=work, args=(e,)) for e in encs]
     for t in th:
@@ -678,11 +723,78 @@ def lossless_c3(enc, steps=2, inflight=4):
     dt = time.perf_counter() - t0
     if errors:
         raise errors[0]
-    res["inflight"] = inflight
-    res["mp_per_s_inflight"] = round(npx / 1e6 * n_each * inflight / dt, 3)
+    value = npx / 1e6 * n_each * inflight / dt
+    # SURVEY.md 8(d) full path at the measured bpp: B_dwt + 4C + 3 bpp / 8
+    b_path = dwt_bytes_per_px(3, 2, 6) + 4 * 3 + 3 * bpp / 8
+    res.update({"inflight": inflight, "images": n_each * inflight, "mp_per_s_inflight_c_api": round(value, 3),
+                "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
+                                  "achieved": round(b_path * value * 1e6 / 1e9, 2), "peak": HBM_PEAK / 1e9,
+                                  "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}})
     for e in encs[1:]:
         e.close()
     return res
+
+
+def c4_batch(device, rows=16, ndistinct=2, contexts=8):
+    """C4 (configs[3]) on one GPU, reduced: a Bucketeer batch CSV of `rows`
+    synthetic 5000x7000 RGB8 TIFFs (cycling over `ndistinct` files, as
+    SURVEY.md 8(d) prescribes for the 10k-row batch) through the native batch
+    queue: TIFF read from disk -> lossless encode -> JPX write -> stub upload
+    (reads every byte) -> delete.  Timed from the first submit to the last
+    upload, file I/O included.  Returns (MP/s, seconds, results)."""
+    import csv as _csv
+    import shutil
+    from concurrent.futures import ThreadPoolExecutor
+
+    import imaging as im
+    from jp2hip import batch as jb
+    work = tempfile.mkdtemp(prefix="jp2hip_c4_")
+    try:
+        def gen(i):
+            pth = os.path.join(work, f"synth{i:02d}.tif")
+            with open(pth, "wb") as f:
+                f.write(im.tiff_bytes(im.synth_rgb8(7000, 5000, seed=i), rows_per_strip=64))
+            return pth
+
+        with ThreadPoolExecutor(ndistinct) as ex:
+            paths = list(ex.map(gen, range(ndistinct)))
+        csv_path = os.path.join(work, "batch.csv")
+        with open(csv_path, "w", newline="", encoding="utf-8") as f:
+            wr = _csv.writer(f)
+            wr.writerow(["Item ARK", "File Name"])
+            for i in range(rows):
+                wr.writerow([f"ark:/99999/synth{i:05d}", os.path.basename(paths[i % ndistinct])])
+        items = jb.read_batch_csv(csv_path, path_prefix=work)
+        out_dir = os.path.join(work, "out")
+        os.makedirs(out_dir, exist_ok=True)
+        with jb.BatchQueue(device=device, contexts=contexts) as q:
+            for k, it in enumerate(items[:contexts]):  # warm-up: device buffers of every context
+                q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k))
+            q.drain()
+            t0 = time.perf_counter()
+            for it in items:
+                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)))
+            res = q.drain()
+            dt = time.perf_counter() - t0
+        ok = sum(1 for r in res if r["status"] == 0)
+        return 5000 * 7000 / 1e6 * ok / dt, dt, res
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def lossless_c4(device):
+    rows = 16
+    value, dt, res = c4_batch(device, rows=rows)
+    ok = [r for r in res if r["status"] == 0]
+    bpp = 8 * float(np.mean([r["out_bytes"] for r in ok])) / (5000 * 7000) if ok else 0.0
+    b_path = dwt_bytes_per_px(3, 1, 6) + 4 * 3 + 3 * bpp / 8
+    return {"workload": "C4: Bucketeer batch CSV of 5000x7000 RGB8 TIFFs (2 distinct, seeds 0-1) -> native "
+                        "per-GPU queue (disk read, lossless 5/3 encode, JPX write, stub upload, delete)",
+            "rows": rows, "images_ok": len(ok), "mp_per_s": round(value, 3), "seconds": round(dt, 3),
+            "bpp": round(bpp, 4), "timed_span": "first submit -> last upload, file I/O included",
+            "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
+                              "achieved": round(b_path * value * 1e6 / 1e9, 2), "peak": HBM_PEAK / 1e9,
+                              "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}}
 
 
 if __name__ == "__main__":

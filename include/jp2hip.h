@@ -105,6 +105,9 @@ typedef struct jp2hip_layout {
                                              /* tiles, row-major per plane  */
 } jp2hip_layout;
 
+/* Stage times (ingest_ms .. t2_ms, t1_cm_ms, t1_mq_ms) come from HIP events
+ * and are filled only for a context created with jp2hip_config.profile = 1
+ * (0 otherwise); total_ms, h2d_ms and the counts are always filled. */
 typedef struct jp2hip_stats {
     double total_ms;      /* host wall time of the call                       */
     double h2d_ms;        /* source upload (encode_file / encode_tiff only)   */
@@ -134,9 +137,14 @@ const char *jp2hip_last_error(void);
 /* 1 if a gfx950 device is usable (ConverterFactory.checkSystemKakadu analogue). */
 int jp2hip_probe(void);
 
-/* Number of visible HIP devices that are gfx950 (0 if none): how many GPUs a
- * converter spreads its contexts over (device ordinals 0..n-1). */
+/* Number of visible HIP devices that are gfx950 (0 if none). */
 int jp2hip_device_count(void);
+
+/* The HIP ordinals of the visible gfx950 devices (what jp2hip_config.device
+ * takes), at most `max` of them written to `ordinals`; returns how many there
+ * are.  A converter spreads its contexts over these, not over 0..n-1 (a
+ * non-gfx950 device may hold a low ordinal). */
+int jp2hip_device_ordinals(int32_t *ordinals, int32_t max);
 
 /* Fill the Bucketeer recipe for JP2HIP_LOSSY / JP2HIP_LOSSLESS. */
 void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion);

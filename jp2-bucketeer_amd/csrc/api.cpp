@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -416,8 +417,23 @@ void fill_stats(jp2hip_stats *stats, const jp2hip::StageTimes &st, double t_star
     stats->mq_decisions = sum.decisions;
 }
 
+// The caller's recipe (or the default for `conversion`) with its padding
+// bytes zeroed, so PlanCache's byte compare sees only the fields.
+jp2hip_recipe recipe_of(const jp2hip_recipe *recipe, int conversion) {
+    jp2hip_recipe rc;
+    std::memset(&rc, 0, sizeof rc);
+    if (recipe) rc = *recipe;
+    else default_recipe(&rc, conversion);
+    const size_t gap0 = offsetof(jp2hip_recipe, mct) + sizeof rc.mct, gap1 = offsetof(jp2hip_recipe, qstep);
+    if (gap1 > gap0) std::memset((char *)&rc + gap0, 0, gap1 - gap0);
+    static_assert(offsetof(jp2hip_recipe, flush_period) + sizeof(int32_t) == sizeof(jp2hip_recipe),
+                  "jp2hip_recipe: no tail padding");
+    return rc;
+}
+
 // The whole encode with the source already in device memory.  On success
-// *out is a malloc'd buffer holding the complete file.  Everything up to the
+// *out is the complete file in a pinned buffer from this library's pool
+// (out_alloc; released with jp2hip_free).  Everything up to the
 // code-stream bytes runs on the GPU (tier-2 included, t2_device.hip); the host picks
 // the rate-control budgets from one small summary per pass and writes the
 // file and main headers.
@@ -427,9 +443,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     using namespace jp2hip;
     if (conversion != JP2HIP_LOSSY && conversion != JP2HIP_LOSSLESS)
         return fail("conversion must be JP2HIP_LOSSY (0) or JP2HIP_LOSSLESS (1)");
-    jp2hip_recipe rc;
-    if (recipe) rc = *recipe;
-    else default_recipe(&rc, conversion);
+    const jp2hip_recipe rc = recipe_of(recipe, conversion);
     if (!lay || !d_src) return fail("null source or layout");
     ctx->gpu.take_waits();  // count this encode's host waits (stats)
     std::string err;
@@ -471,8 +485,9 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         iters = 1;
         cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
     } else {
-        // the rate loop runs on the device (GpuEncoder::rate_loop): three
-        // iterations are enqueued per host wait, the usual encode needs two
+        // the rate loop runs on the device (GpuEncoder::rate_loop): two
+        // iterations are enqueued per host wait, what the usual encode needs
+        // (a third would be launched only to return at once)
         RateState init;
         std::memset(&init, 0, sizeof init);
         init.target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
@@ -482,7 +497,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         RateState rs;
         bool restart = true;
         for (;;) {
-            if (!ctx->gpu.rate_loop(plan, init, restart, 3, prof, st, rs, sum, err)) return fail(err);
+            if (!ctx->gpu.rate_loop(plan, init, restart, 2, prof, st, rs, sum, err)) return fail(err);
             restart = false;
             if (sum.err) return fail("tier-1 output capacity exceeded");
             if (rs.safety) {
@@ -542,9 +557,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     auto allreduce = [&](int64_t *v, int n) {
         return world <= 1 || sp->allreduce_sum(sp->user, v, (int32_t)n) == 0;
     };
-    jp2hip_recipe rc;
-    if (recipe) rc = *recipe;
-    else default_recipe(&rc, conversion);
+    const jp2hip_recipe rc = recipe_of(recipe, conversion);
     if (!lay || !d_src) return fail("null source or layout");
     ctx->gpu.take_waits();
     Plan full;
@@ -677,17 +690,31 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     const size_t fh = with_main ? file_header_bytes(full) : 0;
     const uint64_t head = with_main ? fh + mh.size() : 0;
     const uint64_t part = head + (uint64_t)(have ? sum.part_bytes : 0) + (with_eoc ? 2 : 0);
+    // everything this rank's emission allocates is allocated before the
+    // ranks agree on the part sizes, so a rank that cannot fails with the
+    // others (the failure slot sizes[world]); a HIP error in the emission
+    // itself, after the exchange, fails this rank alone: the caller treats
+    // any rank's failure as the encode's (jp2hip.h)
+    uint8_t *buf = out_alloc(part ? part : 1);
+    bool ready = buf != nullptr;
+    if (!ready) err = "out of (pinned) host memory";
+    if (ready && have) ready = ctx->gpu.t2_reserve(sum.part_bytes, err);
     std::vector<int64_t> sizes((size_t)world + 1, 0);
     sizes[rank] = (int64_t)part;
-    if (!allreduce(sizes.data(), world + 1)) return fail("split: all-reduce failed");
-    if (sizes[world]) return fail("split: another rank failed");
+    sizes[world] = ready ? 0 : 1;
+    if (!allreduce(sizes.data(), world + 1)) {
+        out_free(buf);
+        return fail("split: all-reduce failed");
+    }
+    if (sizes[world]) {
+        out_free(buf);
+        return fail(ready ? std::string("split: another rank failed") : err);
+    }
     uint64_t off = 0, flen = 0;
     for (int r = 0; r < world; r++) {
         if (r < rank) off += (uint64_t)sizes[r];
         flen += (uint64_t)sizes[r];
     }
-    uint8_t *buf = out_alloc(part ? part : 1);
-    if (!buf) return fail("out of (pinned) host memory");
     if (with_main) {
         std::vector<uint64_t> Kcom = K;
         if (rc.rate_bpp <= 0.0) Kcom[L - 1] = 0;
@@ -734,15 +761,20 @@ int jp2hip_probe(void) {
     return 0;
 }
 
-int jp2hip_device_count(void) {
+int jp2hip_device_ordinals(int32_t *ordinals, int32_t max) {
     int n = 0, k = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
     for (int i = 0; i < n; i++) {
         hipDeviceProp_t p;
-        if (hipGetDeviceProperties(&p, i) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) k++;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) {
+            if (ordinals && k < max) ordinals[k] = i;
+            k++;
+        }
     }
     return k;
 }
+
+int jp2hip_device_count(void) { return jp2hip_device_ordinals(nullptr, 0); }
 
 void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
     if (recipe) default_recipe(recipe, conversion);

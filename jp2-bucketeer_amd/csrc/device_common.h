@@ -116,6 +116,46 @@ __device__ __forceinline__ uint64_t wg_excl_scan64(uint64_t n, uint64_t *wsum, u
     return ex;
 }
 
+// --------------------------------------------------------------------------
+// Device rate loop (RateState, jp2hip_internal.h): the same arithmetic as the
+// oracle's loop (oracle_encode, rate_bpp > 0).  One step, after a tier-2
+// sizing pass summarised in `sum`: stop when the code-stream fits the target
+// (or after 8 iterations), else lower the budget.  Each step that runs also
+// leaves the state and the summary it decided on in host-mapped memory
+// (out_rs, out_sum): the host reads them after its wait, no copy launches.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void rate_budgets(const RateState &r, int L, int64_t *budget) {
+    const int64_t b = r.budget < 0 ? 0 : r.budget;
+    for (int l = 0; l < L; l++) budget[l] = b >> (L - 1 - l);
+}
+__device__ __forceinline__ void rate_step(RateState *rs, const T2Summary *sum, int L, int64_t *budget,
+                                          RateState *out_rs, T2Summary *out_sum) {
+    RateState r = *rs;
+    if (r.halt) return;
+    if (sum->err) {  // tier-1 overflow: the host reports it
+        r.halt = 1;
+    } else if (r.it == 0 && r.skip_target > 0 && sum->skipped && sum->t1_bytes < r.skip_target) {
+        r.safety = 1;  // slope prediction's safety net: the host re-runs the front
+        r.halt = 1;
+    } else {
+        r.iters++;
+        r.cs_bytes = r.fixed + sum->part_bytes;
+        if (r.cs_bytes <= r.target || r.it == 7) {
+            r.halt = 1;
+        } else {
+            // exponential back-off + 1/16 of the overshoot + 64 B, as the oracle
+            const int64_t over = r.cs_bytes - r.target;
+            r.budget -= (over << r.it) + (over >> 4) + 64;
+            if (r.budget < 0) r.budget = 0;
+            r.it++;
+            rate_budgets(r, L, budget);
+        }
+    }
+    *rs = r;
+    *out_rs = r;
+    *out_sum = *sum;
+}
+
 // Files each block's coded planes in k_t1_cm3's per-depth work lists
 // (T1ItemArgs, gpu_encoder.h); called by every lane of a thread-per-block
 // kernel (`valid` false past the last block), one atomic per wave and depth.

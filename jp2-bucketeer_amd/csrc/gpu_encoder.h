@@ -97,7 +97,8 @@ struct T1MqArgs {
     int32_t *lengths;
     int *err;
     unsigned long long *span;  // [2] execution span in 100 MHz ticks (~min start, max end)
-    int64_t *dbg;  // optional per-block census [block][4] (debug)
+    int64_t *dbg;  // optional per-block census [block][6] (debug builds: decisions, modeller cycles
+                   // and barrier cycles, coder cycles and barrier cycles, lane position)
 };
 // fused ingest + DWT (dwt.hip)
 struct DwtLaunch {
@@ -161,6 +162,9 @@ class GpuEncoder {
     // (else continue the one on the device).
     bool rate_loop(const Plan &plan, const RateState &init, bool restart, int batch, bool profile, StageTimes &st,
                    RateState &rs, T2Summary &sum, std::string &err);
+    // the device code-stream buffer t2_emit writes, sized for part_bytes
+    // (t2_emit reserves it too; the split path reserves before its exchange)
+    bool t2_reserve(uint64_t part_bytes, std::string &err);
     // host_dst must be pinned (hipHostMalloc) memory
     bool t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
                  StageTimes &st, std::string &err);
@@ -185,7 +189,10 @@ class GpuEncoder {
     bool apply_thresholds(const Plan &plan, const int *halt, std::string &err);
     void select_launch(const Plan &plan, const int *halt);
     T2Args t2_args(const Plan &plan) const;
-    void t2_size_launch(const Plan &plan, bool with_kc, const int *halt);
+    // tier-2 sizing; with rs (device rate loop) k_t2_total also runs the
+    // loop's step, leaving state + summary at out_rs (host-mapped)
+    void t2_size_launch(const Plan &plan, bool with_kc, const int *halt, RateState *rs = nullptr,
+                        RateState *out_rs = nullptr);
     bool host_wait(std::string &err);
     // host -> device copy through this context's pinned staging memory: a
     // pageable source goes through the runtime's shared staging buffer and
@@ -207,7 +214,7 @@ class GpuEncoder {
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
         est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, llbuf0, llbuf1, ordkey, segval, thr, items,
-        slotoff, stream_buf, counts, dspp, dbgbuf, t1fill;
+        slotoff, stream_buf, counts, dspp, dbgbuf, t1fill, dbgsel;
     // PCRD selection (k_hull / k_select): slope-bin histogram, ticket + list
     // fills, candidate lists
     DevBuf pcrd_hb, pcrd_hc, sel_ctl, sel_key, sel_size;
@@ -217,6 +224,7 @@ class GpuEncoder {
     RateState *d_rs_out = nullptr;  // its device address
     DevBuf t2prec, t2tp, t2tt, t2lblock, t2incl, t2pklen, t2pkoff, t2tplen, t2tphdr, t2tpoff, t2blkdst, t2out, t2sum;
     int t2_nprec = 0, t2_ntp = 0;
+    bool t2_wave = true;  // precincts of <= 64 blocks: k_t2_wave (layer assignment fused in)
     uint64_t front_gen = 0, t2_gen = 0;  // plan generation whose tables are resident
     T2Summary *h_sum = nullptr;
     int64_t *h_tot = nullptr;  // pinned [8]: t1 total, -, k_t1_mq span[2], unpack error, segment tail[2]

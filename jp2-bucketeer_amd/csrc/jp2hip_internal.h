@@ -139,6 +139,7 @@ struct T2Tables {
     std::vector<PrecDesc> prec;
     std::vector<TpDesc> tp;   // code-stream order
     int64_t tt_nodes = 0;
+    int max_prec_blocks = 0;  // code-blocks of the largest precinct
 };
 // Tables for tiles [tile0, tile1) of `P` (blocks rebased by -block0: a
 // tile-split rank's blocks are its sub-plan's).

@@ -770,8 +770,8 @@ __global__ void __launch_bounds__(256) k_plane_hist(PredictArgs a) {
 // kstar = #{k in [1, kSlopeBins) : sum_{j >= k} hist[j] >= goal} (the
 // oracle's downward scan), kcut = kstar - kSkipMargin.  One wave; lane l owns
 // bins [16 l, 16 l + 16).
-__global__ void __launch_bounds__(64) k_plane_cut(const unsigned long long *hist, int64_t goal, int *kcut) {
-    const int lane = threadIdx.x;
+__device__ __forceinline__ int plane_cut(const unsigned long long *hist, int64_t goal) {
+    const int lane = threadIdx.x & 63;
     constexpr int kPer = kSlopeBins / 64;
     unsigned long long h[kPer], part = 0;
 #pragma unroll
@@ -793,17 +793,24 @@ __global__ void __launch_bounds__(64) k_plane_cut(const unsigned long long *hist
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    if (lane == 0) *kcut = cnt - kSkipMargin;
+    return cnt - kSkipMargin;
 }
 
 // the lowest coded plane of each block, then its items in tier-1's work lists
-__global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a, T1ItemArgs ia) {
+// (every workgroup finds the cut from the histogram itself: no launch for it)
+__global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a, T1ItemArgs ia, int64_t goal) {
+    __shared__ int kcut;
+    if (threadIdx.x < 64) {
+        const int kc = plane_cut(a.hist, goal);
+        if (threadIdx.x == 0) kcut = kc;
+    }
+    __syncthreads();
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = b < a.nblocks;
     const int P = in ? a.P[b] : 0;
     int pmin = P > 0 ? P - 1 : 0;
     if (in) {
-        const int kc = *a.kcut;
+        const int kc = kcut;
         const double wgt = a.weight[b];
         for (int p = 0; p < P; p++) {
             const size_t i = (size_t)b * 32 + p;
@@ -947,10 +954,9 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
 //  2. every workgroup, thread per code-block: the hull segments whose key falls
 //     in one of those bins are appended to that bin's candidate list;
 //  3. the last workgroup to arrive (agent-scope release / acquire ticket,
-//     cdna_hip_programming.md Guideline 16) resolves each layer by a radix
-//     select over its bin's candidates, 8 bits a round from the top: the largest
-//     key v with (bytes above the bin) + (candidate bytes with key >= v) >
-//     budget is the first key not taken, K' = v + 1.
+//     cdna_hip_programming.md Guideline 16) resolves each layer inside its
+//     bin: the largest key v with (bytes above the bin) + (candidate bytes
+//     with key >= v) > budget is the first key not taken, K' = v + 1.
 // The ticket and list fill counters are zeroed by k_quant and left zero by
 // the last workgroup for the next launch (the device rate loop runs several).
 struct SelectArgs {
@@ -966,9 +972,10 @@ struct SelectArgs {
     uint32_t *lsize;
     uint32_t *ctl;    // [0] arrival ticket, [1 + i] fill of list i
     uint64_t *K, *Kc;
+    int64_t *dbg;     // debug builds: [0] lists, [1 + i] list sizes, [33 + l] rounds, [65 + l] survivors
 };
 
-constexpr int kSelThreads = 1024, kSelGroup = 8;
+constexpr int kSelThreads = 1024, kSelBrute = 64;
 __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
     __shared__ unsigned long long sfx[kPcrdBins];  // S(bin): bytes of the bins >= bin
     __shared__ int8_t binmap[kPcrdBins];           // bin -> candidate list (-1: none)
@@ -978,9 +985,14 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
     __shared__ int list_bin[kMaxLayers];
     __shared__ uint32_t list_off[kMaxLayers + 1];
     __shared__ int nlist, last;
-    __shared__ unsigned long long rh[kSelGroup][256];
-    __shared__ unsigned long long rpre[kMaxLayers], racc[kMaxLayers];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, L = a.layers;
+    // last workgroup: the narrowing state and the survivors
+    __shared__ uint64_t rlo, rhi, rmax;
+    __shared__ int64_t rneed;
+    __shared__ uint32_t rcount;
+    __shared__ uint64_t bkey[kSelBrute];
+    __shared__ uint32_t bsize[kSelBrute];
+    __shared__ uint32_t hcnt[kPcrdBins];
+    const int tid = threadIdx.x, lane = tid & 63, L = a.layers;
     if (a.halt && *a.halt) return;
     // 1. suffix sums, 4 bins per thread
     {
@@ -1046,11 +1058,22 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
             for (int i = 1; i < nh; i++) {
                 const uint64_t key = hk[i];
                 const int li = binmap[pcrd_bin(key)];
-                if (li >= 0) {
-                    const int32_t r1 = R[hp[i] - 1];
-                    const uint32_t at = list_off[li] + atomicAdd(&a.ctl[1 + li], 1u);
-                    a.lkey[at] = key;
-                    a.lsize[at] = (uint32_t)(r1 - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
+                // one fill atomic per wave and list (a list's lanes take
+                // consecutive slots): same-word atomics serialise in L2
+                uint64_t todo = __ballot(li >= 0);
+                while (todo) {
+                    const int lead = __builtin_ctzll(todo);
+                    const int lj = __shfl(li, lead, 64);
+                    const uint64_t grp = __ballot(li == lj);
+                    uint32_t base = 0;
+                    if (lane == lead) base = atomicAdd(&a.ctl[1 + lj], (uint32_t)__popcll(grp));
+                    base = (uint32_t)__shfl((int)base, lead, 64);
+                    if (li == lj) {
+                        const uint32_t at = list_off[lj] + base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+                        a.lkey[at] = key;
+                        a.lsize[at] = (uint32_t)(R[hp[i] - 1] - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
+                    }
+                    todo &= ~grp;
                 }
             }
         }
@@ -1069,64 +1092,137 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
     }
     __syncthreads();
     if (!last) return;
-    for (int g0 = 0; g0 < L; g0 += kSelGroup) {
-        const int ng = min(kSelGroup, L - g0);
-        if (tid < ng) {
-            rpre[g0 + tid] = 0;
-            racc[g0 + tid] = 0;
+    if (a.dbg && tid == 0) {
+        a.dbg[0] = nlist;
+        for (int i = 0; i < nlist; i++) a.dbg[1 + i] = list_off[i + 1] - list_off[i];
+    }
+    // Each layer: the largest candidate key v with (bytes above the bin) +
+    // (candidate bytes with key >= v) > budget.  The key range is narrowed by
+    // 4096-way histograms (bytes and counts) over the candidates in range --
+    // a bin is 2^47 keys wide, one round leaves a handful (a round starts
+    // from the bin's own bounds and count: no pass for them) -- until at most
+    // kSelBrute remain, whose totals are then summed directly.
+    uint64_t *hist = (uint64_t *)sfx;  // (the suffix sums are done with)
+    for (int l = 0; l < L; l++) {
+        if (lbin[l] < 0) {
+            if (tid == 0) a.K[l] = a.Kc[l] = 0ull;  // every segment fits
+            continue;
         }
-        for (int shift = 56; shift >= 0; shift -= 8) {
-            for (int i = tid; i < kSelGroup * 256; i += kSelThreads) (&rh[0][0])[i] = 0;
-            __syncthreads();
-            for (int j = 0; j < ng; j++) {
-                const int l = g0 + j;
-                if (lbin[l] < 0) continue;
-                const int li = lli[l];
-                const uint64_t pre = rpre[l];
-                for (uint32_t i = list_off[li] + tid; i < list_off[li + 1]; i += kSelThreads) {
-                    const uint64_t key = a.lkey[i];
-                    if (shift == 56 || (key >> (shift + 8)) == (pre >> (shift + 8)))
-                        atomicAdd(&rh[j][(key >> shift) & 255u], (unsigned long long)a.lsize[i]);
-                }
+        const int li = lli[l];
+        const uint32_t i0 = list_off[li], i1 = list_off[li + 1];
+        const int bn = lbin[l];
+        if (tid == 0) {
+            rcount = i1 - i0;
+            rneed = lneed[l];
+            if (bn > 0 && bn < kPcrdBins - 1) {
+                rlo = (uint64_t)(bn + kPcrdBinBase) << 47;
+                rhi = rlo + ((1ull << 47) - 1ull);
+            } else {  // a clamped end bin: the candidates' own key range
+                rlo = ~0ull;
+                rhi = 0ull;
             }
-            __syncthreads();
-            if (wv < ng && lbin[g0 + wv] >= 0) {  // one wave per layer picks the digit
-                const int l = g0 + wv;
-                uint64_t v[4], s = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) s += (v[k] = rh[wv][4 * lane + k]);
-                const uint64_t inc = wave_incl_scan64(s);
-                const unsigned long long tot = (unsigned long long)__shfl((long long)inc, 63, 64);
-                const int64_t need = lneed[l] - (int64_t)racc[l];
-                // S_d = bytes of digits >= d; the largest d with S_d > need
-                unsigned long long Sd = tot - inc;  // digits above this lane's four
-                int dk = -1;
-                unsigned long long Sabove = 0;
-#pragma unroll
-                for (int k = 3; k >= 0; k--) {
-                    const unsigned long long up = Sd;
-                    Sd += v[k];
-                    if (dk < 0 && (int64_t)Sd > need) {
-                        dk = k;
-                        Sabove = up;
-                    }
-                }
-                const uint64_t m = __ballot(dk >= 0);
-                const int src = 63 - __builtin_clzll(m);  // (m != 0: the bin's bytes exceed need)
-                if (lane == src) {
-                    rpre[l] |= (uint64_t)(4 * lane + dk) << shift;
-                    racc[l] += Sabove;
-                }
-            }
-            __syncthreads();
-        }
-        if (tid < ng) {
-            const int l = g0 + tid;
-            const uint64_t k = lbin[l] < 0 ? 0ull : rpre[l] + 1;
-            a.K[l] = k;
-            a.Kc[l] = k;
         }
         __syncthreads();
+        if (rlo > rhi) {
+            uint64_t mn = ~0ull, mx = 0ull;
+            for (uint32_t i = i0 + tid; i < i1; i += kSelThreads) {
+                const uint64_t k = a.lkey[i];
+                mn = min(mn, k);
+                mx = max(mx, k);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mn = min(mn, (uint64_t)__shfl_xor((long long)mn, o, 64));
+                mx = max(mx, (uint64_t)__shfl_xor((long long)mx, o, 64));
+            }
+            if (lane == 0) {
+                atomicMin((unsigned long long *)&rlo, (unsigned long long)mn);
+                atomicMax((unsigned long long *)&rhi, (unsigned long long)mx);
+            }
+            __syncthreads();
+        }
+        for (int round = 0;; round++) {
+            const uint64_t flo = rlo, fhi = rhi;
+            const uint32_t cnt = rcount;
+            const int64_t need = rneed;
+            if (flo == fhi || cnt <= (uint32_t)kSelBrute) {
+                // survivors: v = the largest key whose total exceeds need
+                __syncthreads();
+                if (tid == 0) {
+                    rcount = 0;
+                    rmax = flo;  // (one key value left: it is v)
+                }
+                __syncthreads();
+                if (flo != fhi) {
+                    if (tid == 0) rmax = 0ull;
+                    for (uint32_t i = i0 + tid; i < i1; i += kSelThreads) {
+                        const uint64_t k = a.lkey[i];
+                        if (k >= flo && k <= fhi) {
+                            const uint32_t at = atomicAdd(&rcount, 1u);
+                            bkey[at] = k;  // (cnt <= kSelBrute candidates lie in range)
+                            bsize[at] = a.lsize[i];
+                        }
+                    }
+                    __syncthreads();
+                    const uint32_t c = rcount;
+                    if (tid < (int)c) {
+                        const uint64_t k = bkey[tid];
+                        int64_t g = 0;
+                        for (uint32_t j = 0; j < c; j++) g += bkey[j] >= k ? (int64_t)bsize[j] : 0;
+                        if (g > need) atomicMax((unsigned long long *)&rmax, (unsigned long long)k);
+                    }
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    a.K[l] = a.Kc[l] = rmax + 1;
+                    if (a.dbg) {
+                        a.dbg[33 + l] = round;
+                        a.dbg[65 + l] = cnt;
+                    }
+                }
+                __syncthreads();
+                break;
+            }
+            // bytes and counts per 1/4096 of the key range; the sub-range the
+            // budget falls in
+            const int shift = max(0, 64 - __builtin_clzll(fhi - flo) - 12);
+            for (int i = tid; i < kPcrdBins; i += kSelThreads) {
+                hist[i] = 0ull;
+                hcnt[i] = 0u;
+            }
+            __syncthreads();
+            for (uint32_t i = i0 + tid; i < i1; i += kSelThreads) {
+                const uint64_t k = a.lkey[i];
+                if (k >= flo && k <= fhi) {
+                    const uint32_t sb = (uint32_t)((k - flo) >> shift);
+                    atomicAdd((unsigned long long *)&hist[sb], (unsigned long long)a.lsize[i]);
+                    atomicAdd(&hcnt[sb], 1u);
+                }
+            }
+            __syncthreads();
+            {
+                uint64_t v[4], sm = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) sm += (v[i] = hist[4 * tid + i]);
+                uint64_t tot;
+                const uint64_t pre = wg_excl_scan64<kSelThreads>(sm, wsum, tot);
+                uint64_t S = tot - pre;  // bytes of the sub-ranges >= 4 tid
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    // the largest sub-range s with S(s) > need: S(s) > need >= S(s + 1)
+                    const uint64_t Sn = S - v[i];
+                    if ((int64_t)S > need && (int64_t)Sn <= need) {
+                        const uint64_t lo = flo + ((uint64_t)(4 * tid + i) << shift);
+                        rlo = lo;
+                        rhi = lo + ((1ull << shift) - 1ull) > fhi ? fhi : lo + ((1ull << shift) - 1ull);
+                        rneed = need - (int64_t)Sn;
+                        rcount = hcnt[4 * tid + i];
+                    }
+                    S = Sn;
+                }
+            }
+            __syncthreads();
+        }
     }
     if (tid <= nlist) a.ctl[tid] = 0u;  // ticket and fill counters, for the next launch
 }
@@ -1270,7 +1366,7 @@ GpuEncoder::~GpuEncoder() {
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
-                     &t1fill};
+                     &t1fill, &dbgsel};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -1672,9 +1768,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
             }
             if (!h2d(hist.ptr, h_hist.data(), sizeof(int64_t) * kSlopeBins, err)) return false;
         }
-        hipLaunchKernelGGL(k_plane_cut, dim3(1), dim3(64), 0, stream, (const unsigned long long *)hist.ptr,
-                           skip_target * 128, (int *)kcut.ptr);
-        hipLaunchKernelGGL(k_plane_pmin, dim3((nb + 255) / 256), dim3(256), 0, stream, pa, ia);
+        hipLaunchKernelGGL(k_plane_pmin, dim3((nb + 255) / 256), dim3(256), 0, stream, pa, ia, skip_target * 128);
         HIPCHECK(hipGetLastError());
     } else {
         launch_t1_items(ia, stream);
@@ -1729,7 +1823,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ma.dbg = nullptr;
     ma.span = (unsigned long long *)mqspan.ptr;
     if (dd) {
-        if (!ensure<int64_t>(dbgbuf, (size_t)nb * 4, err)) return false;
+        if (!ensure<int64_t>(dbgbuf, (size_t)nb * 6, err)) return false;
         ma.dbg = (int64_t *)dbgbuf.ptr;
     }
     launch_t1_mq(ma, stream);
@@ -1774,7 +1868,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!dump(dd, "est.bin", est, (size_t)nb * 32 * 4, err)) return false;
         if (!dump(dd, "pmin.bin", pmin, nb, err)) return false;
         if (!dump(dd, "bp.bin", bp, plan.bp_words * 8, err)) return false;
-        if (!dump(dd, "mqdbg.bin", dbgbuf, (size_t)nb * 4 * 8, err)) return false;
+        if (!dump(dd, "mqdbg.bin", dbgbuf, (size_t)nb * 6 * 8, err)) return false;
     }
     // no host wait: tier-1 totals and the overflow flag reach the host with
     // the first tier-2 summary (t2_size), stage times via collect_profile()
@@ -1828,6 +1922,13 @@ void GpuEncoder::select_launch(const Plan &plan, const int *halt) {
     sa.ctl = (uint32_t *)sel_ctl.ptr;
     sa.K = (uint64_t *)thr.ptr;
     sa.Kc = (uint64_t *)thr.ptr + kMaxLayers;
+    sa.dbg = nullptr;
+#ifdef JP2HIP_DEBUG_DUMPS
+    if (getenv("JP2HIP_DUMP_DIR")) {
+        std::string e;
+        if (ensure<int64_t>(dbgsel, 128, e)) sa.dbg = (int64_t *)dbgsel.ptr;
+    }
+#endif
     hipLaunchKernelGGL(k_select, dim3((nb + kSelThreads - 1) / kSelThreads), dim3(kSelThreads), 0, stream, sa);
 }
 
@@ -1882,18 +1983,15 @@ bool GpuEncoder::apply_thresholds(const Plan &plan, const int *halt, std::string
     aa.rates = (const int32_t *)rates.ptr;
     aa.nl = (uint8_t *)nl.ptr;
     aa.lrate = (int32_t *)lrate.ptr;
-    if (nb) hipLaunchKernelGGL(k_apply, dim3((nb + 255) / 256), dim3(256), 0, stream, aa);
+    // (k_t2_wave assigns the layers itself in its sizing pass)
+    if (nb && !t2_wave) hipLaunchKernelGGL(k_apply, dim3((nb + 255) / 256), dim3(256), 0, stream, aa);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[7], stream));
     return true;
 }
 
-// Device rate loop (RateState, jp2hip_internal.h): same arithmetic as the
-// host loop it replaces and the oracle's (oracle_encode, rate_bpp > 0).
-__device__ __forceinline__ void rate_budgets(const RateState &r, int L, int64_t *budget) {
-    const int64_t b = r.budget < 0 ? 0 : r.budget;
-    for (int l = 0; l < L; l++) budget[l] = b >> (L - 1 - l);
-}
+// Device rate loop (RateState, jp2hip_internal.h; the step itself is
+// rate_step in device_common.h, run by k_t2_total)
 __global__ void k_rate_init(RateState *rs, RateState init, int L, int64_t *budget) {
     RateState r = init;
     r.it = 0;
@@ -1905,47 +2003,6 @@ __global__ void k_rate_init(RateState *rs, RateState init, int L, int64_t *budge
     *rs = r;
     rate_budgets(r, L, budget);
 }
-// Each iteration that runs also leaves the state and the summary it decided
-// on in host-mapped memory (out_rs, out_sum): the host reads them after its
-// wait with no copy launches.
-__device__ __forceinline__ void rate_out(const RateState &r, const T2Summary *sum, RateState *out_rs,
-                                         T2Summary *out_sum) {
-    *out_rs = r;
-    *out_sum = *sum;
-}
-__global__ void k_rate_step(RateState *rs, const T2Summary *sum, int L, int64_t *budget, RateState *out_rs,
-                            T2Summary *out_sum) {
-    RateState r = *rs;
-    if (r.halt) return;
-    if (sum->err) {  // tier-1 overflow: the host reports it
-        r.halt = 1;
-        *rs = r;
-        rate_out(r, sum, out_rs, out_sum);
-        return;
-    }
-    if (r.it == 0 && r.skip_target > 0 && sum->skipped && sum->t1_bytes < r.skip_target) {
-        r.safety = 1;
-        r.halt = 1;
-        *rs = r;
-        rate_out(r, sum, out_rs, out_sum);
-        return;
-    }
-    r.iters++;
-    r.cs_bytes = r.fixed + sum->part_bytes;
-    if (r.cs_bytes <= r.target || r.it == 7) {
-        r.halt = 1;
-    } else {
-        // exponential back-off + 1/16 of the overshoot + 64 B, as the oracle
-        const int64_t over = r.cs_bytes - r.target;
-        r.budget -= (over << r.it) + (over >> 4) + 64;
-        if (r.budget < 0) r.budget = 0;
-        r.it++;
-        rate_budgets(r, L, budget);
-    }
-    *rs = r;
-    rate_out(r, sum, out_rs, out_sum);
-}
-
 bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart, int batch, bool profile,
                            StageTimes &st, RateState &rs, T2Summary &sum, std::string &err) {
     HIPCHECK(hipSetDevice(device));
@@ -1961,16 +2018,19 @@ bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart
     const int *halt = &d->halt;
     HIPCHECK(hipEventRecord(ev[6], stream));
     if (restart) hipLaunchKernelGGL(k_rate_init, dim3(1), dim3(1), 0, stream, d, init, L, (int64_t *)budget.ptr);
+    (void)o_sum;
     for (int i = 0; i < batch; i++) {
         select_launch(plan, halt);
         if (!apply_thresholds(plan, halt, err)) return false;
-        t2_size_launch(plan, true, halt);
-        hipLaunchKernelGGL(k_rate_step, dim3(1), dim3(1), 0, stream, d, (const T2Summary *)t2sum.ptr, L,
-                           (int64_t *)budget.ptr, o_rs, o_sum);
+        t2_size_launch(plan, true, halt, d, o_rs);
     }
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[9], stream));
     if (!host_wait(err)) return false;
+#ifdef JP2HIP_DEBUG_DUMPS
+    if (const char *dd = getenv("JP2HIP_DUMP_DIR"))
+        if (dbgsel.ptr && !dump(dd, "seldbg.bin", dbgsel, 128 * 8, err)) return false;
+#endif
     std::atomic_thread_fence(std::memory_order_acquire);
     std::memcpy(&sum, h_rs + 1, sizeof sum);
     std::memcpy(&rs, h_rs, sizeof rs);

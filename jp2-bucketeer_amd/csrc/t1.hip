@@ -738,6 +738,8 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         ndec = left;
         cur = ptr[0];
     }
+    uint64_t cyc_wait = 0;  // debug census: shader cycles spent at the chunk barrier
+    const uint64_t cyc0 = __builtin_readcyclecounter();
     for (int it = 0;; it++) {
         // close finished passes (empty passes close at once)
         while (left <= 0 && s < nseg) {
@@ -796,9 +798,15 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
             ptr++;
             cur = nxt;
         }
+        const uint64_t c1 = a.dbg ? __builtin_readcyclecounter() : 0;
         __syncthreads();  // chunk `it` ready; the coder is done with chunk it - 1
+        if (a.dbg) cyc_wait += __builtin_readcyclecounter() - c1;
     }
-    if (a.dbg && b >= 0) a.dbg[(size_t)b * 4 + 0] = ndec;
+    if (a.dbg && b >= 0) {  // debug census: decisions, modeller cycles, of which at the barrier
+        a.dbg[(size_t)b * 6 + 0] = ndec;
+        a.dbg[(size_t)b * 6 + 1] = (int64_t)(__builtin_readcyclecounter() - cyc0);
+        a.dbg[(size_t)b * 6 + 2] = (int64_t)cyc_wait;
+    }
 }
 
 // Coder (wave 1): C, CT, B and the output bytes of the same 64 blocks.
@@ -819,16 +827,24 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
         R = a.rates + (size_t)b * kMaxPasses;
     }
     int sdone = 0;
+    uint64_t cyc_wait = 0;  // debug census (as the modeller's)
+    const uint64_t cyc0 = __builtin_readcyclecounter();
     for (int it = 0;; it++) {
+        const uint64_t c1 = a.dbg ? __builtin_readcyclecounter() : 0;
         __syncthreads();  // chunk `it` written by the modeller
+        if (a.dbg) cyc_wait += __builtin_readcyclecounter() - c1;
         const int buf = it & 1;
         // passes that ended before this chunk end at the current length
         const int s_now = sh.segs[buf][lane];
         for (; sdone < s_now; sdone++) R[sdone] = m.bp + 3;
         if (!sh.more[buf]) break;
+        // the chunk's 16 words read up front (one wait, not one per decision)
         const uint32_t *in = &sh.code[buf][0][lane];
+        uint32_t cw[kMqChunk];
 #pragma unroll
-        for (int j = 0; j < kMqChunk; j++) mq_code(m, in[j * 64], ring);
+        for (int j = 0; j < kMqChunk; j++) cw[j] = in[j * 64];
+#pragma unroll
+        for (int j = 0; j < kMqChunk; j++) mq_code(m, cw[j], ring);
         ring_flush(m, ring, fl);
     }
     if (b < 0) return;
@@ -846,6 +862,11 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
     }
     a.npasses[b] = (uint8_t)nseg;
     a.lengths[b] = len;
+    if (a.dbg) {  // coder cycles, of which at the barrier; lane-order position
+        a.dbg[(size_t)b * 6 + 3] = (int64_t)(__builtin_readcyclecounter() - cyc0);
+        a.dbg[(size_t)b * 6 + 4] = (int64_t)cyc_wait;
+        a.dbg[(size_t)b * 6 + 5] = blockIdx.x * 64 + lane;
+    }
 }
 
 // The launch's execution span is recorded in 100 MHz wall-clock ticks
@@ -891,11 +912,6 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
     __syncthreads();
     if (tid < 64) mq_modeller(a, sh);
     else mq_coder(a, sh);
-    if (a.dbg && tid >= 64 && sh.blk[lane] >= 0) {  // debug census: 100 MHz ticks, lane position
-        a.dbg[(size_t)sh.blk[lane] * 4 + 1] = 0;
-        a.dbg[(size_t)sh.blk[lane] * 4 + 2] = (int64_t)(wall_clock64() - w0);
-        a.dbg[(size_t)sh.blk[lane] * 4 + 3] = blockIdx.x * 64 + lane;
-    }
     if (tid == 64) atomicMax(&a.span[1], (unsigned long long)wall_clock64());
 }
 

@@ -123,6 +123,7 @@ void t2_tables(const Plan &P, int tile0, int tile1, int block0, T2Tables &T) {
     T.prec.clear();
     T.tp.clear();
     T.tt_nodes = 0;
+    T.max_prec_blocks = 0;
     // tile-parts per tile, in tile order first
     std::vector<std::vector<TpDesc>> per_tile((size_t)std::max(0, tile1 - tile0));
     for (int t = tile0; t < tile1; t++) {
@@ -143,13 +144,16 @@ void t2_tables(const Plan &P, int tile0, int tile1, int block0, T2Tables &T) {
                         d.nb = (uint8_t)pr.nb;
                         d.tt_off = (int32_t)T.tt_nodes;
                         d.nsop0 = nsop;
+                        int blocks = 0;
                         for (int bi = 0; bi < pr.nb; bi++) {
                             const PrecBand &pb = pr.pb[bi];
                             d.first[bi] = pb.first - block0;
                             d.ncw[bi] = (uint16_t)pb.ncw;
                             d.nch[bi] = (uint16_t)pb.nch;
+                            blocks += pb.ncw * pb.nch;
                             if (pb.ncw && pb.nch) T.tt_nodes += 2 * tree_nodes(pb.ncw, pb.nch);
                         }
+                        T.max_prec_blocks = std::max(T.max_prec_blocks, blocks);
                         T.prec.push_back(d);
                         tp.nprec++;
                         nsop += L;

@@ -45,8 +45,13 @@ struct T2Args {
     int ntp;
     const BlockDesc *blocks;
     const uint8_t *P;       // coded planes per block
-    const uint8_t *nl;      // [block][L] cumulative passes
-    const int32_t *lrate;   // [block][L] cumulative bytes
+    uint8_t *nl;            // [block][L] cumulative passes (written by k_t2_wave<false> / k_apply)
+    int32_t *lrate;         // [block][L] cumulative bytes
+    // layer assignment inputs (k_t2_wave<false>): hulls, thresholds
+    const uint8_t *nhull, *hpass, *npasses;
+    const uint64_t *hkey, *K;
+    const int32_t *rates;
+    int lossless;
     int L, sop, eph, plt;
     uint32_t *tt;           // tag-tree nodes: value | low << 8 | known << 16
     int8_t *lblock, *incl;  // per block coding state
@@ -293,16 +298,239 @@ __global__ void __launch_bounds__(64) k_t2_code(T2Args a) {
     }
 }
 
+// --------------------------------------------------------------------------
+// k_t2_wave: one wave per precinct, lane j = the precinct's j-th code-block
+// (bands in order, raster order inside a band), for precincts of <= 64
+// blocks (the recipe's: at most 2 x 2 per band).  Per layer the lanes work
+// out, in parallel, everything of a block's contribution that is not a
+// tag-tree bit -- pass count codeword (Table B.4), Lblock increments, the
+// length field -- and lane 0 writes the header bits in block order (the tag
+// trees, whose nodes several blocks share, and the 0xFF bit stuffing are
+// serial by nature).  No global memory is touched inside the layer loop.
+// The sizing pass (EMIT = false) also assigns each block its passes per layer
+// from the thresholds K (what k_apply does for the serial kernel) and writes
+// nl / lrate for the emission pass and k_t2_copy.
+// --------------------------------------------------------------------------
+constexpr int kT2Waves = 4;  // precincts per workgroup
+struct T2LaneShared {
+    uint8_t nl[kMaxLayers][64];     // cumulative passes per layer
+    int32_t lr[kMaxLayers][64];     // cumulative bytes per layer
+    uint64_t p1v[64];               // pass-count codeword, then the Lblock comma code
+    int32_t len[64];                // this layer's bytes
+    uint8_t n[64], p1n[64], p2n[64], first[64];
+    uint32_t tt[kLdsNodes];         // tag-tree nodes
+    uint32_t hdr;                   // header bytes of the packet (lane 0 -> all)
+};
+
+// the lanes of one wave see each other's LDS writes in program order; this
+// only keeps the compiler from moving LDS accesses across the point
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// put up to 64 bits (nb <= 64) through the 32-bit-at-a-time writer
+template <bool EMIT>
+__device__ __forceinline__ void put64(DevBits<EMIT> &w, uint64_t v, int nb) {
+    if (nb > 32) {
+        w.put((uint32_t)(v >> 32), nb - 32);
+        nb = 32;
+    }
+    if (nb > 0) w.put((uint32_t)v & (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)), nb);
+}
+
+template <bool EMIT>
+__global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
+    __shared__ T2LaneShared lds[kT2Waves];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pi = blockIdx.x * kT2Waves + wv;
+    if (pi >= a.nprec || (!EMIT && a.halt && *a.halt)) return;  // (wave-uniform)
+    T2LaneShared &S = lds[wv];
+    const PrecDesc d = a.prec[pi];
+    const int L = a.L;
+    // lane -> (band, leaf, block)
+    const int c0 = d.nb > 0 ? d.ncw[0] * d.nch[0] : 0, c1 = d.nb > 1 ? d.ncw[1] * d.nch[1] : 0,
+              c2 = d.nb > 2 ? d.ncw[2] * d.nch[2] : 0;
+    const int nbt = c0 + c1 + c2;
+    const bool own = lane < nbt;
+    const int bi = lane < c0 ? 0 : (lane < c0 + c1 ? 1 : 2);
+    const int leaf = lane - (bi == 0 ? 0 : (bi == 1 ? c0 : c0 + c1));
+    const int b = own ? d.first[bi] + leaf : 0;
+    int zero_planes = 0;
+    if (own) {
+        zero_planes = a.blocks[b].Mb - a.P[b];
+        uint8_t *gnl = a.nl + (size_t)b * L;
+        int32_t *glr = a.lrate + (size_t)b * L;
+        if (!EMIT) {
+            // passes per layer from the thresholds: the last hull point whose
+            // slope key >= K (lossless: the last layer takes every pass).
+            // Hull keys strictly decrease, so each layer's point is found by
+            // walking from the previous layer's (thresholds fall with the
+            // layer: forward); the first 8 keys are loaded together
+            const int nh = a.nhull[b];
+            const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
+            const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
+            const int32_t *R = a.rates + (size_t)b * kMaxPasses;
+            uint64_t k8[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) k8[i] = hk[min(i, kMaxPasses)];
+            int at = 0;  // last hull point with key >= K (point 0: nothing)
+            for (int l = 0; l < L; l++) {
+                int nc;
+                if (a.lossless && l == L - 1) {
+                    nc = a.npasses[b];
+                } else {
+                    const uint64_t K = a.K[l];
+                    auto key = [&](int i) { return i < 8 ? k8[i] : hk[i]; };
+                    while (at + 1 < nh && key(at + 1) >= K) at++;
+                    while (at > 0 && key(at) < K) at--;  // (a threshold above the previous one)
+                    nc = hp[at];
+                }
+                const int32_t r = nc ? R[nc - 1] : 0;
+                S.nl[l][lane] = (uint8_t)nc;
+                S.lr[l][lane] = r;
+                gnl[l] = (uint8_t)nc;
+                glr[l] = r;
+            }
+        } else {
+            for (int l = 0; l < L; l++) {
+                S.nl[l][lane] = gnl[l];
+                S.lr[l][lane] = glr[l];
+            }
+        }
+    }
+    // tag trees (nodes in LDS when they fit, else the precinct's global slot):
+    // inclusion layer and zero bit-planes of every leaf
+    int nodes = 0, toff[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        toff[k] = nodes;
+        if (k < d.nb && d.ncw[k] && d.nch[k]) nodes += 2 * tree_size(d.ncw[k], d.nch[k]);
+    }
+    uint32_t *tt = nodes <= kLdsNodes ? S.tt : a.tt + d.tt_off;
+    int firstl = L;
+    if (own)
+        for (int l = 0; l < L; l++)
+            if (S.nl[l][lane] > 0) {
+                firstl = l;
+                break;
+            }
+    S.first[lane] = (uint8_t)firstl;
+    S.n[lane] = (uint8_t)zero_planes;  // (staged for lane 0's tree_set)
+    wave_lds_sync();
+    if (lane == 0) {
+        for (int i = 0; i < nodes; i++) tt[i] = 0xFFu;  // value 255 = unset, low 0, not known
+        for (int j = 0; j < nbt; j++) {
+            const int jb = j < c0 ? 0 : (j < c0 + c1 ? 1 : 2);
+            const int jl = j - (jb == 0 ? 0 : (jb == 1 ? c0 : c0 + c1));
+            const int w = d.ncw[jb], h = d.nch[jb];
+            uint32_t *ti = tt + toff[jb], *tz = ti + tree_size(w, h);
+            tree_set(ti, w, h, jl, S.first[j]);
+            tree_set(tz, w, h, jl, S.n[j]);
+        }
+    }
+    wave_lds_sync();
+    int incl = -1, lb = 3;  // the lane's block: inclusion layer, Lblock
+    const uint32_t fixed = (a.sop ? 6u : 0u) + (a.eph ? 2u : 0u);
+    for (int l = 0; l < L; l++) {
+        // this block's part of packet l, all but the tag-tree bits
+        int n = 0, len = 0;
+        if (own) {
+            n = (int)S.nl[l][lane] - (l ? (int)S.nl[l - 1][lane] : 0);
+            len = S.lr[l][lane] - (l ? S.lr[l - 1][lane] : 0);
+        }
+        uint64_t p1v = 0;
+        int p1n = 0, p2n = 0;
+        const bool first_time = incl < 0;
+        if (n > 0) {
+            uint32_t cv;
+            int cn;
+            if (n == 1) { cv = 0u; cn = 1; }
+            else if (n == 2) { cv = 2u; cn = 2; }
+            else if (n <= 5) { cv = (3u << 2) | (uint32_t)(n - 3); cn = 4; }
+            else if (n <= 36) { cv = (15u << 5) | (uint32_t)(n - 6); cn = 9; }
+            else { cv = (511u << 7) | (uint32_t)(n - 37); cn = 16; }
+            const int nbits0 = lb + dev_floor_log2(n);
+            const int need = len > 0 ? 32 - __clz(len) : 0;  // bit length of len
+            const int extra = need > nbits0 ? need - nbits0 : 0;
+            lb += extra;
+            p1v = ((uint64_t)cv << (extra + 1)) | (((1ull << extra) - 1ull) << 1);
+            p1n = cn + extra + 1;
+            p2n = lb + dev_floor_log2(n);
+        }
+        S.n[lane] = (uint8_t)n;
+        S.len[lane] = len;
+        S.p1v[lane] = p1v;
+        S.p1n[lane] = (uint8_t)p1n;
+        S.p2n[lane] = (uint8_t)p2n;
+        S.first[lane] = (uint8_t)(first_time ? 1 : 0);
+        const bool nonempty = __ballot(n > 0) != 0ull;
+        if (n > 0 && first_time) incl = l;
+        // body bytes before this block in the packet (blocks in order)
+        const int lin = n > 0 ? len : 0;
+        int body_before = (int)wave_incl_scan((uint32_t)lin) - lin;
+        const int body = __shfl(body_before + lin, 63, 64);
+        wave_lds_sync();
+        const size_t pk = (size_t)pi * L + l;
+        if (lane == 0) {
+            uint8_t *o = nullptr;
+            if (EMIT) {
+                o = a.out + a.pk_off[pk];
+                if (a.sop) {
+                    const uint32_t ns = (uint32_t)(d.nsop0 + l) & 0xFFFFu;
+                    o[0] = 0xFF; o[1] = 0x91; o[2] = 0; o[3] = 4; o[4] = (uint8_t)(ns >> 8); o[5] = (uint8_t)ns;
+                    o += 6;
+                }
+            }
+            DevBits<EMIT> w;
+            w.init(o);
+            w.bit(nonempty ? 1 : 0);
+            if (nonempty)
+                for (int j = 0; j < nbt; j++) {
+                    const int jb = j < c0 ? 0 : (j < c0 + c1 ? 1 : 2);
+                    const int jl = j - (jb == 0 ? 0 : (jb == 1 ? c0 : c0 + c1));
+                    const int cw = d.ncw[jb], ch = d.nch[jb];
+                    uint32_t *ti = tt + toff[jb], *tz = ti + tree_size(cw, ch);
+                    const int nj = S.n[j];
+                    const bool ft = S.first[j] != 0;
+                    if (ft) tree_encode(ti, cw, ch, jl, l + 1, w);
+                    else w.bit(nj > 0 ? 1 : 0);
+                    if (nj <= 0) continue;
+                    if (ft) tree_encode(tz, cw, ch, jl, 1 << 20, w);
+                    put64(w, S.p1v[j], S.p1n[j]);
+                    put64(w, (uint64_t)(uint32_t)S.len[j], S.p2n[j]);
+                }
+            w.flush();
+            if (EMIT) {
+                if (a.eph) { o[w.nbytes] = 0xFF; o[w.nbytes + 1] = 0x92; }
+                S.hdr = (a.sop ? 6u : 0u) + w.nbytes + (a.eph ? 2u : 0u);
+            } else {
+                a.pk_len[pk] = fixed + w.nbytes + (uint32_t)body;
+            }
+        }
+        wave_lds_sync();
+        // body pieces follow the header, in block order
+        if (EMIT && n > 0) a.blkdst[(size_t)b * L + l] = a.pk_off[pk] + S.hdr + (uint64_t)body_before;
+    }
+}
+
 __device__ __forceinline__ int varint_len(uint32_t v) {
     int k = 1;
     while (v >>= 7) k++;
     return k;
 }
 
-// Psot and SOT + PLT + SOD bytes of each tile-part (thread per tile-part)
-__global__ void __launch_bounds__(64) k_t2_tparts(T2Args a) {
-    const int t = blockIdx.x * 64 + threadIdx.x;
-    if (t >= a.ntp || (a.halt && *a.halt)) return;
+// One workgroup: each tile-part's size (SOT + PLT + SOD + packets), their
+// offsets in code-stream order, and the sums the host needs (part size,
+// header bytes, bytes per layer, tier-1 totals); in the device rate loop
+// (rate != null) also the loop's step (rate_step).
+struct RateStepArgs {
+    RateState *rs;
+    int64_t *budget;
+    RateState *out_rs;
+    T2Summary *out_sum;
+};
+__device__ __forceinline__ void tpart_size(const T2Args &a, int t) {
     const TpDesc d = a.tps[t];
     const size_t p0 = (size_t)d.prec0 * a.L, p1 = (size_t)(d.prec0 + d.nprec) * a.L;
     uint64_t body = 0, plt = 0, seg = 0;
@@ -323,17 +551,17 @@ __global__ void __launch_bounds__(64) k_t2_tparts(T2Args a) {
     a.tp_len[t] = (uint32_t)(14 + plt + body);
 }
 
-// One workgroup: tile-part offsets in code-stream order, and the sums the
-// host needs (part size, header bytes, bytes per layer, tier-1 totals).
 __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
                                                   const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
-                                                  const uint64_t *kc, const unsigned long long *acc, T2Summary *sum) {
+                                                  const uint64_t *kc, const unsigned long long *acc, T2Summary *sum,
+                                                  RateStepArgs rate) {
     __shared__ uint64_t part[256];
     __shared__ int64_t lay[256][kMaxLayers > 8 ? 8 : kMaxLayers];
     if (a.halt && *a.halt) return;  // the whole workgroup
     const int tid = threadIdx.x;
     const int chunk = (a.ntp + 255) / 256;
     const int t0 = min(a.ntp, tid * chunk), t1 = min(a.ntp, t0 + chunk);
+    for (int t = t0; t < t1; t++) tpart_size(a, t);
     uint64_t s = 0, hdr = 0;
     for (int t = t0; t < t1; t++) s += a.tp_len[t];
     part[tid] = s;
@@ -426,6 +654,10 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
         sum->tp_hdr_bytes = h;
         sum->err = *t1err;
         for (int l = 0; l < a.L; l++) sum->kc[l] = kc ? kc[l] : 0ull;
+    }
+    if (rate.rs) {
+        __syncthreads();  // (the per-layer sums come from threads 0..7)
+        if (tid == 0) rate_step(rate.rs, sum, a.L, rate.budget, rate.out_rs, rate.out_sum);
     }
 }
 
@@ -531,8 +763,15 @@ T2Args GpuEncoder::t2_args(const Plan &plan) const {
     a.ntp = t2_ntp;
     a.blocks = (const BlockDesc *)blocks.ptr;
     a.P = (const uint8_t *)P.ptr;
-    a.nl = (const uint8_t *)nl.ptr;
-    a.lrate = (const int32_t *)lrate.ptr;
+    a.nl = (uint8_t *)nl.ptr;
+    a.lrate = (int32_t *)lrate.ptr;
+    a.nhull = (const uint8_t *)nhull.ptr;
+    a.hpass = (const uint8_t *)hpass.ptr;
+    a.npasses = (const uint8_t *)npasses.ptr;
+    a.hkey = (const uint64_t *)hkey.ptr;
+    a.K = (const uint64_t *)thr.ptr;
+    a.rates = (const int32_t *)rates.ptr;
+    a.lossless = plan.rc.rate_bpp <= 0.0;
     a.L = plan.rc.layers;
     a.sop = plan.rc.sop;
     a.eph = plan.rc.eph;
@@ -556,6 +795,7 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
     const int L = plan.rc.layers;
     t2_nprec = (int)T.prec.size();
     t2_ntp = (int)T.tp.size();
+    t2_wave = T.max_prec_blocks <= 64;  // k_t2_wave (else the serial k_t2_code + k_apply)
     const size_t npk = (size_t)t2_nprec * L;
     if (!ensure_t2<PrecDesc>(t2prec, T.prec.size(), err) || !ensure_t2<TpDesc>(t2tp, T.tp.size(), err) ||
         !ensure_t2<uint32_t>(t2tt, (size_t)T.tt_nodes, err) || !ensure_t2<int8_t>(t2lblock, nb, err) ||
@@ -574,16 +814,25 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
     return true;
 }
 
-void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt) {
+void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt, RateState *rs,
+                                RateState *out_rs) {
     const int nb = (int)plan.blocks.size();
     T2Args a = t2_args(plan);
     a.halt = halt;
-    if (t2_nprec) hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
-    if (t2_ntp) hipLaunchKernelGGL(k_t2_tparts, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
+    RateStepArgs ra;
+    ra.rs = rs;
+    ra.budget = (int64_t *)budget.ptr;
+    ra.out_rs = out_rs;
+    ra.out_sum = out_rs ? (T2Summary *)(out_rs + 1) : nullptr;
+    if (t2_nprec && t2_wave)
+        hipLaunchKernelGGL(k_t2_wave<false>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
+                           stream, a);
+    else if (t2_nprec)
+        hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
                        (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
                        with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
-                       (const unsigned long long *)ordkey.ptr, (T2Summary *)t2sum.ptr);
+                       (const unsigned long long *)ordkey.ptr, (T2Summary *)t2sum.ptr, ra);
 }
 
 bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,
@@ -606,6 +855,11 @@ bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTime
     return true;
 }
 
+bool GpuEncoder::t2_reserve(uint64_t part_bytes, std::string &err) {
+    HIPCHECK(hipSetDevice(device));
+    return ensure_t2<uint8_t>(t2out, part_bytes, err);
+}
+
 bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
                          StageTimes &st, std::string &err) {
     HIPCHECK(hipSetDevice(device));
@@ -615,7 +869,11 @@ bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, u
     a.base = base;
     HIPCHECK(hipEventRecord(ev[8], stream));
     if (t2_ntp) hipLaunchKernelGGL(k_t2_tp_emit, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
-    if (t2_nprec) hipLaunchKernelGGL(k_t2_code<true>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
+    if (t2_nprec && t2_wave)
+        hipLaunchKernelGGL(k_t2_wave<true>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
+                           stream, a);
+    else if (t2_nprec)
+        hipLaunchKernelGGL(k_t2_code<true>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
     if (nb) hipLaunchKernelGGL(k_t2_copy, dim3((nb + 3) / 4), dim3(256), 0, stream, a, nb, (const uint8_t *)t1out.ptr);
     HIPCHECK(hipGetLastError());
     // host_dst is pinned (api.cpp out_alloc): an async D2H on this context's

@@ -62,7 +62,8 @@ class Stats(Structure):
 
 
 # every symbol include/jp2hip.h declares
-EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_device_count", "jp2hip_recipe_init",
+EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_device_count", "jp2hip_device_ordinals",
+           "jp2hip_recipe_init",
            "jp2hip_create", "jp2hip_destroy", "jp2hip_encode_file", "jp2hip_encode_tiff",
            "jp2hip_tiff_layout", "jp2hip_encode_device", "jp2hip_free",
            # batch path (csrc/batch.cpp; bound in jp2hip.batch)
@@ -95,6 +96,8 @@ def lib():
     L.jp2hip_last_error.restype = c_char_p
     L.jp2hip_probe.restype = c_int
     L.jp2hip_device_count.restype = c_int
+    L.jp2hip_device_ordinals.argtypes = [POINTER(c_int32), c_int32]
+    L.jp2hip_device_ordinals.restype = c_int
     L.jp2hip_recipe_init.argtypes = [POINTER(Recipe), c_int]
     L.jp2hip_create.argtypes = [POINTER(c_void_p), POINTER(Config)]
     L.jp2hip_destroy.argtypes = [c_void_p]
@@ -137,6 +140,16 @@ def probe() -> bool:
 def device_count() -> int:
     """gfx950 devices visible to libjp2hip (0 without a GPU)."""
     return int(lib().jp2hip_device_count())
+
+
+def device_ordinals() -> list[int]:
+    """HIP ordinals of the visible gfx950 devices (Encoder(device=...) takes these)."""
+    n = int(lib().jp2hip_device_ordinals(None, 0))
+    if n <= 0:
+        return []
+    buf = (c_int32 * n)()
+    n = min(n, int(lib().jp2hip_device_ordinals(buf, n)))
+    return [int(buf[i]) for i in range(n)]
 
 
 def recipe(conversion: int, **overrides) -> Recipe:

@@ -117,7 +117,7 @@ class GpuConverter(Converter):
         except OSError as e:  # KakaduConverter.java:48-52 throws BUCKETEER_163 here
             raise IOError(BUCKETEER_002.format(self.tmp_dir)) from e
         if devices is None:
-            devices = list(range(_lib.device_count()))
+            devices = _lib.device_ordinals()
         try:
             self._pool = [_lib.Encoder(d, host_threads) for _ in range(max(1, per_gpu)) for d in devices]
         except _lib.Jp2hipError as e:

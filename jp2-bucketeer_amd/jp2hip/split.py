@@ -32,9 +32,11 @@ from . import _lib
 from ._lib import ALLREDUCE_FN, Jp2hipError, Layout, Split
 
 
-def split_rows(height: int, tile_h: int, rank: int, world: int, flush_period: int = 1024) -> tuple[int, int]:
+def split_rows(height: int, tile_h: int, rank: int, world: int, flush_period: int) -> tuple[int, int]:
     """Image rows [row0, row1) whose tiles rank ``rank`` of ``world`` encodes
-    (whole -flush_period stripes of tile rows, recipe.flush_period)."""
+    (whole -flush_period stripes of tile rows).  Pass the encode's own
+    recipe.tile_h and recipe.flush_period (no default: a band computed with
+    another period is not the band the encoder reads)."""
     r0, r1 = c_int32(), c_int32()
     _lib.lib().jp2hip_split_rows(height, tile_h, flush_period, rank, world, byref(r0), byref(r1))
     return r0.value, r1.value

@@ -27,14 +27,19 @@ def opj(tool: str) -> str | None:
 
 
 def synth_rgb8(h, w, seed=1234, noise=6.0):
-    """C2-style content: sinusoids + checker patch + gaussian noise."""
+    """C2-style content: sinusoids + checker patch + gaussian noise.
+    (Row / column terms are broadcast, not evaluated on the full grid: the
+    same float64 operations in the same order, so the same pixels.)"""
     rng = np.random.default_rng(seed)
-    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
-    img = np.zeros((h, w, 3))
+    x = np.arange(w, dtype=np.float64)[None, :]
+    y = np.arange(h, dtype=np.float64)[:, None]
+    d = 20 * np.sin((x + y) / 11.0)
+    img = np.empty((h, w, 3))
     for c in range(3):
-        img[..., c] = 128 + 40 * np.sin(x / 37.0 + c) + 30 * np.cos(y / 23.0 - c) + 20 * np.sin((x + y) / 11.0)
+        img[..., c] = 128 + 40 * np.sin(x / 37.0 + c) + 30 * np.cos(y / 23.0 - c) + d
+    del d
     ys, xs = slice(h // 5, 2 * h // 5), slice(w // 5, 7 * w // 15)
-    chk = 50 * ((np.floor(x[ys, xs] / 16) + np.floor(y[ys, xs] / 16)) % 2 - 0.5)
+    chk = 50 * ((np.floor(x[:, xs] / 16) + np.floor(y[ys, :] / 16)) % 2 - 0.5)
     img[ys, xs, :] += chk[..., None]
     img += rng.normal(0, noise, img.shape)
     return np.clip(img, 0, 255).astype(np.uint8)
@@ -52,11 +57,13 @@ def testjpx_tiled(pix: np.ndarray, h=4000, w=6000) -> np.ndarray:
 def synth_u16(h, w, comps=3, seed=2):
     """C3/C5-style 16-bit content scaled to [0, 65535] plus N(0, 400)."""
     rng = np.random.default_rng(seed)
-    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
-    out = np.zeros((h, w, comps))
+    x = np.arange(w, dtype=np.float64)[None, :]
+    y = np.arange(h, dtype=np.float64)[:, None]
+    d = 6000 * np.sin((x - y) / 17.0)
+    out = np.empty((h, w, comps))
     for c in range(comps):
-        out[..., c] = 32768 + 12000 * np.sin(x / 53.0 + c) + 9000 * np.cos(y / 31.0 - 2 * c) + \
-            6000 * np.sin((x - y) / 17.0)
+        out[..., c] = 32768 + 12000 * np.sin(x / 53.0 + c) + 9000 * np.cos(y / 31.0 - 2 * c) + d
+    del d
     out += rng.normal(0, 400, out.shape)
     out = np.clip(out, 0, 65535).astype(np.uint16)
     return out if comps > 1 else out[..., 0]

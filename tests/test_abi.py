@@ -216,6 +216,7 @@ def test_factory_without_gpu_or_kakadu(monkeypatch):
     with pytest.raises(IOError, match="Failed to convert TIFF to JP2: img1"):
         conv.convert("img1", "y.tif", Conversion.LOSSLESS)
     assert jp2hip.device_count() == 0
+    assert jp2hip.device_ordinals() == []
     with pytest.raises(ValueError):
         ConverterFactory.get_converter(str)
     ConverterFactory.reset()

@@ -51,6 +51,12 @@ CASES = [
     (600, 777, 1, 16, True, 7, 512),
     (150, 250, 3, 8, True, 0, 512),
     (450, 350, 3, 8, False, 2, 128),
+    # tiles wider than 1024: DWT level 1 by the windowed kernel (k_dwt_l1, one
+    # component fits its LDS) or per component (k_dwt_band<INGEST>)
+    (520, 2100, 1, 8, False, 6, 2048),
+    (300, 2100, 1, 16, True, 6, 2048),
+    (520, 2100, 3, 8, True, 6, 2048),
+    (520, 2100, 3, 8, False, 6, 2048),
 ]
 
 
@@ -102,6 +108,21 @@ def test_golden_lossy_cases(encoder, golden, testjpx_pixels, case):
     ps = im.psnr(img, dec, c["bits"])
     assert abs(ps - c["oracle_psnr"]) < 1e-3
     assert ps >= c["opj_psnr"] - 0.1
+
+
+@pytest.mark.parametrize("cblk", [4, 5])
+@pytest.mark.parametrize("lossless", [True, False])
+def test_small_codeblocks_identical_to_oracle(encoder, cblk, lossless):
+    """Cblk={16,16} / {32,32}: precincts of up to 192 / 48 code-blocks -- tier-2's
+    serial per-precinct kernel (k_t2_code + k_apply, more than 64 blocks) and
+    the wave-per-precinct one (k_t2_wave) -- byte-identical to the oracle."""
+    img = _img(300, 420, 3, 8, seed=5)
+    conv = jp2hip.LOSSLESS if lossless else jp2hip.LOSSY
+    rc = jp2hip.recipe(conv, cblk_w_log2=cblk, cblk_h_log2=cblk)
+    got, st = encoder.encode_tiff(im.tiff_bytes(img), conv, rc)
+    assert got == ol.encode(img, ol.copy_recipe(rc))
+    if lossless:
+        assert np.array_equal(im.decode_pillow(got), img)
 
 
 @pytest.mark.parametrize("rate", [3.0, 1.0])
@@ -342,6 +363,32 @@ def test_gpu_converter_like_kakadu_converter_test(tmp_path, testjpx_pixels):
     with pytest.raises(IOError, match="Failed to convert TIFF to JP2"):
         conv.convert("missing", tmp_path / "nope.tif", Conversion.LOSSY)
     ConverterFactory.reset()
+
+
+def test_unicode_tiff_path(tmp_path, testjpx_pixels):
+    """ImageUploadKakaduIT converts /images/熵.tif (ImageUploadKakaduIT.java:69):
+    a non-ASCII TIFF path through GpuConverter.convert and, below it, the C
+    ABI's jp2hip_encode_file (UTF-8 path bytes, both directions)."""
+    from jp2hip.converters import Conversion, ConverterFactory, GpuConverter
+    d = tmp_path / "图像"
+    d.mkdir()
+    tif = d / "熵.tif"
+    tif.write_bytes(im.tiff_bytes(testjpx_pixels))
+    conv = ConverterFactory.get_converter(GpuConverter)
+    jpx = conv.convert("熵", tif, Conversion.LOSSLESS)
+    assert jpx.exists() and jpx.stat().st_size > 30000
+    assert np.array_equal(im.decode_pillow(jpx.read_bytes()), testjpx_pixels)
+    jpx.unlink()
+    ConverterFactory.reset()
+    enc = jp2hip.Encoder(0)
+    try:
+        out = d / "熵.jpx"
+        enc.encode_file(str(tif), str(out), jp2hip.LOSSLESS)
+        assert np.array_equal(im.decode_pillow(out.read_bytes()), testjpx_pixels)
+        with pytest.raises(jp2hip.Jp2hipError, match="cannot open TIFF"):
+            enc.encode_file(str(d / "熵-missing.tif"), str(d / "x.jpx"), jp2hip.LOSSLESS)
+    finally:
+        enc.close()
 
 
 def test_concurrent_callers(tmp_path):

@@ -1,36 +1,48 @@
 #!/usr/bin/env python3
-"""Per-block MQ census on the GPU (debug): decisions vs shader cycles."""
-import os, sys, tempfile
+"""Per-block MQ census on the GPU (debug library): decisions, and the shader
+cycles of the modeller and coder waves (k_t1_mq), with the part of each spent
+at the chunk barrier -- which of the two chains sets the pace.
+
+  make -C jp2-bucketeer_amd/csrc debug
+  JP2HIP_LIBRARY=jp2-bucketeer_amd/jp2hip/libjp2hip_debug.so python tests/tools/mq_census.py
+"""
+import os
+import sys
+import tempfile
+
 import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(ROOT, "tests")); sys.path.insert(0, os.path.join(ROOT, "jp2-bucketeer_amd"))
-import imaging as im, jp2hip
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "jp2-bucketeer_amd"))
+import imaging as im  # noqa: E402
+import jp2hip  # noqa: E402
+
 img = im.synth_rgb8(4000, 6000, seed=1234)
 tif = im.tiff_bytes(img)
 enc = jp2hip.Encoder(0, profile=True)
 enc.encode_tiff(tif, jp2hip.LOSSY)
-d = tempfile.mkdtemp(); os.environ["JP2HIP_DUMP_DIR"] = d
+d = tempfile.mkdtemp()
+os.environ["JP2HIP_DUMP_DIR"] = d
 out, st = enc.encode_tiff(tif, jp2hip.LOSSY)
-a = np.fromfile(os.path.join(d, "mqdbg.bin"), dtype=np.int64).reshape(-1, 4)
-dec, cyc, wall = a[:, 0], a[:, 1], a[:, 2]
+a = np.fromfile(os.path.join(d, "mqdbg.bin"), dtype=np.int64).reshape(-1, 6)
+dec, mcyc, mwait, ccyc, cwait, pos = (a[:, i] for i in range(6))
 m = dec > 0
-print("t1_mq_ms", st.t1_mq_ms, "blocks", m.sum(), "dec total", dec.sum(), "max", dec.max())
-
-
-
-o = np.argsort(-cyc)[:8]
-for i in o: print(i, a[i])
-print("decisions per block: mean", dec[m].mean(), "p50", np.median(dec[m]), "p99", np.percentile(dec[m], 99))
-wt = wall[m] / 100.0  # us
-print("per-block wall us: mean", wt.mean(), "p50", np.median(wt), "p99", np.percentile(wt, 99), "max", wt.max())
-print("sum decisions / t1_mq_ms => Gdec/s", dec.sum() / (st.t1_mq_ms * 1e-3) / 1e9)
-print("stages", st.as_dict())
-gi = a[:, 3]
-lanes = int(os.environ.get("JP2HIP_MQ_LANES", "64"))
-wv = gi[m] // lanes
-import collections
-print("ns per decision (per block wall/dec): p10 %.1f p50 %.1f p90 %.1f" % tuple(np.percentile(wall[m] * 10.0 / dec[m], [10, 50, 90])))
-for q in (0, 1, 2, 10, 100, 300, 1000):
-    sel = wv == q
-    if sel.any():
-        print("wave", q, "dec max", dec[m][sel].max(), "min", dec[m][sel].min(), "wall us max", wall[m][sel].max() / 100.0)
+print("t1_mq_ms %.3f  blocks %d  decisions %d  max/block %d" % (st.t1_mq_ms, m.sum(), dec.sum(), dec.max()))
+wave = pos[m] // 64
+for w in (0, 1, 2, 5, 20, 100):
+    sel = wave == w
+    if not sel.any():
+        continue
+    dm = dec[m][sel].max()
+    mc, mw = mcyc[m][sel].max(), mwait[m][sel].max()
+    cc, cw = ccyc[m][sel].max(), cwait[m][sel].max()
+    print(f"wave {w:4d}: decisions max {dm:6d}  modeller {mc / dm:6.1f} cyc/dec ({mw / mc * 100:4.1f}% at barrier)"
+          f"  coder {cc / dm:6.1f} cyc/dec ({cw / cc * 100:4.1f}% at barrier)")
+print("stages", {k: round(v, 3) for k, v in st.as_dict().items() if k.endswith("_ms")})
+sel = os.path.join(d, "seldbg.bin")
+if os.path.exists(sel):
+    s = np.fromfile(sel, dtype=np.int64)
+    n = int(s[0])
+    print("k_select (last call): lists", n, "sizes", s[1:1 + n].tolist(), "rounds", s[33:39].tolist(),
+          "survivors", s[65:71].tolist())
