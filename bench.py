@@ -255,7 +255,8 @@ def run(args):
     batch = max(1, args.batch or nf)
     total = args.steps * batch
     host_threads = max(2, 16 // nf)
-    encs = [jp2hip.Encoder(local, host_threads=host_threads, profile=True) for _ in range(nf)]
+    prof = os.environ.get("JP2HIP_BENCH_PROFILE", "1") != "0"  # stage times from HIP events (roofline below)
+    encs = [jp2hip.Encoder(local, host_threads=host_threads, profile=prof) for _ in range(nf)]
     rc = jp2hip.recipe(jp2hip.LOSSY)
     # every C2 launch's stage times, so the kernel averages cover the same
     # launches a rocprofv3 --kernel-trace of this command sees
@@ -391,14 +392,15 @@ def run(args):
             # DWT stage time from HIP events on the context's stream: under
             # load (the event span includes waiting for CUs other images
             # hold) and alone (one image on the GPU)
-            "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
+            "roofline_dwt": ({"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                              "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                              "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
                              "alg_bytes_per_px": round(dwt_bytes_per_px(C, 1, L), 3),
                              "stage_ms": round(avg["dwt_ms"], 4),
                              "alone": {"stage_ms": round(dwt_alone, 4),
                                        "achieved": round(dwt_alg / (dwt_alone * 1e-3) / 1e9, 2),
-                                       "frac": round(dwt_alg / (dwt_alone * 1e-3) / HBM_PEAK, 5)}},
+                                       "frac": round(dwt_alg / (dwt_alone * 1e-3) / HBM_PEAK, 5)}}
+                             if avg["dwt_ms"] > 0 and dwt_alone > 0 else None),
             "t1_counters": {"k_t1_mq": sq_counters("k_t1_mq"), "k_t1_cm3": sq_counters("k_t1_cm3"),
                             "k_quant": sq_counters("k_quant")},
             "stages_ms": {k: round(avg[k], 4) for k in ("ingest_ms", "dwt_ms", "quant_ms", "t1_cm_ms",

@@ -382,6 +382,79 @@ bool unpack_if_compressed(jp2hip_ctx *ctx, const void *&d_src, size_t src_len, c
     return true;
 }
 
+// Tile-split with compressed or tiled strips (a rank's band of a BigTIFF
+// master): only the strips / tiles that image rows [row0, row1) touch are
+// decoded -- as a stand-alone image of their rows [R0, R1) -- and the result
+// is described as a full-image layout of uncompressed strips whose entries
+// outside the band are never read (the sub-plan reads only its rows).  Only
+// the band's units must lie inside d_src, as for uncompressed strips.
+bool unpack_band(jp2hip_ctx *ctx, const void *&d_src, size_t src_len, const jp2hip_layout *&lay, int row0, int row1,
+                 jp2hip_layout &ulay, std::vector<uint64_t> &uoffs, std::string &err) {
+    if (lay->compression <= 1 && lay->tile_width <= 0) return true;
+    const bool tiled = lay->tile_width > 0;
+    if (lay->width <= 0 || lay->height <= 0 || !lay->strip_offsets || !lay->strip_bytes ||
+        (tiled && lay->tile_height <= 0) || (!tiled && lay->rows_per_strip <= 0) || (lay->planar != 1 && lay->planar != 2) ||
+        lay->components < 1 || (lay->bits != 8 && lay->bits != 16)) {
+        err = "layout: compressed strips / tiles need a geometry, strip_offsets and strip_bytes";
+        return false;
+    }
+    const int uh = tiled ? lay->tile_height : lay->rows_per_strip;  // rows per unit
+    const int planes = lay->planar == 2 ? lay->components : 1;
+    const int64_t across = tiled ? (lay->width + lay->tile_width - 1) / lay->tile_width : 1;
+    const int64_t urows = (lay->height + (int64_t)uh - 1) / uh;  // unit rows per plane
+    const int64_t per_plane = across * urows;
+    if (per_plane * planes > lay->nstrips) {
+        err = tiled ? "layout: too few tiles" : "layout: too few strips";
+        return false;
+    }
+    const int64_t u0 = std::max(0, row0) / uh;
+    const int64_t u1 = std::min<int64_t>(urows, ((int64_t)std::min(row1, lay->height) + uh - 1) / uh);
+    if (u1 <= u0) {
+        err = "layout: empty band";
+        return false;
+    }
+    const int R0 = (int)(u0 * uh), R1 = (int)std::min<int64_t>(lay->height, u1 * uh);
+    const uint64_t px = (uint64_t)(lay->planar == 2 ? 1 : lay->components) * (uint64_t)(lay->bits / 8);
+    const uint64_t unit = tiled ? (uint64_t)lay->tile_width * lay->tile_height * px : 0;
+    std::vector<uint64_t> voff, vcnt;
+    for (int p = 0; p < planes; p++)
+        for (int64_t u = u0; u < u1; u++)
+            for (int64_t x = 0; x < across; x++) {
+                const size_t i = (size_t)(p * per_plane + u * across + x);
+                const uint64_t o = lay->strip_offsets[i], n = lay->strip_bytes[i];
+                if (o > src_len || n > src_len - o || (lay->compression <= 1 && n < unit)) {
+                    err = "layout: strip / tile " + std::to_string(i) + " of the band lies outside the source buffer";
+                    return false;
+                }
+                voff.push_back(o);
+                vcnt.push_back(n);
+            }
+    jp2hip_layout v = *lay;
+    v.height = R1 - R0;
+    v.nstrips = (int32_t)voff.size();
+    v.strip_offsets = voff.data();
+    v.strip_bytes = vcnt.data();
+    jp2hip_layout vu;
+    std::vector<uint64_t> vuoffs;
+    const void *d2 = nullptr;
+    if (!ctx->gpu.unpack_strips(d_src, v, vu, vuoffs, &d2, err)) return false;
+    // the full-image view: unit row u of plane p at its decoded place
+    const uint64_t row_bytes = (uint64_t)lay->width * px;
+    ulay = vu;
+    ulay.height = lay->height;
+    ulay.rows_per_strip = uh;
+    ulay.nstrips = (int32_t)(urows * planes);
+    uoffs.assign((size_t)(urows * planes), 0);
+    for (int p = 0; p < planes; p++)
+        for (int64_t u = u0; u < u1; u++)
+            uoffs[(size_t)(p * urows + u)] = tiled ? vuoffs[(size_t)p] + (uint64_t)(u - u0) * uh * row_bytes
+                                                   : vuoffs[(size_t)(p * (u1 - u0) + (u - u0))];
+    ulay.strip_offsets = uoffs.data();
+    d_src = d2;
+    lay = &ulay;
+    return true;
+}
+
 // Kdu-Layer-Info byte counts: the code-stream through each layer.
 void layer_end_of(const jp2hip::Plan &P, int64_t tp_hdr_bytes, const int64_t *layer_bytes, int64_t *layer_end) {
     std::vector<uint8_t> mh;
@@ -562,18 +635,20 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     ctx->gpu.take_waits();
     Plan full;
     std::string err;
-    // every rank sees the same layout, so all of them stop here together
-    if (lay->compression > 1 || lay->tile_width > 0)
-        return fail("split: compressed or tiled TIFFs are not supported; rewrite as uncompressed strips first");
     if (!build_plan(full, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
     int tr0, tr1;
     split_tile_rows(full.nty, rc.tile_h, full.h, rc.flush_period, rank, world, tr0, tr1);
     Plan sub;
     make_subplan(full, tr0, tr1, sub);
     const bool have = sub.ntc > 0;
-    // only this rank's rows are read, so only their strips must be in d_src
-    // (a rank that fails here still joins every exchange below)
-    bool ok = !have || validate_layout(lay, src_len, sub.row0, sub.row0 + sub.band_h, err);
+    // only this rank's rows are read, so only their strips (or tiles) must be
+    // in d_src; compressed / tiled units of the band are decoded here (a rank
+    // that fails here still joins every exchange below)
+    jp2hip_layout ulay;
+    std::vector<uint64_t> uoffs;
+    const bool packed = lay->compression > 1 || lay->tile_width > 0;
+    bool ok = !have || (packed ? unpack_band(ctx, d_src, src_len, lay, sub.row0, sub.row0 + sub.band_h, ulay, uoffs, err)
+                               : validate_layout(lay, src_len, sub.row0, sub.row0 + sub.band_h, err));
     const bool prof = ctx->cfg.profile != 0;
     StageTimes st;
     std::vector<uint64_t> keys;

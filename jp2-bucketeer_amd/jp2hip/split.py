@@ -152,9 +152,12 @@ def band_strips(tif: bytes, layout: Layout, offsets, row0: int, row1: int):
     Returns (buffer, Layout, offsets) with offsets rebased to the buffer, so a
     rank uploads only its band of a multi-GB TIFF.  Offsets of strips outside
     the band are 0 and never read (kernels.hip k_ingest / dwt.hip band_load
-    touch only the rows of their band)."""
+    touch only the rows of their band).  Compressed strips and tiles are
+    packed whole, with their byte counts (the ``offsets`` array then holds
+    the offsets followed by the counts, as jp2hip.tiff_layout returns them);
+    the encoder decodes only the band's units (api.cpp unpack_band)."""
     if layout.compression > 1 or layout.tile_width > 0:
-        raise Jp2hipError("band-only upload needs uncompressed strips; upload the whole file")
+        return _band_units(tif, layout, offsets, row0, row1)
     rps, h, w = layout.rows_per_strip, layout.height, layout.width
     per_plane = (h + rps - 1) // rps
     planes = layout.components if layout.planar == 2 else 1
@@ -173,6 +176,34 @@ def band_strips(tif: bytes, layout: Layout, offsets, row0: int, row1: int):
     lay = Layout(layout.width, layout.height, layout.components, layout.bits, layout.planar,
                  layout.big_endian, layout.rows_per_strip, layout.nstrips,
                  ctypes.cast(new, POINTER(c_uint64)))
+    return b"".join(chunks), lay, new
+
+
+def _band_units(tif: bytes, layout: Layout, offsets, row0: int, row1: int):
+    """band_strips for compressed strips or tiles: every unit (strip, or tile
+    of a tile row) that rows [row0, row1) touch, with its byte count."""
+    tiled = layout.tile_width > 0
+    uh = layout.tile_height if tiled else layout.rows_per_strip
+    across = -(-layout.width // layout.tile_width) if tiled else 1
+    urows = -(-layout.height // uh)
+    per_plane = across * urows
+    planes = layout.components if layout.planar == 2 else 1
+    n = layout.nstrips
+    u0, u1 = row0 // uh, min(urows, -(-row1 // uh)) if row1 > row0 else row0 // uh
+    new = (c_uint64 * (2 * n))()
+    chunks, pos = [], 0
+    for p in range(planes):
+        for u in range(u0, u1):
+            for x in range(across):
+                idx = p * per_plane + u * across + x
+                o, nb = int(offsets[idx]), int(offsets[n + idx])
+                chunks.append(tif[o:o + nb])
+                new[idx], new[n + idx] = pos, nb
+                pos += nb
+    lay = Layout(layout.width, layout.height, layout.components, layout.bits, layout.planar,
+                 layout.big_endian, layout.rows_per_strip, n, ctypes.cast(new, POINTER(c_uint64)),
+                 layout.compression, layout.predictor, ctypes.cast(ctypes.byref(new, 8 * n), POINTER(c_uint64)),
+                 layout.tile_width, layout.tile_height)
     return b"".join(chunks), lay, new
 
 

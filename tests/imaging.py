@@ -377,8 +377,9 @@ def tiff_bytes_compressed(img: np.ndarray, compression: str, predictor: bool = F
     return data
 
 
-def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False) -> bytes:
-    """Uncompressed chunky BigTIFF (version 43, LONG8 strip offsets / counts)."""
+def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False, strip_codec=None, compression=1) -> bytes:
+    """Chunky BigTIFF (version 43, LONG8 strip offsets / counts); uncompressed,
+    or each strip passed through `strip_codec` (then tagged `compression`)."""
     if img.ndim == 2:
         img = img[..., None]
     h, w, nc = img.shape
@@ -388,6 +389,8 @@ def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False) -> bytes
     nst = (h + rps - 1) // rps
     strips = [np.ascontiguousarray(img[s * rps:(s + 1) * rps]) for s in range(nst)]
     strips = [b.astype(b.dtype.newbyteorder(e)).tobytes() for b in strips]
+    if strip_codec is not None:
+        strips = [strip_codec(x) for x in strips]
     ntags = 10
     ifd_off = 16
     arr_off = ifd_off + 8 + 20 * ntags + 8
@@ -403,7 +406,7 @@ def bigtiff_bytes(img: np.ndarray, rows_per_strip=64, big_endian=False) -> bytes
         raw = struct.pack(e + fmt * len(vals), *vals)
         return struct.pack(e + "HHQ", t, typ, cnt) + (raw + b"\0" * 8)[:8]
 
-    tags = [ent(256, 4, 1, [w]), ent(257, 4, 1, [h]), ent(258, 3, nc, [bits] * nc), ent(259, 3, 1, [1]),
+    tags = [ent(256, 4, 1, [w]), ent(257, 4, 1, [h]), ent(258, 3, nc, [bits] * nc), ent(259, 3, 1, [compression]),
             ent(262, 3, 1, [2 if nc >= 3 else 1]),
             ent(273, 16, nst, [offs[0]] if nst == 1 else [so_off]), ent(277, 3, 1, [nc]), ent(278, 4, 1, [rps]),
             ent(279, 16, nst, [len(strips[0])] if nst == 1 else [sbc_off]), ent(284, 3, 1, [1])]

@@ -181,6 +181,34 @@ def test_band_strips_rebases_offsets():
                 assert buf[boffs[i]:boffs[i] + n] == tif[offs[i]:offs[i] + n]
 
 
+def test_band_units_pack_compressed_strips_and_tiles():
+    """Compressed strips and tiles of a band are packed whole with their byte
+    counts (offsets, then counts, as tiff_layout returns them)."""
+    img = im.synth_rgb8(300, 170, seed=2)
+    for tif in (im.tiff_bytes(img, rows_per_strip=48, strip_codec=im.lzw_encode, compression=5),
+                im.tiff_bytes(img, rows_per_strip=7, planar=True, strip_codec=im.packbits_encode, compression=32773),
+                im.tiled_tiff_bytes(img, tile=(32, 48)),
+                im.tiled_tiff_bytes(img, tile=(32, 48), planar=True, deflate=True)):
+        lay, offs = jp2hip.tiff_layout(tif)
+        n = lay.nstrips
+        buf, blay, boffs = js.band_strips(tif, lay, offs, 128, 256)
+        assert blay.compression == lay.compression and blay.tile_width == lay.tile_width
+        uh = lay.tile_height if lay.tile_width else lay.rows_per_strip
+        across = -(-lay.width // lay.tile_width) if lay.tile_width else 1
+        per_plane = across * -(-lay.height // uh)
+        planes = 3 if lay.planar == 2 else 1
+        seen = 0
+        for p in range(planes):
+            for u in range(128 // uh, -(-256 // uh)):
+                for x in range(across):
+                    i = p * per_plane + u * across + x
+                    nb = offs[n + i]
+                    assert boffs[n + i] == nb and blay.strip_bytes[i] == nb
+                    assert buf[boffs[i]:boffs[i] + nb] == tif[offs[i]:offs[i] + nb]
+                    seen += nb
+        assert seen == len(buf)
+
+
 def test_exports_split_symbols():
     from jp2hip import _lib
     L = _lib.lib()
@@ -289,6 +317,46 @@ def test_split_band_only_upload(encoder):
     single, _ = encoder.encode_tiff(tif, jp2hip.LOSSY, rc)
     got, _ = _encode_world(tif, jp2hip.LOSSY, rc, 3, band_only=True)
     assert got == single
+
+
+def _packed_masters():
+    """(name, TIFF bytes, conversion) of compressed / tiled masters of one
+    1300x700 image: band boundaries (256-row tile rows) fall inside strips
+    and tiles (48-row units)."""
+    rgb = im.synth_rgb8(1300, 700, seed=21)
+    g16 = im.synth_u16(1300, 700, comps=1, seed=22)
+    return [
+        ("lzw48", im.tiff_bytes(rgb, rows_per_strip=48, strip_codec=im.lzw_encode, compression=5), rgb),
+        ("lzw_pred_pillow", im.tiff_bytes_compressed(rgb, "tiff_lzw", predictor=True, rows_per_strip=16), rgb),
+        ("deflate_pillow", im.tiff_bytes_compressed(rgb, "tiff_adobe_deflate", rows_per_strip=40), rgb),
+        ("packbits_planar", im.tiff_bytes(rgb, rows_per_strip=48, planar=True, strip_codec=im.packbits_encode,
+                                          compression=32773), rgb),
+        ("tiled", im.tiled_tiff_bytes(rgb, tile=(64, 48)), rgb),
+        ("tiled_deflate_planar", im.tiled_tiff_bytes(rgb, tile=(64, 48), planar=True, deflate=True), rgb),
+        ("bigtiff_lzw_gray16", im.bigtiff_bytes(g16, rows_per_strip=48, strip_codec=im.lzw_encode, compression=5),
+         g16),
+    ]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idx", range(7), ids=["lzw48", "lzw_pred_pillow", "deflate_pillow", "packbits_planar",
+                                               "tiled", "tiled_deflate_planar", "bigtiff_lzw_gray16"])
+def test_split_compressed_and_tiled_masters(encoder, idx):
+    """SURVEY.md 8(f) row 3 on the C5 route: LZW / Deflate / PackBits strips,
+    tiled TIFFs and an LZW BigTIFF split over 2 and 3 ranks -- each rank
+    decoding only its band's strips or tiles, from the whole file or from a
+    band-only upload -- concatenate to the single-GPU file of the same pixels
+    from an uncompressed TIFF."""
+    name, tif, img = _packed_masters()[idx]
+    lossless = idx % 2 == 1
+    conv = jp2hip.LOSSLESS if lossless else jp2hip.LOSSY
+    rc = jp2hip.recipe(conv, levels=6, tile_w=256, tile_h=256)
+    want, _ = encoder.encode_tiff(im.tiff_bytes(img), conv, rc)
+    single, _ = encoder.encode_tiff(tif, conv, rc)
+    assert single == want, name
+    for world, band_only in ((2, False), (3, True)):
+        got, _ = _encode_world(tif, conv, rc, world, band_only=band_only)
+        assert got == want, (name, world, band_only)
 
 
 @pytest.mark.gpu
