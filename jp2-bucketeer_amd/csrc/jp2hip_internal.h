@@ -17,7 +17,10 @@ constexpr int kMaxPasses = 96;    // 3*32-2 rounded up; per-block pass table str
 // margin (bins) kept below the predicted rate-target bin
 constexpr int kSlopeBins = 1024;
 constexpr int kSlopeBinBase = (1023 - 64) << 3;
-constexpr int kSkipMargin = 12;
+#ifndef JP2HIP_SKIP_MARGIN
+#define JP2HIP_SKIP_MARGIN 12
+#endif
+constexpr int kSkipMargin = JP2HIP_SKIP_MARGIN;
 // PCRD threshold selection (kernels.hip k_hull / k_select): hull segment bytes
 // histogrammed over 1/32-octave bins of the slope key (bits 47..62 of the
 // IEEE double, 2^-64 .. 2^64, clamped at both ends); the exact threshold is

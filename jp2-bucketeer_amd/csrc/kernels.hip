@@ -228,10 +228,30 @@ __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
 }
 
 // Deflate (RFC 1951) in a zlib wrapper (RFC 1950): TIFF compression 8
-// (Adobe Deflate) and 32946 (the older Deflate code), one lane per strip.
-// Canonical Huffman codes are kept as 16 per-length counts plus the symbols
-// in code order, and a code is decoded by walking the lengths (no lookup
-// table to build, so a block's tables cost ~1 KB of lane scratch).
+// (Adobe Deflate) and 32946 (the older Deflate code), one wave per strip.
+// A Huffman stream has no positions known before decoding it, so a strip is
+// one serial chain; the wave runs it with wave-uniform control flow (every
+// lane executes the same decode, the state in scalar registers) and uses its
+// lanes where the work is parallel:
+//   - the compressed bytes reach an LDS ring 1 KiB per vector load (16 bytes
+//     a lane), one chunk loaded ahead, so the bit reader never waits on HBM;
+//   - the code tables (counts, symbols in code order, 2^FB-entry direct
+//     lookup) are built by the lanes: ranks within a code length by ballot,
+//     lookup entries filled a symbol per lane;
+//   - a match is copied by the lanes at once (one byte each; an overlapping
+//     match, dist < 64, as its period-dist pattern);
+//   - the 32 KiB window leaves for HBM 4 KiB at a time in 16-byte stores.
+// kInfLanes is the wave width (the host build of tests/test_inflate_host.py
+// runs the same text with one lane).
+#ifndef JP2HIP_INF_LANES
+#define JP2HIP_INF_LANES 64
+#endif
+constexpr int kInfLanes = JP2HIP_INF_LANES;
+constexpr uint32_t kInChunkWords = 4 * kInfLanes;       // words per ring refill (16 bytes a lane)
+constexpr uint32_t kInRingWords = 2 * (kInChunkWords > 16 ? kInChunkWords : 16);  // >= two chunks
+constexpr uint32_t kInfWin = 32768, kInfWM = kInfWin - 1;
+constexpr int kInfLB = 12, kInfDB = 9;                  // direct-lookup bits: literal/length, distance
+
 __constant__ uint16_t kInfLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                          31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
 __constant__ uint8_t kInfLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
@@ -240,35 +260,87 @@ __constant__ uint16_t kInfDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    1
 __constant__ uint8_t kInfDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kInfClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// LSB-first bit reader over the strip's aligned 32-bit words: a queue of 8
-// words is loaded ahead of the 64-bit buffer, so each word's HBM latency is
-// hidden behind the decoding of the 28 bytes before it.  Words past the
-// stream read as zero (never loaded); `remaining` counts the real bits, and
-// consuming past them sets `bad`.
-struct InfBits {
-    const uint32_t *w;
-    uint64_t nw, k, remaining, buf;
+__device__ __forceinline__ uint32_t inf_uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t inf_uni64(uint64_t v) {
+    return ((uint64_t)inf_uni((uint32_t)(v >> 32)) << 32) | inf_uni((uint32_t)v);
+}
+
+struct InfShared {
+    uint32_t ring[kInRingWords];          // compressed stream words
+    uint8_t win[kInfWin];                 // sliding window = output staging
+    uint16_t lfast[1 << kInfLB], dfast[1 << kInfDB];
+    uint16_t lcnt[16], dcnt[16], lsym[288], dsym[32];
+    uint8_t lens[320];
+    uint16_t lbase[29], dbase[30];
+    uint8_t lextra[29], dextra[30];
+    uint32_t scr[64];                     // table-build scratch
+};
+
+// LSB-first bit reader over the strip's 16-byte-aligned words, fed from the
+// LDS ring.  Words past the stream read as zero (never loaded); `remaining`
+// counts the real bits, and consuming past them sets `bad`.
+struct InfIn {
+    const uint32_t *w;                 // aligned base of the stream
+    uint32_t nw;                       // words holding stream bytes
+    uint32_t k;                        // next word into buf
+    uint32_t loaded;                   // words written to the ring
+    uint4 pre;                         // this lane's 16 bytes of the chunk after them
+    uint64_t buf, remaining;
     int cnt;
-    uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
     bool bad;
-    __device__ __forceinline__ uint32_t ld(uint64_t i) const { return i < nw ? w[i] : 0u; }
-    __device__ __forceinline__ void init(const uint8_t *in, uint64_t n) {
-        const uint64_t addr = (uint64_t)(uintptr_t)in, head = addr & 3;
-        w = (const uint32_t *)(uintptr_t)(addr - head);  // aligned word: same page as a stream byte
-        nw = (head + n + 3) >> 2;
-        buf = (uint64_t)ld(0) >> (8 * head);
-        cnt = 32 - 8 * (int)head;
-        q0 = ld(1); q1 = ld(2); q2 = ld(3); q3 = ld(4); q4 = ld(5); q5 = ld(6); q6 = ld(7); q7 = ld(8);
-        k = 9;
+    uint32_t *ring;
+    int lane;
+    __device__ __forceinline__ uint4 chunk(uint32_t c) const {  // this lane's part of chunk c
+        const uint32_t w0 = c * kInChunkWords + 4u * (uint32_t)lane;
+        if (w0 + 4 <= nw) return *(const uint4 *)(w + w0);
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (w0 + 0 < nw) v.x = w[w0 + 0];
+        if (w0 + 1 < nw) v.y = w[w0 + 1];
+        if (w0 + 2 < nw) v.z = w[w0 + 2];
+        return v;
+    }
+    __device__ __forceinline__ void top_up() {  // the prefetched chunk into the ring, the next one in flight
+        const uint32_t c = loaded / kInChunkWords;
+        ((uint4 *)ring)[(c * kInfLanes + (uint32_t)lane) % (kInRingWords / 4)] = pre;
+        loaded += kInChunkWords;
+        pre = chunk(c + 1);
+    }
+    __device__ __forceinline__ void init(const uint8_t *in, uint64_t n, uint32_t *r, int ln) {
+        const uint64_t addr = (uint64_t)(uintptr_t)in, head = addr & 15;
+        w = (const uint32_t *)(uintptr_t)(addr - head);
+        nw = (uint32_t)((head + n + 3) >> 2);
+        ring = r;
+        lane = ln;
+        loaded = 0;
+        pre = chunk(0);
+        k = (uint32_t)(head >> 2);
+        ensure();
+        const uint32_t w0 = inf_uni(ring[head >> 2]);
+        buf = (uint64_t)w0 >> (8 * (head & 3));
+        cnt = 32 - 8 * (int)(head & 3);
+        k = (uint32_t)(head >> 2) + 1;
         remaining = n * 8;
         bad = false;
     }
+    // at least 8 words (256 bits) ahead of k in the ring: called once per
+    // symbol / code length / stored byte (each reads < 64 bits), so refill()
+    // itself never tops up (one top-up site, not one per bit-reader call)
+    __device__ __forceinline__ void ensure() {
+        while (k + 8 >= loaded) top_up();  // (once per 1 KiB on the GPU)
+        // the state is wave-uniform: say so, so the decode runs on the
+        // scalar unit with scalar branches (the compiler cannot prove it
+        // through the lane-dependent loads of top_up)
+        buf = inf_uni64(buf);
+        remaining = inf_uni64(remaining);
+        cnt = (int)inf_uni((uint32_t)cnt);
+        k = inf_uni(k);
+        loaded = inf_uni(loaded);
+    }
     __device__ __forceinline__ void refill() {
         if (cnt > 32) return;
-        buf |= (uint64_t)q0 << cnt;
+        buf |= (uint64_t)inf_uni(ring[k % kInRingWords]) << cnt;
         cnt += 32;
-        q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
-        q7 = ld(k++);
+        k++;
     }
     __device__ __forceinline__ uint32_t peek(int kb) { refill(); return (uint32_t)buf & ((1u << kb) - 1u); }
     __device__ __forceinline__ void drop(int kb) {
@@ -285,16 +357,14 @@ struct InfBits {
     __device__ __forceinline__ void align() { refill(); drop((int)(remaining & 7)); }  // to the next byte
 };
 
-// Canonical Huffman table: 16 per-length counts, the symbols in code order,
-// and a 2^FB-entry direct lookup ((len << 9) | sym) for codes of <= FB bits
-// (0: longer code, decoded by walking the lengths).
-__device__ int inf_walk(InfBits &b, const uint16_t *cnt, const uint16_t *sym) {
+// Canonical code of a length-walk (codes longer than the direct lookup)
+__device__ int inf_walk(InfIn &b, const uint16_t *cnt, const uint16_t *sym) {
     int code = 0, first = 0, index = 0;
     for (int len = 1; len <= 15; len++) {
         code |= (int)b.get(1);
         if (b.bad) return -1;
-        const int count = cnt[len];
-        if (code - count < first) return sym[index + (code - first)];
+        const int count = (int)inf_uni(cnt[len]);
+        if (code - count < first) return (int)inf_uni(sym[index + (code - first)]);
         index += count;
         first = (first + count) << 1;
         code <<= 1;
@@ -303,8 +373,8 @@ __device__ int inf_walk(InfBits &b, const uint16_t *cnt, const uint16_t *sym) {
 }
 
 template <int FB>
-__device__ __forceinline__ int inf_decode(InfBits &b, const uint16_t *fast, const uint16_t *cnt, const uint16_t *sym) {
-    const uint32_t e = fast[b.peek(FB)];
+__device__ __forceinline__ int inf_decode(InfIn &b, const uint16_t *fast, const uint16_t *cnt, const uint16_t *sym) {
+    const uint32_t e = inf_uni(fast[b.peek(FB)]);
     if (e) {
         b.drop((int)(e >> 9));
         return b.bad ? -1 : (int)(e & 511u);
@@ -312,74 +382,107 @@ __device__ __forceinline__ int inf_decode(InfBits &b, const uint16_t *fast, cons
     return inf_walk(b, cnt, sym);
 }
 
-// false: over-subscribed lengths (an incomplete code is accepted; its unused
-// codes fail in inf_walk)
+// Canonical Huffman table from n code lengths, built by the lanes: 16
+// per-length counts (LDS atomics), each length's first code and first symbol
+// slot (one uniform pass over the 15 lengths), every symbol's rank among the
+// lower-numbered symbols of its length (a ballot per length and chunk of
+// kInfLanes symbols), then the symbols in code order and the 2^FB-entry
+// direct lookup ((len << 9) | sym, 0: a longer code), a symbol per lane.
+// `scr`: 64 words of LDS.  false: over-subscribed lengths (an incomplete
+// code is accepted; its unused codes fail in inf_walk).
+__device__ __forceinline__ uint32_t inf_ballot_below(bool p, int lane, uint32_t &tot) {
+#if JP2HIP_INF_LANES > 1
+    const uint64_t m = __ballot(p);
+    tot = (uint32_t)__popcll(m);
+    return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+#else
+    tot = p ? 1u : 0u;
+    return 0u;
+#endif
+}
 template <int FB>
-__device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const uint8_t *len, int n) {
-    for (int l = 0; l < 16; l++) cnt[l] = 0;
-    for (int s = 0; s < n; s++) cnt[len[s]]++;
+__device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const uint8_t *len, int n, int lane,
+                          uint32_t *scr) {
+    uint32_t *cl = scr, *offs = scr + 16, *next = scr + 32, *seen = scr + 48;
+    for (int i = lane; i < 64; i += kInfLanes) scr[i] = 0u;
+    for (int i = lane; i < (1 << FB) / 8; i += kInfLanes) ((uint4 *)fast)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    for (int s = lane; s < n; s += kInfLanes)
+        if (len[s]) atomicAdd(&cl[len[s]], 1u);
+    __builtin_amdgcn_wave_barrier();
     int left = 1;
+    uint32_t code = 0, off = 0;
     for (int l = 1; l < 16; l++) {
-        left = (left << 1) - cnt[l];
-        if (left < 0) return false;
-    }
-    uint16_t offs[16], next[16];
-    offs[1] = 0;
-    for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
-    int code = 0;
-    next[0] = 0;
-    for (int l = 1; l < 16; l++) {
-        code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
-        next[l] = (uint16_t)code;
-    }
-    for (int i = 0; i < (1 << FB); i++) fast[i] = 0;
-    for (int s = 0; s < n; s++) {
-        const int l = len[s];
-        if (!l) continue;
-        sym[offs[l]++] = (uint16_t)s;
-        const uint32_t c = next[l]++;
-        if (l <= FB) {
-            const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);  // stream order: code MSB first
-            for (uint32_t i = r; i < (1u << FB); i += 1u << l) fast[i] = (uint16_t)((l << 9) | s);
+        const uint32_t c = inf_uni(cl[l]);
+        left = (left << 1) - (int)c;
+        if (lane == 0) {
+            offs[l] = off;
+            next[l] = code;
+            cnt[l] = (uint16_t)c;
         }
+        off += c;
+        code = (code + c) << 1;
+    }
+    if (lane == 0) cnt[0] = 0;
+    if (left < 0) return false;
+    __builtin_amdgcn_wave_barrier();
+    for (int s0 = 0; s0 < n; s0 += kInfLanes) {
+        const int s = s0 + lane;
+        const uint32_t l = s < n ? len[s] : 0u;
+        uint32_t rank = 0;
+        for (int q = 1; q < 16; q++) {
+            uint32_t tot;
+            const uint32_t below = inf_ballot_below(l == (uint32_t)q, lane, tot);
+            if (tot) {
+                if (l == (uint32_t)q) rank = seen[q] + below;
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) seen[q] += tot;
+            }
+        }
+        if (l) {
+            sym[offs[l] + rank] = (uint16_t)s;
+            if ((int)l <= FB) {
+                const uint32_t r = __builtin_bitreverse32(next[l] + rank) >> (32 - l);  // stream order: code MSB first
+                for (uint32_t i = r; i < (1u << FB); i += 1u << l) fast[i] = (uint16_t)((l << 9) | (uint32_t)s);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
     return true;
 }
 
-// One strip per single-lane workgroup (see k_unlzw); the code tables and the
-// 32 KB sliding window live in LDS, so matches copy from LDS, not from HBM,
-// and the output reaches HBM from the window in 16-byte stores every 4 KB
-// (per-byte global stores would make every input refill wait on them).
-__global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
-    constexpr int LB = 12, DB = 9;
-    constexpr uint32_t WM = 32767;
-    __shared__ uint16_t lcnt[16], lsym[288], dcnt[16], dsym[32], lfast[1 << LB], dfast[1 << DB];
-    __shared__ uint8_t lens[320];
-    __shared__ uint16_t lbase[29], dbase[30];
-    __shared__ uint8_t lextra[29], dextra[30];
-    __shared__ __attribute__((aligned(16))) uint8_t win[WM + 1];
-    const int s = blockIdx.x;
-    if (s >= a.nstrips || threadIdx.x) return;
-    for (int i = 0; i < 30; i++) {  // per-match lookups from LDS, not the constant bank
-        if (i < 29) { lbase[i] = kInfLenBase[i]; lextra[i] = kInfLenExtra[i]; }
-        dbase[i] = kInfDistBase[i];
-        dextra[i] = kInfDistExtra[i];
+__global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
+    __shared__ __attribute__((aligned(16))) InfShared S;
+    const int s = blockIdx.x, lane = (int)threadIdx.x;
+    if (s >= a.nstrips) return;
+    for (int i = lane; i < 30; i += kInfLanes) {  // per-match lookups from LDS, not the constant bank
+        if (i < 29) { S.lbase[i] = kInfLenBase[i]; S.lextra[i] = kInfLenExtra[i]; }
+        S.dbase[i] = kInfDistBase[i];
+        S.dextra[i] = kInfDistExtra[i];
     }
-    const uint8_t *in = a.src + a.off[s];
-    const uint64_t n = a.cnt[s], cap = strip_out_bytes(a, s);
+    // the strip's geometry as wave-uniform (scalar) values: everything the
+    // decode derives from them stays scalar, and its branches too
+    const uint8_t *in = a.src + inf_uni64(a.off[s]);
+    const uint64_t n = inf_uni64(a.cnt[s]), cap = inf_uni64(strip_out_bytes(a, s));
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
     uint64_t pos = 0, flushed = 0;
+    // window bytes [flushed, upto) to HBM: 16-byte stores from the lanes
+    // (upto a multiple of 16 except at the end of the strip)
     auto flush = [&](uint64_t upto) {
-        for (; flushed + 16 <= upto; flushed += 16)
-            *(uint4 *)(out + flushed) = *(const uint4 *)&win[(uint32_t)flushed & WM];
-        for (; flushed < upto; flushed++) out[flushed] = win[(uint32_t)flushed & WM];
+        const uint64_t whole = flushed + ((upto - flushed) & ~(uint64_t)15);
+        for (uint64_t o = flushed + 16u * (uint64_t)lane; o < whole; o += 16u * kInfLanes)
+            *(uint4 *)(out + o) = *(const uint4 *)&S.win[(uint32_t)o & kInfWM];
+        for (uint64_t o = whole + (uint64_t)lane; o < upto; o += kInfLanes) out[o] = S.win[(uint32_t)o & kInfWM];
+        flushed = upto;
     };
-    bool bad = n < 2 || (in[0] & 15) != 8 || (in[0] >> 4) > 7 || ((in[0] << 8) | in[1]) % 31 || (in[1] & 0x20);
-    InfBits b;
-    b.init(in, n);
+    const uint32_t h0 = inf_uni(n >= 1 ? in[0] : 0u), h1 = inf_uni(n >= 2 ? in[1] : 0u);
+    bool bad = n < 2 || (h0 & 15) != 8 || (h0 >> 4) > 7 || ((h0 << 8) | h1) % 31 || (h1 & 0x20);
+    InfIn b;
+    b.init(in, n, S.ring, lane);
     b.get(16);  // zlib CMF, FLG (checked above)
     bool last = false;
     while (!bad && !last) {
+        b.ensure();
         last = b.get(1);
         const int type = (int)b.get(2);
         if (b.bad) { bad = true; break; }
@@ -390,85 +493,111 @@ __global__ void __launch_bounds__(64) k_inflate(UnpackArgs a) {
             if (b.bad || len != (~nlen & 0xFFFFu)) { bad = true; break; }
             if (pos + len > cap) { len = (uint32_t)(cap - pos); last = true; }  // strip full: stop here
             for (uint32_t i = 0; i < len; i++) {
-                win[(uint32_t)pos & WM] = (uint8_t)b.get(8);
+                b.ensure();
+                const uint32_t v = b.get(8);
+                if (lane == 0) S.win[(uint32_t)pos & kInfWM] = (uint8_t)v;
                 if (++pos - flushed >= 4096) flush(flushed + 4096);
             }
             if (b.bad) { bad = true; break; }
             continue;
         }
         if (type == 1) {  // fixed codes
-            for (int i = 0; i < 288; i++) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-            for (int i = 0; i < 30; i++) lens[288 + i] = 5;
-            inf_build<LB>(lcnt, lsym, lfast, lens, 288);
-            inf_build<DB>(dcnt, dsym, dfast, lens + 288, 30);
+            for (int i = lane; i < 318; i += kInfLanes)
+                S.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
+            __builtin_amdgcn_wave_barrier();
+            inf_build<kInfLB>(S.lcnt, S.lsym, S.lfast, S.lens, 288, lane, S.scr);
+            inf_build<kInfDB>(S.dcnt, S.dsym, S.dfast, S.lens + 288, 30, lane, S.scr);
         } else if (type == 2) {  // dynamic codes
             const int nlen = (int)b.get(5) + 257, ndist = (int)b.get(5) + 1, ncode = (int)b.get(4) + 4;
             if (nlen > 286 || ndist > 30) { bad = true; break; }
-            for (int i = 0; i < 19; i++) lens[kInfClOrder[i]] = i < ncode ? (uint8_t)b.get(3) : 0;
-            if (b.bad || !inf_build<7>(lcnt, lsym, lfast, lens, 19)) { bad = true; break; }
+            b.ensure();
+            for (int i = 0; i < 19; i++) {
+                const uint32_t v = i < ncode ? b.get(3) : 0u;
+                if (lane == 0) S.lens[kInfClOrder[i]] = (uint8_t)v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (b.bad || !inf_build<7>(S.lcnt, S.lsym, S.lfast, S.lens, 19, lane, S.scr)) { bad = true; break; }
             int i = 0;
             while (i < nlen + ndist) {
-                const int sy = inf_decode<7>(b, lfast, lcnt, lsym);
+                b.ensure();
+                const int sy = inf_decode<7>(b, S.lfast, S.lcnt, S.lsym);
                 if (sy < 0 || b.bad) { bad = true; break; }
-                if (sy < 16) { lens[i++] = (uint8_t)sy; continue; }
-                uint8_t v = 0;
+                if (sy < 16) {
+                    if (lane == 0) S.lens[i] = (uint8_t)sy;
+                    i++;
+                    continue;
+                }
+                uint32_t v = 0;
                 int rep;
                 if (sy == 16) {
                     if (i == 0) { bad = true; break; }
-                    v = lens[i - 1];
+                    v = inf_uni(S.lens[i - 1]);
                     rep = 3 + (int)b.get(2);
                 } else if (sy == 17) rep = 3 + (int)b.get(3);
                 else rep = 11 + (int)b.get(7);
                 if (i + rep > nlen + ndist) { bad = true; break; }
-                while (rep--) lens[i++] = v;
+                for (int j = lane; j < rep; j += kInfLanes) S.lens[i + j] = (uint8_t)v;
+                i += rep;
             }
-            if (bad || b.bad || lens[256] == 0) { bad = true; break; }
-            if (!inf_build<LB>(lcnt, lsym, lfast, lens, nlen) || !inf_build<DB>(dcnt, dsym, dfast, lens + nlen, ndist)) {
+            __builtin_amdgcn_wave_barrier();
+            if (bad || b.bad || inf_uni(S.lens[256]) == 0) { bad = true; break; }
+            if (!inf_build<kInfLB>(S.lcnt, S.lsym, S.lfast, S.lens, nlen, lane, S.scr) ||
+                !inf_build<kInfDB>(S.dcnt, S.dsym, S.dfast, S.lens + nlen, ndist, lane, S.scr)) {
                 bad = true;
                 break;
             }
         } else { bad = true; break; }
         for (;;) {  // literal / length-distance symbols up to end-of-block
-            int sy = inf_decode<LB>(b, lfast, lcnt, lsym);
+            b.ensure();
+            pos = inf_uni64(pos);
+            flushed = inf_uni64(flushed);
+            int sy = inf_decode<kInfLB>(b, S.lfast, S.lcnt, S.lsym);
             if (sy < 0) { bad = true; break; }
             if (sy < 256) {
                 if (pos >= cap) { last = true; break; }  // strip full: trailing data ignored
-                win[(uint32_t)pos++ & WM] = (uint8_t)sy;
-                if (pos - flushed >= 4096) flush(flushed + 4096);
+                if (lane == 0) S.win[(uint32_t)pos & kInfWM] = (uint8_t)sy;
+                if (++pos - flushed >= 4096) flush(flushed + 4096);
                 continue;
             }
             if (sy == 256) break;
             sy -= 257;
             if (sy >= 29) { bad = true; break; }
-            const uint32_t len = lbase[sy] + b.get(lextra[sy]);
-            const int d = inf_decode<DB>(b, dfast, dcnt, dsym);
+            uint32_t len = inf_uni(S.lbase[sy]) + b.get((int)inf_uni(S.lextra[sy]));
+            const int d = inf_decode<kInfDB>(b, S.dfast, S.dcnt, S.dsym);
             if (d < 0 || d >= 30) { bad = true; break; }
-            const uint32_t dist = dbase[d] + b.get(dextra[d]);
+            const uint32_t dist = inf_uni(S.dbase[d]) + b.get((int)inf_uni(S.dextra[d]));
             if (b.bad || dist > pos) { bad = true; break; }
+            bool full = false;
             if (pos + len > cap) {  // the strip ends inside this match: keep what fits
-                for (uint32_t k = 0; pos + k < cap; k++) win[(uint32_t)(pos + k) & WM] = win[(uint32_t)(pos - dist + k) & WM];
-                pos = cap;
-                last = true;
-                break;
+                len = (uint32_t)(cap - pos);
+                full = true;
             }
-            const uint32_t src = (uint32_t)(pos - dist), dst = (uint32_t)pos;
-            uint32_t k = 0;
-            if (dist >= 8)  // 8 independent LDS reads, then the writes
-                for (; k + 8 <= len; k += 8) {
-                    uint8_t t[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) t[j] = win[(src + k + j) & WM];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) win[(dst + k + j) & WM] = t[j];
-                }
-            for (; k < len; k++) win[(dst + k) & WM] = win[(src + k) & WM];  // may overlap forward (dist < len)
+            const uint32_t p0 = (uint32_t)pos;
+            if (dist >= (uint32_t)kInfLanes) {
+                // rounds of kInfLanes bytes: a round reads only bytes before it
+                for (uint32_t o = 0; o < len; o += kInfLanes)
+                    if (o + (uint32_t)lane < len) {
+                        const uint32_t x = p0 + o + (uint32_t)lane;
+                        S.win[x & kInfWM] = S.win[(x - dist) & kInfWM];
+                    }
+            } else {
+                // overlapping: byte pos + x repeats byte pos - dist + (x mod dist),
+                // all of them already final
+                for (uint32_t o = 0; o < len; o += kInfLanes)
+                    if (o + (uint32_t)lane < len) {
+                        const uint32_t x = o + (uint32_t)lane;
+                        S.win[(p0 + x) & kInfWM] = S.win[(p0 - dist + x % dist) & kInfWM];
+                    }
+            }
+            __builtin_amdgcn_wave_barrier();
             pos += len;
             if (pos - flushed >= 4096) flush(flushed + 4096);
+            if (full) { last = true; break; }
         }
         if (b.bad) bad = true;
     }
     if (!bad) flush(pos);
-    if (bad || pos != cap) atomicOr(a.err, 2);
+    if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
 }
 
 // Predictor 2: each sample adds the same component of the pixel to its left
@@ -743,23 +872,32 @@ struct PredictArgs {
     uint8_t *pmin;
 };
 
-// Thread per (block, plane) slot; neighbouring blocks land in few bins, so
-// the workgroup sums into an LDS histogram first.
+// Thread per block, its planes in a loop (a thread per (block, plane) slot
+// left most lanes idle: 32 slots for ~12 planes); a workgroup covers
+// kHistBlocks consecutive blocks, whose planes land in few bins, so it sums
+// into an LDS histogram and flushes only the bins it touched.
+constexpr int kHistBlocks = 1024;
 __global__ void __launch_bounds__(256) k_plane_hist(PredictArgs a) {
     __shared__ unsigned long long lh[kSlopeBins];
     for (int i = threadIdx.x; i < kSlopeBins; i += 256) lh[i] = 0;
     __syncthreads();
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // block * 32 + plane
-    if (i < (size_t)a.nblocks * 32) {
-        const int b = (int)(i >> 5), p = (int)(i & 31);
-        // every load issues at once (a load under the p < P branch waited for P)
+    const int b0 = blockIdx.x * kHistBlocks;
+    const int b1 = min(a.nblocks, b0 + kHistBlocks);
+    for (int b = b0 + (int)threadIdx.x; b < b1; b += 256) {
         const int Pb = a.P[b];
-        const int64_t dd = a.dref[i] + a.dsig[i];
         const double wb = a.weight[b];
-        const uint32_t e = a.est[i];
-        if (p < Pb) {
+        const size_t i0 = (size_t)b * 32;
+        // the next plane's three loads in flight while this one is binned
+        int64_t dd = Pb > 0 ? a.dref[i0] + a.dsig[i0] : 0;
+        uint32_t e = Pb > 0 ? a.est[i0] : 0u;
+        for (int p = 0; p < Pb; p++) {
+            const int pn = min(p + 1, 31);
+            const int64_t ddn = a.dref[i0 + pn] + a.dsig[i0 + pn];
+            const uint32_t en = a.est[i0 + pn];
             const int k = plane_bin(dd, wb, e);
             if (k >= 0) atomicAdd(&lh[k], (unsigned long long)e);
+            dd = ddn;
+            e = en;
         }
     }
     __syncthreads();
@@ -1340,6 +1478,14 @@ __global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
 // --------------------------------------------------------------------------
 // Device pipeline
 // --------------------------------------------------------------------------
+// Stage-cost experiments (tests/tools/stage_cost2.sh) build with
+// -DJP2HIP_REPEAT_STAGE=<n> to launch one stage's kernels twice (they are
+// idempotent): 1 DWT, 2 quantiser, 3 MQ, 4 hull, 5 tier-2 sizing wave kernel.
+// Product builds never define it.
+#ifndef JP2HIP_REPEAT_STAGE
+#define JP2HIP_REPEAT_STAGE 0
+#endif
+#define REPEAT_IF(n) for (int rep_ = 0; rep_ < (JP2HIP_REPEAT_STAGE == (n) ? 2 : 1); rep_++)
 template <typename T>
 static bool ensure(DevBuf &b, size_t count, std::string &err) {
     size_t bytes = count * sizeof(T);
@@ -1503,7 +1649,7 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
             }
         }
         else if (lay.compression == 8 || lay.compression == 32946)
-            hipLaunchKernelGGL(k_inflate, dim3(ns), dim3(1), 0, stream, ua);
+            hipLaunchKernelGGL(k_inflate, dim3(ns), dim3(kInfLanes), 0, stream, ua);
         else hipLaunchKernelGGL(k_unpackbits, dim3(ns), dim3(64), 0, stream, ua);
         HIPCHECK(hipGetLastError());
         if (lay.predictor == 2) {  // per decoded row of a strip / of a tile
@@ -1670,7 +1816,9 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
         dl.coef = coef.ptr; dl.scratch0 = llbuf0.ptr; dl.scratch1 = llbuf1.ptr;
-        if (!launch_dwt(dl, stream)) {
+        bool dwt_ok = true;
+        REPEAT_IF(1) dwt_ok = dwt_ok && launch_dwt(dl, stream);
+        if (!dwt_ok) {
             err = std::string("DWT launch failed: ") + hipGetErrorString(hipGetLastError());
             return false;
         }
@@ -1727,8 +1875,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     const size_t qlds = (size_t)qa.max_mb * 64 * sizeof(uint64_t);
     if (nb) {
         const dim3 gq((nb + kQuantWaves - 1) / kQuantWaves), bq(64 * kQuantWaves);
-        if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, gq, bq, qlds * kQuantWaves, stream, qa);
-        else hipLaunchKernelGGL(k_quant<false>, gq, bq, qlds * kQuantWaves, stream, qa);
+        REPEAT_IF(2) {
+            if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, gq, bq, qlds * kQuantWaves, stream, qa);
+            else hipLaunchKernelGGL(k_quant<false>, gq, bq, qlds * kQuantWaves, stream, qa);
+        }
     }
     HIPCHECK(hipGetLastError());
     // S4b: slope prediction -> lowest coded plane per block, and the tier-1
@@ -1754,7 +1904,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         pa.hist = (unsigned long long *)hist.ptr;
         pa.kcut = (int *)kcut.ptr;
         pa.pmin = (uint8_t *)pmin.ptr;
-        hipLaunchKernelGGL(k_plane_hist, dim3((nb * 32 + 255) / 256), dim3(256), 0, stream, pa);
+        hipLaunchKernelGGL(k_plane_hist, dim3((nb + kHistBlocks - 1) / kHistBlocks), dim3(256), 0, stream, pa);
         HIPCHECK(hipGetLastError());
         if (reduce) {
             h_hist.resize(kSlopeBins);
@@ -1826,7 +1976,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         if (!ensure<int64_t>(dbgbuf, (size_t)nb * 6, err)) return false;
         ma.dbg = (int64_t *)dbgbuf.ptr;
     }
-    launch_t1_mq(ma, stream);
+    REPEAT_IF(3) launch_t1_mq(ma, stream);
 
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(ev[4], stream));
@@ -1843,7 +1993,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ha.hdist = (int64_t *)hdist.ptr;
     ha.hbytes = (unsigned long long *)pcrd_hb.ptr;
     ha.hcount = (uint32_t *)pcrd_hc.ptr;
-    if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + kHullThreads - 1) / kHullThreads), dim3(kHullThreads), 0, stream, ha);
+    REPEAT_IF(4) if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + kHullThreads - 1) / kHullThreads), dim3(kHullThreads), 0, stream, ha);
     HIPCHECK(hipGetLastError());
     // candidate lists: room for every hull segment (the bound sum(3 Mb - 2))
     int64_t nseg_bound = 0;

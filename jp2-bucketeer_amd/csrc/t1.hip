@@ -44,11 +44,8 @@ constexpr uint8_t kPadDecision = CX_PAD << 1;
 // at most w*h coding decisions + w*h sign decisions + 3 per run-length column
 // (each pass is padded to a 16-byte boundary; the MQ kernel prefetches one
 // 16-byte chunk past the end of a pass)
-#ifndef JP2HIP_STREAM_CAP_MUL
-#define JP2HIP_STREAM_CAP_MUL 1  // experiment builds only: slot footprint x N
-#endif
 __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
-    return (((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u) * JP2HIP_STREAM_CAP_MUL;
+    return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
 }
 
 constexpr int kCmWaves = 4;  // items per workgroup

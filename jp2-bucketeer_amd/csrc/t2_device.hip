@@ -534,16 +534,24 @@ __device__ __forceinline__ void tpart_size(const T2Args &a, int t) {
     const TpDesc d = a.tps[t];
     const size_t p0 = (size_t)d.prec0 * a.L, p1 = (size_t)(d.prec0 + d.nprec) * a.L;
     uint64_t body = 0, plt = 0, seg = 0;
-    for (size_t i = p0; i < p1; i++) {
-        const uint32_t len = a.pk_len[i];
-        body += len;
-        if (a.plt) {
-            const uint64_t k = (uint64_t)varint_len(len);
-            if (i == p0 || seg + k > 65532) {
-                if (i != p0) plt += 5 + seg;
-                seg = 0;
+    for (size_t i0 = p0; i0 < p1; i0 += 8) {  // 8 lengths' loads in flight at a time
+        uint32_t l8[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) l8[j] = a.pk_len[min(i0 + j, p1 - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const size_t i = i0 + j;
+            if (i >= p1) break;
+            const uint32_t len = l8[j];
+            body += len;
+            if (a.plt) {
+                const uint64_t k = (uint64_t)varint_len(len);
+                if (i == p0 || seg + k > 65532) {
+                    if (i != p0) plt += 5 + seg;
+                    seg = 0;
+                }
+                seg += k;
             }
-            seg += k;
         }
     }
     if (a.plt && p1 > p0) plt += 5 + seg;
@@ -551,67 +559,55 @@ __device__ __forceinline__ void tpart_size(const T2Args &a, int t) {
     a.tp_len[t] = (uint32_t)(14 + plt + body);
 }
 
-__global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
-                                                  const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
-                                                  const uint64_t *kc, const unsigned long long *acc, T2Summary *sum,
-                                                  RateStepArgs rate) {
-    __shared__ uint64_t part[256];
-    __shared__ int64_t lay[256][kMaxLayers > 8 ? 8 : kMaxLayers];
+// One workgroup of kTotThreads: tile-part sizes (a thread per tile-part, or
+// a contiguous run of them), their offsets by a workgroup scan, and every sum
+// the host needs as per-thread partials reduced through one LDS table (a wave
+// sum each, then the waves' partials): no thread walks a serial loop over
+// the others' results.
+constexpr int kTotThreads = 1024, kTotWaves = kTotThreads / 64;
+constexpr int kTotSums = kMaxLayers + 5;  // layers, tp headers, t1 bytes, passes, decisions, skipped
+__global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
+                                                          const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
+                                                          const uint64_t *kc, const unsigned long long *acc,
+                                                          T2Summary *sum, RateStepArgs rate) {
+    __shared__ uint64_t wsum[kTotWaves + 1];
+    __shared__ int64_t red[kTotWaves][kTotSums];
     if (a.halt && *a.halt) return;  // the whole workgroup
-    const int tid = threadIdx.x;
-    const int chunk = (a.ntp + 255) / 256;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int L = a.L;
+    const int chunk = (a.ntp + kTotThreads - 1) / kTotThreads;
     const int t0 = min(a.ntp, tid * chunk), t1 = min(a.ntp, t0 + chunk);
     for (int t = t0; t < t1; t++) tpart_size(a, t);
     uint64_t s = 0, hdr = 0;
     for (int t = t0; t < t1; t++) s += a.tp_len[t];
-    part[tid] = s;
-    __syncthreads();
-    if (tid == 0) {  // exclusive scan of the 256 chunk sums
-        uint64_t acc = 0;
-        for (int i = 0; i < 256; i++) {
-            const uint64_t v = part[i];
-            part[i] = acc;
-            acc += v;
-        }
-        sum->part_bytes = (int64_t)acc;
-    }
-    __syncthreads();
-    uint64_t o = part[tid];
+    uint64_t tot;
+    uint64_t o = wg_excl_scan64<kTotThreads>(s, wsum, tot);
+    if (tid == 0) sum->part_bytes = (int64_t)tot;
     for (int t = t0; t < t1; t++) {
         a.tp_off[t] = o;
         o += a.tp_len[t];
         hdr += a.tp_hdr[t];
     }
-    // per-layer packet bytes (layers in groups of 8 through shared memory)
-    for (int l0 = 0; l0 < a.L; l0 += 8) {
-        int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        // precinct-major: a thread's 8 layer loads at clamped indices, issued together
-        for (int pq = tid; pq < a.nprec; pq += 256) {
-            uint32_t x[8];
+    // per-layer packet bytes: precinct-major, a precinct's L lengths per thread
+    int64_t lay[kMaxLayers];
 #pragma unroll
-            for (int k = 0; k < 8; k++) x[k] = a.pk_len[(size_t)pq * a.L + min(l0 + k, a.L - 1)];
+    for (int l = 0; l < kMaxLayers; l++) lay[l] = 0;
+    for (int pq = tid; pq < a.nprec; pq += kTotThreads) {
+        const uint32_t *pl = a.pk_len + (size_t)pq * L;
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] += l0 + k < a.L ? x[k] : 0u;
-        }
-        for (int k = 0; k < 8; k++) lay[tid][k] = v[k];
-        __syncthreads();
-        if (tid < 8 && l0 + tid < a.L) {
-            int64_t acc = 0;
-            for (int i = 0; i < 256; i++) acc += lay[i][tid];
-            sum->layer_bytes[l0 + tid] = acc;
-        }
-        __syncthreads();
+        for (int l = 0; l < kMaxLayers; l++)
+            if (l < L) lay[l] += pl[l];
     }
-    // tier-1 totals (acc: decisions per block in the low 40 bits, k_t1_cm3)
-    int64_t tb = 0, tp = 0, nd = 0;
-    int skipped = 0;
-    for (int b0 = 0; b0 < nblocks; b0 += 4 * 256) {  // 4 blocks' loads in flight per thread
+    // tier-1 totals (acc: decisions per block in the low 40 bits, k_t1_cm3),
+    // 4 blocks' loads in flight per thread
+    int64_t tb = 0, tp = 0, nd = 0, skipped = 0;
+    for (int b0 = 0; b0 < nblocks; b0 += 4 * kTotThreads) {
         int32_t ln[4];
         uint32_t np[4], pm[4];
         unsigned long long kk[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int b = min(b0 + u * 256 + tid, nblocks - 1);
+            const int b = min(b0 + u * kTotThreads + tid, nblocks - 1);
             ln[u] = lengths[b];
             np[u] = npasses[b];
             kk[u] = acc[b];
@@ -619,45 +615,43 @@ __global__ void __launch_bounds__(256) k_t2_total(T2Args a, int nblocks, const i
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)
-            if (b0 + u * 256 + tid < nblocks) {
+            if (b0 + u * kTotThreads + tid < nblocks) {
                 tb += ln[u];
                 tp += np[u];
                 nd += (int64_t)(kk[u] & ((1ull << 40) - 1ull));
                 skipped |= pm[u] > 0;
             }
     }
-    lay[tid][1] = nd;
-    part[tid] = (uint64_t)tb;
+    // reductions: wave sums, then thread j < kTotSums adds the waves' partials of sum j
+    auto wave_put = [&](int j, int64_t v) {
+        v = wave_sum64(v);
+        if (lane == 0) red[wv][j] = v;
+    };
+#pragma unroll
+    for (int l = 0; l < kMaxLayers; l++)
+        if (l < L) wave_put(l, lay[l]);
+    wave_put(kMaxLayers + 0, (int64_t)hdr);
+    wave_put(kMaxLayers + 1, tb);
+    wave_put(kMaxLayers + 2, tp);
+    wave_put(kMaxLayers + 3, nd);
+    wave_put(kMaxLayers + 4, skipped);
     __syncthreads();
-    if (tid == 0) {
-        uint64_t acc = 0;
-        for (int i = 0; i < 256; i++) acc += part[i];
-        sum->t1_bytes = (int64_t)acc;
+    if (tid < kTotSums && (tid >= kMaxLayers || tid < L)) {
+        int64_t v = 0;
+#pragma unroll
+        for (int w = 0; w < kTotWaves; w++) v += red[w][tid];
+        if (tid < kMaxLayers) sum->layer_bytes[tid] = v;
+        else if (tid == kMaxLayers + 0) sum->tp_hdr_bytes = v;
+        else if (tid == kMaxLayers + 1) sum->t1_bytes = v;
+        else if (tid == kMaxLayers + 2) sum->coded_passes = v;
+        else if (tid == kMaxLayers + 3) sum->decisions = v;
+        else sum->skipped = v != 0;
     }
-    __syncthreads();
-    part[tid] = (uint64_t)tp | ((uint64_t)skipped << 63);
-    lay[tid][0] = (int64_t)hdr;
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t acc = 0;
-        int64_t h = 0, dsum = 0;
-        int sk = 0;
-        for (int i = 0; i < 256; i++) {
-            acc += part[i] & ~(1ull << 63);
-            sk |= (int)(part[i] >> 63);
-            h += lay[i][0];
-            dsum += lay[i][1];
-        }
-        sum->decisions = dsum;
-        sum->coded_passes = (int64_t)acc;
-        sum->skipped = sk;
-        sum->tp_hdr_bytes = h;
-        sum->err = *t1err;
-        for (int l = 0; l < a.L; l++) sum->kc[l] = kc ? kc[l] : 0ull;
-    }
+    if (tid < L) sum->kc[tid] = kc ? kc[tid] : 0ull;
+    if (tid == 0) sum->err = *t1err;
     if (rate.rs) {
-        __syncthreads();  // (the per-layer sums come from threads 0..7)
-        if (tid == 0) rate_step(rate.rs, sum, a.L, rate.budget, rate.out_rs, rate.out_sum);
+        __syncthreads();  // every field of *sum written
+        if (tid == 0) rate_step(rate.rs, sum, L, rate.budget, rate.out_rs, rate.out_sum);
     }
 }
 
@@ -824,12 +818,16 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt,
     ra.budget = (int64_t *)budget.ptr;
     ra.out_rs = out_rs;
     ra.out_sum = out_rs ? (T2Summary *)(out_rs + 1) : nullptr;
+#ifndef JP2HIP_REPEAT_STAGE
+#define JP2HIP_REPEAT_STAGE 0  // stage-cost experiments only (kernels.hip)
+#endif
+    for (int rep_ = 0; rep_ < (JP2HIP_REPEAT_STAGE == 5 ? 2 : 1); rep_++)
     if (t2_nprec && t2_wave)
         hipLaunchKernelGGL(k_t2_wave<false>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
                            stream, a);
     else if (t2_nprec)
         hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
-    hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(256), 0, stream, a, nb, (const int32_t *)lengths.ptr,
+    hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(kTotThreads), 0, stream, a, nb, (const int32_t *)lengths.ptr,
                        (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
                        with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
                        (const unsigned long long *)ordkey.ptr, (T2Summary *)t2sum.ptr, ra);

@@ -16,9 +16,14 @@
 #define __launch_bounds__(x)
 #define __shared__ static
 #define __constant__ static const
+#define JP2HIP_INF_LANES 1
+#define __builtin_amdgcn_readfirstlane(x) (x)
+#define __builtin_amdgcn_wave_barrier() ((void)0)
 struct uint4 { uint32_t x, y, z, w; };
+static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 static struct { int x; } blockIdx, threadIdx;
 static inline int atomicOr(int *p, int v) { int o = *p; *p |= v; return o; }
+static inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
 using std::min;
 // [[MAIN]]
 using namespace jp2hip;

@@ -1,4 +1,4 @@
-"""k_inflate (kernels.hip) compiled for the host and run under AddressSanitizer:
+"""k_inflate (kernels.hip) compiled for the host -- a one-lane wave -- and run under AddressSanitizer:
 zlib streams of every level at every byte alignment decode exactly, and
 truncated or reserved-block streams report a corrupt strip.  The GPU tests
 (test_gpu_parity.py) run the same kernel on the device; this one runs on CPU."""
@@ -18,7 +18,7 @@ def _kernel_text():
     h = open(HDR).read()
     ua = h[h.index("struct UnpackArgs {"):h.index("// LZW strips, segment-parallel")]
     s = open(SRC).read()
-    inf = s[s.index("__constant__ uint16_t kInfLenBase"):s.index("// Predictor 2: each sample adds")]
+    inf = s[s.index("#ifndef JP2HIP_INF_LANES"):s.index("// Predictor 2: each sample adds")]
     return "namespace jp2hip {\n" + ua + inf + "}\n"
 
 
