@@ -17,10 +17,7 @@ constexpr int kMaxPasses = 96;    // 3*32-2 rounded up; per-block pass table str
 // margin (bins) kept below the predicted rate-target bin
 constexpr int kSlopeBins = 1024;
 constexpr int kSlopeBinBase = (1023 - 64) << 3;
-#ifndef JP2HIP_SKIP_MARGIN
-#define JP2HIP_SKIP_MARGIN 12
-#endif
-constexpr int kSkipMargin = JP2HIP_SKIP_MARGIN;
+constexpr int kSkipMargin = 12;
 // PCRD threshold selection (kernels.hip k_hull / k_select): hull segment bytes
 // histogrammed over 1/32-octave bins of the slope key (bits 47..62 of the
 // IEEE double, 2^-64 .. 2^64, clamped at both ends); the exact threshold is
@@ -143,6 +140,7 @@ struct T2Tables {
     std::vector<TpDesc> tp;   // code-stream order
     int64_t tt_nodes = 0;
     int max_prec_blocks = 0;  // code-blocks of the largest precinct
+    int max_prec_nodes = 0;   // tag-tree nodes of the largest precinct
 };
 // Tables for tiles [tile0, tile1) of `P` (blocks rebased by -block0: a
 // tile-split rank's blocks are its sub-plan's).

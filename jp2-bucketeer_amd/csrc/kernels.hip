@@ -277,17 +277,19 @@ struct InfShared {
 };
 
 // LSB-first bit reader over the strip's 16-byte-aligned words, fed from the
-// LDS ring.  Words past the stream read as zero (never loaded); `remaining`
-// counts the real bits, and consuming past them sets `bad`.
+// LDS ring.  Words past the stream read as zero (never loaded): decoding runs
+// on to the end of the strip's output or of the block, and a stream that was
+// read past its end (consumed() > 8 n) is reported corrupt at the end -- no
+// per-read bookkeeping on the hot path.
 struct InfIn {
     const uint32_t *w;                 // aligned base of the stream
     uint32_t nw;                       // words holding stream bytes
     uint32_t k;                        // next word into buf
     uint32_t loaded;                   // words written to the ring
+    uint32_t head_bits;                // bits before the stream in word 0
     uint4 pre;                         // this lane's 16 bytes of the chunk after them
-    uint64_t buf, remaining;
+    uint64_t buf;
     int cnt;
-    bool bad;
     uint32_t *ring;
     int lane;
     __device__ __forceinline__ uint4 chunk(uint32_t c) const {  // this lane's part of chunk c
@@ -305,6 +307,20 @@ struct InfIn {
         loaded += kInChunkWords;
         pre = chunk(c + 1);
     }
+    // at least 8 words (256 bits) ahead of k in the ring: called once per
+    // symbol / code length / stored byte (each reads < 64 bits), so refill()
+    // itself never tops up (one top-up site, not one per bit-reader call)
+    __device__ __forceinline__ void ensure() {
+        if (k + 8 >= loaded) {
+            do top_up(); while (k + 8 >= loaded);  // (once per 1 KiB on the GPU)
+            // the state is wave-uniform: say so after the lane-dependent
+            // loads, so the decode keeps running on the scalar unit
+            buf = inf_uni64(buf);
+            cnt = (int)inf_uni((uint32_t)cnt);
+            k = inf_uni(k);
+            loaded = inf_uni(loaded);
+        }
+    }
     __device__ __forceinline__ void init(const uint8_t *in, uint64_t n, uint32_t *r, int ln) {
         const uint64_t addr = (uint64_t)(uintptr_t)in, head = addr & 15;
         w = (const uint32_t *)(uintptr_t)(addr - head);
@@ -319,23 +335,9 @@ struct InfIn {
         buf = (uint64_t)w0 >> (8 * (head & 3));
         cnt = 32 - 8 * (int)(head & 3);
         k = (uint32_t)(head >> 2) + 1;
-        remaining = n * 8;
-        bad = false;
+        head_bits = (uint32_t)(8 * head);
     }
-    // at least 8 words (256 bits) ahead of k in the ring: called once per
-    // symbol / code length / stored byte (each reads < 64 bits), so refill()
-    // itself never tops up (one top-up site, not one per bit-reader call)
-    __device__ __forceinline__ void ensure() {
-        while (k + 8 >= loaded) top_up();  // (once per 1 KiB on the GPU)
-        // the state is wave-uniform: say so, so the decode runs on the
-        // scalar unit with scalar branches (the compiler cannot prove it
-        // through the lane-dependent loads of top_up)
-        buf = inf_uni64(buf);
-        remaining = inf_uni64(remaining);
-        cnt = (int)inf_uni((uint32_t)cnt);
-        k = inf_uni(k);
-        loaded = inf_uni(loaded);
-    }
+    __device__ __forceinline__ uint64_t consumed() const { return (uint64_t)k * 32 - (uint64_t)cnt - head_bits; }
     __device__ __forceinline__ void refill() {
         if (cnt > 32) return;
         buf |= (uint64_t)inf_uni(ring[k % kInRingWords]) << cnt;
@@ -344,8 +346,6 @@ struct InfIn {
     }
     __device__ __forceinline__ uint32_t peek(int kb) { refill(); return (uint32_t)buf & ((1u << kb) - 1u); }
     __device__ __forceinline__ void drop(int kb) {
-        if (remaining < (uint64_t)kb) { bad = true; remaining = 0; }
-        else remaining -= kb;
         buf >>= kb;
         cnt -= kb;
     }
@@ -354,7 +354,7 @@ struct InfIn {
         drop(kb);
         return v;
     }
-    __device__ __forceinline__ void align() { refill(); drop((int)(remaining & 7)); }  // to the next byte
+    __device__ __forceinline__ void align() { refill(); drop((int)((0u - (uint32_t)consumed()) & 7u)); }  // to the next byte
 };
 
 // Canonical code of a length-walk (codes longer than the direct lookup)
@@ -362,7 +362,6 @@ __device__ int inf_walk(InfIn &b, const uint16_t *cnt, const uint16_t *sym) {
     int code = 0, first = 0, index = 0;
     for (int len = 1; len <= 15; len++) {
         code |= (int)b.get(1);
-        if (b.bad) return -1;
         const int count = (int)inf_uni(cnt[len]);
         if (code - count < first) return (int)inf_uni(sym[index + (code - first)]);
         index += count;
@@ -377,7 +376,7 @@ __device__ __forceinline__ int inf_decode(InfIn &b, const uint16_t *fast, const 
     const uint32_t e = inf_uni(fast[b.peek(FB)]);
     if (e) {
         b.drop((int)(e >> 9));
-        return b.bad ? -1 : (int)(e & 511u);
+        return (int)(e & 511u);
     }
     return inf_walk(b, cnt, sym);
 }
@@ -463,16 +462,22 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
     // the strip's geometry as wave-uniform (scalar) values: everything the
     // decode derives from them stays scalar, and its branches too
     const uint8_t *in = a.src + inf_uni64(a.off[s]);
-    const uint64_t n = inf_uni64(a.cnt[s]), cap = inf_uni64(strip_out_bytes(a, s));
+    const uint64_t n = inf_uni64(a.cnt[s]);
+    const uint64_t cap64 = inf_uni64(strip_out_bytes(a, s));
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
-    uint64_t pos = 0, flushed = 0;
+    if (cap64 >= (1ull << 32)) {  // a strip / tile of 4 GiB or more: not a TIFF the host parser accepts
+        if (lane == 0) atomicOr(a.err, 2);
+        return;
+    }
+    const uint32_t cap = (uint32_t)cap64;
+    uint32_t pos = 0, flushed = 0;
     // window bytes [flushed, upto) to HBM: 16-byte stores from the lanes
     // (upto a multiple of 16 except at the end of the strip)
-    auto flush = [&](uint64_t upto) {
-        const uint64_t whole = flushed + ((upto - flushed) & ~(uint64_t)15);
-        for (uint64_t o = flushed + 16u * (uint64_t)lane; o < whole; o += 16u * kInfLanes)
-            *(uint4 *)(out + o) = *(const uint4 *)&S.win[(uint32_t)o & kInfWM];
-        for (uint64_t o = whole + (uint64_t)lane; o < upto; o += kInfLanes) out[o] = S.win[(uint32_t)o & kInfWM];
+    auto flush = [&](uint32_t upto) {
+        const uint32_t whole = flushed + ((upto - flushed) & ~15u);
+        for (uint32_t o = flushed + 16u * (uint32_t)lane; o < whole; o += 16u * kInfLanes)
+            *(uint4 *)(out + o) = *(const uint4 *)&S.win[o & kInfWM];
+        for (uint32_t o = whole + (uint32_t)lane; o < upto; o += kInfLanes) out[o] = S.win[o & kInfWM];
         flushed = upto;
     };
     const uint32_t h0 = inf_uni(n >= 1 ? in[0] : 0u), h1 = inf_uni(n >= 2 ? in[1] : 0u);
@@ -485,20 +490,18 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
         b.ensure();
         last = b.get(1);
         const int type = (int)b.get(2);
-        if (b.bad) { bad = true; break; }
         if (type == 0) {  // stored: to the byte boundary, LEN, ~LEN, bytes
             b.align();
             uint32_t len = b.get(16);
             const uint32_t nlen = b.get(16);
-            if (b.bad || len != (~nlen & 0xFFFFu)) { bad = true; break; }
-            if (pos + len > cap) { len = (uint32_t)(cap - pos); last = true; }  // strip full: stop here
+            if (len != (~nlen & 0xFFFFu)) { bad = true; break; }
+            if (len > cap - pos) { len = cap - pos; last = true; }  // strip full: stop here
             for (uint32_t i = 0; i < len; i++) {
                 b.ensure();
                 const uint32_t v = b.get(8);
-                if (lane == 0) S.win[(uint32_t)pos & kInfWM] = (uint8_t)v;
+                if (lane == 0) S.win[pos & kInfWM] = (uint8_t)v;
                 if (++pos - flushed >= 4096) flush(flushed + 4096);
             }
-            if (b.bad) { bad = true; break; }
             continue;
         }
         if (type == 1) {  // fixed codes
@@ -516,12 +519,12 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
                 if (lane == 0) S.lens[kInfClOrder[i]] = (uint8_t)v;
             }
             __builtin_amdgcn_wave_barrier();
-            if (b.bad || !inf_build<7>(S.lcnt, S.lsym, S.lfast, S.lens, 19, lane, S.scr)) { bad = true; break; }
+            if (!inf_build<7>(S.lcnt, S.lsym, S.lfast, S.lens, 19, lane, S.scr)) { bad = true; break; }
             int i = 0;
             while (i < nlen + ndist) {
                 b.ensure();
                 const int sy = inf_decode<7>(b, S.lfast, S.lcnt, S.lsym);
-                if (sy < 0 || b.bad) { bad = true; break; }
+                if (sy < 0) { bad = true; break; }
                 if (sy < 16) {
                     if (lane == 0) S.lens[i] = (uint8_t)sy;
                     i++;
@@ -540,7 +543,7 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
                 i += rep;
             }
             __builtin_amdgcn_wave_barrier();
-            if (bad || b.bad || inf_uni(S.lens[256]) == 0) { bad = true; break; }
+            if (bad || inf_uni(S.lens[256]) == 0) { bad = true; break; }
             if (!inf_build<kInfLB>(S.lcnt, S.lsym, S.lfast, S.lens, nlen, lane, S.scr) ||
                 !inf_build<kInfDB>(S.dcnt, S.dsym, S.dfast, S.lens + nlen, ndist, lane, S.scr)) {
                 bad = true;
@@ -549,13 +552,11 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
         } else { bad = true; break; }
         for (;;) {  // literal / length-distance symbols up to end-of-block
             b.ensure();
-            pos = inf_uni64(pos);
-            flushed = inf_uni64(flushed);
             int sy = inf_decode<kInfLB>(b, S.lfast, S.lcnt, S.lsym);
-            if (sy < 0) { bad = true; break; }
             if (sy < 256) {
+                if (sy < 0) { bad = true; break; }
                 if (pos >= cap) { last = true; break; }  // strip full: trailing data ignored
-                if (lane == 0) S.win[(uint32_t)pos & kInfWM] = (uint8_t)sy;
+                if (lane == 0) S.win[pos & kInfWM] = (uint8_t)sy;
                 if (++pos - flushed >= 4096) flush(flushed + 4096);
                 continue;
             }
@@ -566,13 +567,13 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
             const int d = inf_decode<kInfDB>(b, S.dfast, S.dcnt, S.dsym);
             if (d < 0 || d >= 30) { bad = true; break; }
             const uint32_t dist = inf_uni(S.dbase[d]) + b.get((int)inf_uni(S.dextra[d]));
-            if (b.bad || dist > pos) { bad = true; break; }
+            if (dist > pos) { bad = true; break; }
             bool full = false;
-            if (pos + len > cap) {  // the strip ends inside this match: keep what fits
-                len = (uint32_t)(cap - pos);
+            if (len > cap - pos) {  // the strip ends inside this match: keep what fits
+                len = cap - pos;
                 full = true;
             }
-            const uint32_t p0 = (uint32_t)pos;
+            const uint32_t p0 = pos;
             if (dist >= (uint32_t)kInfLanes) {
                 // rounds of kInfLanes bytes: a round reads only bytes before it
                 for (uint32_t o = 0; o < len; o += kInfLanes)
@@ -594,8 +595,8 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
             if (pos - flushed >= 4096) flush(flushed + 4096);
             if (full) { last = true; break; }
         }
-        if (b.bad) bad = true;
     }
+    bad = bad || b.consumed() > 8 * n;  // read past the end of the stream: truncated
     if (!bad) flush(pos);
     if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
 }

@@ -151,16 +151,19 @@ __device__ __forceinline__ void tree_encode(uint32_t *nd, int w, int h, int leaf
         bool known = (e >> 16) & 1u;
         if (low > nlow) nlow = low;
         else low = nlow;
-        while (low < threshold) {
-            if (low >= value) {
-                if (!known) {
-                    bw.bit(1);
-                    known = true;
-                }
-                break;
-            }
-            bw.bit(0);
-            low++;
+        // B.10.2 walk, as one field: a 0 per step of `low` up to
+        // min(value, threshold), then a 1 if the value is reached below the
+        // threshold and not yet known
+        const int nz = max(0, min(value, threshold) - low);
+        low += nz;
+        const bool one = low < threshold && !known;
+        if (one) known = true;
+        const int nb = nz + (one ? 1 : 0);
+        if (nb > 32) {
+            bw.put(0u, nb - 32);
+            bw.put(one ? 1u : 0u, 32);
+        } else if (nb > 0) {
+            bw.put(one ? 1u : 0u, nb);
         }
         e = (uint32_t)value | ((uint32_t)low << 8) | (known ? (1u << 16) : 0u);
     }
@@ -312,21 +315,22 @@ __global__ void __launch_bounds__(64) k_t2_code(T2Args a) {
 // nl / lrate for the emission pass and k_t2_copy.
 // --------------------------------------------------------------------------
 constexpr int kT2Waves = 4;  // precincts per workgroup
+constexpr int kWaveNodes = 256;  // tag-tree nodes of one k_t2_wave precinct (LDS)
 struct T2LaneShared {
     uint8_t nl[kMaxLayers][64];     // cumulative passes per layer
     int32_t lr[kMaxLayers][64];     // cumulative bytes per layer
-    uint64_t p1v[64];               // pass-count codeword, then the Lblock comma code
-    int32_t len[64];                // this layer's bytes
-    uint8_t n[64], p1n[64], p2n[64], first[64];
-    uint32_t tt[kLdsNodes];         // tag-tree nodes
+    uint8_t n[64], first[64];       // tree_set staging: zero bit-planes, first layer
+    uint32_t tt[kWaveNodes];        // tag-tree nodes (the host picks k_t2_wave only when they fit)
     uint32_t hdr;                   // header bytes of the packet (lane 0 -> all)
 };
 
-// the lanes of one wave see each other's LDS writes in program order; this
-// only keeps the compiler from moving LDS accesses across the point
+// the lanes of one wave see each other's LDS writes in program order (the
+// LDS performs a wave's operations in issue order); this only keeps the
+// compiler from moving or caching memory accesses across the point -- no
+// s_waitcnt (a wavefront-scope fence waited for every global store in flight)
 __device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
 }
 
 // put up to 64 bits (nb <= 64) through the 32-bit-at-a-time writer
@@ -374,23 +378,43 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
             uint64_t k8[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) k8[i] = hk[min(i, kMaxPasses)];
+            // layers in groups of 8: the hull points of the group first (keys
+            // in registers), then its 8 pass-table loads together, then the 8
+            // rate loads together (two load round trips per group, not two
+            // per layer)
             int at = 0;  // last hull point with key >= K (point 0: nothing)
-            for (int l = 0; l < L; l++) {
-                int nc;
-                if (a.lossless && l == L - 1) {
-                    nc = a.npasses[b];
-                } else {
-                    const uint64_t K = a.K[l];
-                    auto key = [&](int i) { return i < 8 ? k8[i] : hk[i]; };
-                    while (at + 1 < nh && key(at + 1) >= K) at++;
-                    while (at > 0 && key(at) < K) at--;  // (a threshold above the previous one)
-                    nc = hp[at];
+            auto key = [&](int i) { return i < 8 ? k8[i] : hk[i]; };
+            for (int l0 = 0; l0 < L; l0 += 8) {
+                int atv[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int l = l0 + j;
+                    if (l < L && !(a.lossless && l == L - 1)) {
+                        const uint64_t K = a.K[l];
+                        while (at + 1 < nh && key(at + 1) >= K) at++;
+                        while (at > 0 && key(at) < K) at--;  // (a threshold above the previous one)
+                    }
+                    atv[j] = at;
                 }
-                const int32_t r = nc ? R[nc - 1] : 0;
-                S.nl[l][lane] = (uint8_t)nc;
-                S.lr[l][lane] = r;
-                gnl[l] = (uint8_t)nc;
-                glr[l] = r;
+                int ncv[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int l = l0 + j;
+                    ncv[j] = (a.lossless && l == L - 1) ? (int)a.npasses[b] : (int)hp[atv[j]];
+                }
+                int32_t rv[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) rv[j] = R[max(ncv[j], 1) - 1];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int l = l0 + j;
+                    if (l >= L) break;
+                    const int32_t r = ncv[j] ? rv[j] : 0;
+                    S.nl[l][lane] = (uint8_t)ncv[j];
+                    S.lr[l][lane] = r;
+                    gnl[l] = (uint8_t)ncv[j];
+                    glr[l] = r;
+                }
             }
         } else {
             for (int l = 0; l < L; l++) {
@@ -399,15 +423,15 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
             }
         }
     }
-    // tag trees (nodes in LDS when they fit, else the precinct's global slot):
-    // inclusion layer and zero bit-planes of every leaf
+    // tag trees in LDS (an LDS pointer, so no flat access): inclusion layer
+    // and zero bit-planes of every leaf
     int nodes = 0, toff[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         toff[k] = nodes;
         if (k < d.nb && d.ncw[k] && d.nch[k]) nodes += 2 * tree_size(d.ncw[k], d.nch[k]);
     }
-    uint32_t *tt = nodes <= kLdsNodes ? S.tt : a.tt + d.tt_off;
+    uint32_t *tt = S.tt;
     int firstl = L;
     if (own)
         for (int l = 0; l < L; l++)
@@ -458,12 +482,6 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
             p1n = cn + extra + 1;
             p2n = lb + dev_floor_log2(n);
         }
-        S.n[lane] = (uint8_t)n;
-        S.len[lane] = len;
-        S.p1v[lane] = p1v;
-        S.p1n[lane] = (uint8_t)p1n;
-        S.p2n[lane] = (uint8_t)p2n;
-        S.first[lane] = (uint8_t)(first_time ? 1 : 0);
         const bool nonempty = __ballot(n > 0) != 0ull;
         if (n > 0 && first_time) incl = l;
         // body bytes before this block in the packet (blocks in order)
@@ -491,14 +509,17 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
                     const int jl = j - (jb == 0 ? 0 : (jb == 1 ? c0 : c0 + c1));
                     const int cw = d.ncw[jb], ch = d.nch[jb];
                     uint32_t *ti = tt + toff[jb], *tz = ti + tree_size(cw, ch);
-                    const int nj = S.n[j];
-                    const bool ft = S.first[j] != 0;
+                    // block j's fields from lane j's registers (no LDS round trip)
+                    const int nj = __builtin_amdgcn_readlane(n, j);
+                    const bool ft = __builtin_amdgcn_readlane(first_time ? 1 : 0, j) != 0;
                     if (ft) tree_encode(ti, cw, ch, jl, l + 1, w);
                     else w.bit(nj > 0 ? 1 : 0);
                     if (nj <= 0) continue;
                     if (ft) tree_encode(tz, cw, ch, jl, 1 << 20, w);
-                    put64(w, S.p1v[j], S.p1n[j]);
-                    put64(w, (uint64_t)(uint32_t)S.len[j], S.p2n[j]);
+                    const uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(p1v >> 32), j) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)p1v, j);
+                    put64(w, pv, __builtin_amdgcn_readlane(p1n, j));
+                    put64(w, (uint64_t)(uint32_t)__builtin_amdgcn_readlane(len, j), __builtin_amdgcn_readlane(p2n, j));
                 }
             w.flush();
             if (EMIT) {
@@ -669,32 +690,53 @@ __global__ void __launch_bounds__(64) k_t2_tp_emit(T2Args a) {
     p[11] = (uint8_t)d.tnsot;
     p += 12;
     const size_t p0 = (size_t)d.prec0 * a.L, p1 = (size_t)(d.prec0 + d.nprec) * a.L;
-    if (a.plt) {  // PLT segments (A.7.3): lengths as 7-bit groups, <= 65532 bytes each
+    // packet lengths are loaded 8 at a time ahead of the byte stores (a load
+    // after a byte store would wait for it: the stores may alias)
+    if (a.plt && p1 > p0) {  // PLT segments (A.7.3): lengths as 7-bit groups, <= 65532 bytes each
         size_t i = p0;
         int z = 0;
+        uint8_t *hdr = p;
+        p += 5;
+        uint32_t seg = 0;
         while (i < p1) {
-            uint8_t *hdr = p;
-            p += 5;
-            uint32_t seg = 0;
-            while (i < p1) {
-                const uint32_t len = a.pk_len[i];
+            uint32_t l8[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) l8[j] = a.pk_len[min(i + j, p1 - 1)];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (i >= p1) break;
+                const uint32_t len = l8[j];
                 const int k = varint_len(len);
-                if (seg + (uint32_t)k > 65532) break;
-                for (int j = k - 1; j >= 0; j--) *p++ = (uint8_t)(((len >> (7 * j)) & 0x7F) | (j ? 0x80 : 0));
+                if (seg + (uint32_t)k > 65532) {  // close this segment, open the next
+                    hdr[0] = 0xFF; hdr[1] = 0x58;
+                    hdr[2] = (uint8_t)((3 + seg) >> 8); hdr[3] = (uint8_t)(3 + seg);
+                    hdr[4] = (uint8_t)z++;
+                    hdr = p;
+                    p += 5;
+                    seg = 0;
+                }
+                for (int q = k - 1; q >= 0; q--) *p++ = (uint8_t)(((len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0));
                 seg += (uint32_t)k;
                 i++;
             }
-            hdr[0] = 0xFF; hdr[1] = 0x58;
-            hdr[2] = (uint8_t)((3 + seg) >> 8); hdr[3] = (uint8_t)(3 + seg);
-            hdr[4] = (uint8_t)z++;
         }
+        hdr[0] = 0xFF; hdr[1] = 0x58;
+        hdr[2] = (uint8_t)((3 + seg) >> 8); hdr[3] = (uint8_t)(3 + seg);
+        hdr[4] = (uint8_t)z;
     }
     p[0] = 0xFF; p[1] = 0x93;
     p += 2;
     uint64_t o = (uint64_t)(p - a.out);
-    for (size_t i = p0; i < p1; i++) {
-        a.pk_off[i] = o;
-        o += a.pk_len[i];
+    for (size_t i0 = p0; i0 < p1; i0 += 8) {
+        uint32_t l8[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) l8[j] = a.pk_len[min(i0 + j, p1 - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (i0 + j < p1) {
+                a.pk_off[i0 + j] = o;
+                o += l8[j];
+            }
     }
 }
 
@@ -789,7 +831,7 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
     const int L = plan.rc.layers;
     t2_nprec = (int)T.prec.size();
     t2_ntp = (int)T.tp.size();
-    t2_wave = T.max_prec_blocks <= 64;  // k_t2_wave (else the serial k_t2_code + k_apply)
+    t2_wave = T.max_prec_blocks <= 64 && T.max_prec_nodes <= kWaveNodes;  // k_t2_wave (else the serial k_t2_code + k_apply)
     const size_t npk = (size_t)t2_nprec * L;
     if (!ensure_t2<PrecDesc>(t2prec, T.prec.size(), err) || !ensure_t2<TpDesc>(t2tp, T.tp.size(), err) ||
         !ensure_t2<uint32_t>(t2tt, (size_t)T.tt_nodes, err) || !ensure_t2<int8_t>(t2lblock, nb, err) ||
