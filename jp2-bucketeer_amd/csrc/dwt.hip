@@ -268,11 +268,11 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn r
 // the 4-step footprint: the 16 kept samples are exact, as in lift_regs),
 // scaled and written de-interleaved as 8 low + 8 high words (two 16-byte
 // stores each when the row is aligned).  Rows as in hlift_write.
-template <bool REV, int NROWS, bool ALIGNED, typename RowFn>
-__device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, RowFn rows) {
+template <bool REV, int NROWS, bool ALIGNED, int NT = kDwtThreads, typename RowFn>
+__device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, RowFn rows, int nrows = NROWS) {
     const int nseg = (W + 15) >> 4;
     const int nlh = (W + 1) / 2;
-    for (int it = threadIdx.x; it < NROWS * nseg; it += kDwtThreads) {
+    for (int it = threadIdx.x; it < nrows * nseg; it += NT) {
         const int r = it / nseg, k = it - r * nseg;
         int32_t *lrow, *hrow;
         if (!rows(r, lrow, hrow)) continue;
@@ -739,103 +739,91 @@ struct DwtTailArgs {
     int level, levels;
 };
 
-// Levels level..levels of one tile-component, entirely in LDS.  1024 threads
-// as 8 rows x 128 columns (no index divisions; a tail level is <= 128 x 128
-// for the recipe's tiles).  Each level works on a dense copy of its input
-// (row stride = its width) and writes the LL it leaves densely into the
-// other buffer for the next level, so every access is unit- or 2-stride
-// (the in-place layout -- element (i, j) of level k at (i << k, j << k) --
-// cost 2^k-way LDS bank conflicts at every step of the deeper levels).
+// Levels level..levels of one tile-component, entirely in LDS, with the
+// band kernels' window lifting (each level two barrier-separated passes
+// instead of one barrier per lifting step):
+//   vertical   thread = (column, group of kTailRG rows): the group plus a
+//              4-row halo on each side read into registers, lifted there
+//              (lift_regs: the halo absorbs the lifting footprint, the kept
+//              rows are exact), scaled, written to the padded row layout
+//              hlift_seg reads;
+//   horizontal hlift_seg over every row (16-sample segments with halos in
+//              registers), high bands (and the last level's LL) straight to
+//              HBM, a non-final LL densely into `ll` for the next level.
+// The level's input is dense (row stride = its width): the LL scratch of the
+// previous level, then `ll`.  Same expressions in the same order as the
+// oracle (bit-exact).
 constexpr int kTailThreads = 1024;
-constexpr int kTailCols = 128, kTailRows = kTailThreads / kTailCols;
-template <bool REV>
-__device__ __forceinline__ void tail_lift(int32_t *x, int idx, int lidx, int ridx, int step) {
-    if (REV) {
-        if (step == 0) x[idx] -= (x[lidx] + x[ridx]) >> 1;
-        else x[idx] += (x[lidx] + x[ridx] + 2) >> 2;
-    } else {
-        float *f = (float *)x;
-        const float cf = step == 0 ? A97 : (step == 1 ? B97 : (step == 2 ? G97 : D97));
-        float t = f[lidx] + f[ridx];
-        t = cf * t;
-        f[idx] = f[idx] + t;
-    }
-}
-
+constexpr int kTailRG = 16;                                   // rows per vertical item
+constexpr int kTailWords = 16384 + 64 * 4 + kPadL + kPadR;    // padded rows of a <= 128 x 128 level
 template <bool REV>
 __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
-    __shared__ int32_t bufA[kDwtLdsWords];      // a level's input
-    __shared__ int32_t bufB[kDwtLdsWords / 4];  // the LL it leaves
-    const int tc = blockIdx.x;
-    const int tx = threadIdx.x & (kTailCols - 1), ty = threadIdx.x / kTailCols;
+    __shared__ __attribute__((aligned(16))) int32_t rows_[kTailWords];  // vertical output, padded rows
+    __shared__ int32_t ll[kDwtLdsWords / 4];                             // the next level's input (dense)
+    const int tc = blockIdx.x, tid = threadIdx.x;
     int sh = a.level - 1;
     int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh;
     int H = (a.tc_h[tc] + (1 << sh) - 1) >> sh;
-    {
-        const int32_t *s = (const int32_t *)a.src + (size_t)tc * a.src_tc;
-        for (int y = ty; y < H; y += kTailRows)
-            for (int x = tx; x < W; x += kTailCols) bufA[y * W + x] = s[(size_t)y * a.src_stride + x];
-    }
-    __syncthreads();
-    int32_t *cur = bufA, *nxt = bufB;
+    // the first level reads the previous level's LL scratch in HBM directly,
+    // later levels the LL the previous one left in `ll` (two inlined copies of
+    // the vertical pass, so each knows its address space)
+    const int32_t *g_src = (const int32_t *)a.src + (size_t)tc * a.src_tc;
     int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
-    const int nsteps = REV ? 2 : 4;
+    constexpr int NR = kTailRG + 2 * kDwtHalo;
     for (int lv = a.level; lv <= a.levels; lv++) {
-        const int ld = W;
-        // vertical lifting (odd rows first), symmetric extension at 0 / H-1
-        if (H > 1)
-            for (int st = 0; st < nsteps; st++) {
-                const int par = (st & 1) ? 0 : 1;
-                for (int y = par + 2 * ty; y < H; y += 2 * kTailRows) {
-                    const int l = y > 0 ? y - 1 : y + 1, r = y + 1 < H ? y + 1 : y - 1;
-                    for (int x = tx; x < W; x += kTailCols) tail_lift<REV>(cur, y * ld + x, l * ld + x, r * ld + x, st);
+        const int ld = lds_row_stride(W);
+        // ---- vertical: column x, rows [g * kTailRG, +kTailRG) ----
+        auto vertical = [&](const int32_t *srcp, int sstride) {
+            const int ngrp = (H + kTailRG - 1) / kTailRG;
+            for (int it = tid; it < W * ngrp; it += kTailThreads) {
+                const int g = it / W, x = it - g * W;
+                const int r0 = g * kTailRG, y0 = r0 - kDwtHalo;
+                int32_t v[NR];
+                // every row load issues before any is used (clamped rows, zeroed after)
+#pragma unroll
+                for (int i = 0; i < NR; i++) v[i] = srcp[min(max(y0 + i, 0), H - 1) * sstride + x];
+#pragma unroll
+                for (int i = 0; i < NR; i++) {
+                    const int y = y0 + i;
+                    v[i] = (y >= 0 && y < H) ? v[i] : 0;
                 }
-                __syncthreads();
-            }
-        if (!REV && H > 1) {
-            float *f = (float *)cur;
-            for (int y = ty; y < H; y += kTailRows)
-                for (int x = tx; x < W; x += kTailCols) {
-                    const int o = y * ld + x;
-                    f[o] = (y & 1) ? f[o] * K97 : f[o] * INVK97;
-                }
-            __syncthreads();
-        }
-        if (W > 1)
-            for (int st = 0; st < nsteps; st++) {
-                const int par = (st & 1) ? 0 : 1;
-                for (int y = ty; y < H; y += kTailRows)
-                    for (int x = par + 2 * tx; x < W; x += 2 * kTailCols) {
-                        const int l = x > 0 ? x - 1 : x + 1, r = x + 1 < W ? x + 1 : x - 1;
-                        tail_lift<REV>(cur, y * ld + x, y * ld + l, y * ld + r, st);
+                if (H > 1) {
+                    lift_regs<REV, NR>(v, y0, H);
+                    if (!REV) {
+#pragma unroll
+                        for (int i = kDwtHalo; i < kDwtHalo + kTailRG; i++)
+                            v[i] = __float_as_int(__int_as_float(v[i]) * ((i & 1) ? K97 : INVK97));
                     }
-                __syncthreads();
-            }
-        const int nlv = (H + 1) / 2, nlh = (W + 1) / 2;
-        const bool last = lv == a.levels;
-        // high bands (and the final LL) straight to HBM; a non-final LL,
-        // scaled, densely into the other buffer
-        for (int y = ty; y < H; y += kTailRows) {
-            const bool ylo = (y & 1) == 0;
-            int32_t *drow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
-            for (int j = tx; j < W; j += kTailCols) {
-                const bool lo = j < nlh;
-                const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
-                int32_t v = cur[y * ld + x];
-                if (!REV && W > 1) {
-                    float f = __int_as_float(v);
-                    f = lo ? f * INVK97 : f * K97;
-                    v = __float_as_int(f);
                 }
-                if (lo && ylo && !last) nxt[(y >> 1) * nlh + j] = v;
-                else drow[j] = v;
+#pragma unroll
+                for (int i = 0; i < kTailRG; i++)
+                    if (r0 + i < H) rows_[kPadL + (r0 + i) * ld + x] = v[kDwtHalo + i];
+            }
+        };
+        if (lv == a.level) vertical(g_src, a.src_stride);
+        else vertical(ll, W);
+        __syncthreads();
+        // ---- horizontal lifting, scaling, de-interleaved write ----
+        const int nlv = (H + 1) / 2;
+        const bool last = lv == a.levels;
+        const int nlh = (W + 1) / 2;
+        auto rowfn = [&](int y, int32_t *&lrow, int32_t *&hrow) -> bool {
+            const bool ylo = (y & 1) == 0;
+            hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
+            lrow = (ylo && !last) ? ll + (y >> 1) * nlh : hrow;
+            return true;
+        };
+        if (W > 1 && (W & 15) == 0) hlift_seg<REV, 0, true, kTailThreads>(rows_, W, ld, rowfn, H);
+        else if (W > 1) hlift_seg<REV, 0, false, kTailThreads>(rows_, W, ld, rowfn, H);
+        else {  // one column: no horizontal transform (the LL is the column itself)
+            for (int y = tid; y < H; y += kTailThreads) {
+                int32_t *lrow, *hrow;
+                rowfn(y, lrow, hrow);
+                lrow[0] = rows_[kPadL + y * ld];
             }
         }
         if (last) break;
         __syncthreads();
-        int32_t *t = cur;
-        cur = nxt;
-        nxt = t;
         W = nlh;
         H = nlv;
     }
@@ -924,7 +912,8 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
     for (int lv = 1; lv <= p.levels; lv++) {
         const int maxW = (p.plane_w + (1 << (lv - 1)) - 1) >> (lv - 1);
         const int maxH = (p.plane_h + (1 << (lv - 1)) - 1) >> (lv - 1);
-        if (lv >= 2 && maxW * maxH <= kDwtLdsWords && ((maxW + 1) / 2) * ((maxH + 1) / 2) <= kDwtLdsWords / 4) {
+        if (lv >= 2 && ((maxW + 1) / 2) * ((maxH + 1) / 2) <= kDwtLdsWords / 4 &&
+            lds_row_stride(maxW) * maxH + kPadL + kPadR <= kTailWords) {
             DwtTailArgs t;
             t.src = scratch[(lv - 1) & 1];
             t.src_stride = ll_stride;
