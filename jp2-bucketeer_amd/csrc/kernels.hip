@@ -696,10 +696,12 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     // one issued.
     uint32_t col[64];
     const int hm1 = d.h - 1;
+    // all 64 row loads in flight at once (the column lives in 64 registers
+    // either way)
+#pragma unroll
+    for (int y = 0; y < 64; y++) col[y] = (uint32_t)src[(size_t)min(y, hm1) * a.plane_w];
 #pragma unroll
     for (int y0 = 0; y0 < 64; y0 += 32) {
-#pragma unroll
-        for (int y = y0; y < y0 + 32; y++) col[y] = (uint32_t)src[(size_t)min(y, hm1) * a.plane_w];
 #pragma unroll
         for (int y = y0; y < y0 + 32; y++) {
             const int32_t raw = (int32_t)col[y];
@@ -746,17 +748,34 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     // magnitudes only from here on
 #pragma unroll
     for (int y = 0; y < 64; y++) col[y] &= 0x7FFFFFFFu;
-    // every plane's column mask, kept in LDS for the distortion sums below
-    for (int p = 0; p < P; p++) {
-        uint32_t c_lo = 0, c_hi = 0;
+    // every plane's column mask, kept in LDS for the distortion sums below.
+    // Four planes at a time: a row's 4 bits are spread to the 4 bytes of a
+    // word by one multiply (nib * 0x204081 & 0x01010101), so G[g] collects
+    // rows 8g..8g+7 with plane p0+k in byte k; each plane's 64-bit mask is
+    // then byte k of G[0..7], gathered by v_perm_b32 (4 ops per row group of
+    // 4 planes instead of 2 per row and plane)
+    for (int p0 = 0; p0 < P; p0 += 4) {
+        uint32_t G[8];
 #pragma unroll
-        for (int y = 0; y < 32; y++) {
-            c_lo |= __builtin_amdgcn_ubfe(col[y], (uint32_t)p, 1u) << y;
-            c_hi |= __builtin_amdgcn_ubfe(col[y + 32], (uint32_t)p, 1u) << y;
+        for (int g = 0; g < 8; g++) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                acc |= (__umul24(__builtin_amdgcn_ubfe(col[8 * g + i], (uint32_t)p0, 4u), 0x00204081u) & 0x01010101u) << i;
+            G[g] = acc;
         }
-        const uint64_t m = ((uint64_t)c_hi << 32) | c_lo;
-        planes[p * 64 + lane] = m;
-        BT[(size_t)p * 64 + lane] = m;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = p0 + k;
+            if (p >= P) break;
+            // bytes k of (G0, G1) and (G2, G3) -> low halves; the pair merged
+            const uint32_t sel = (uint32_t)k | ((uint32_t)(k + 4) << 8) | 0x0C0C0000u;
+            const uint32_t lo = __builtin_amdgcn_perm(G[1], G[0], sel) | (__builtin_amdgcn_perm(G[3], G[2], sel) << 16);
+            const uint32_t hi = __builtin_amdgcn_perm(G[5], G[4], sel) | (__builtin_amdgcn_perm(G[7], G[6], sel) << 16);
+            const uint64_t m = ((uint64_t)hi << 32) | lo;
+            planes[p * 64 + lane] = m;
+            BT[(size_t)p * 64 + lane] = m;
+        }
     }
     constexpr bool lossless = REV;
     constexpr int dd = lossless ? 0 : 1;  // reconstruction offset, half-units
