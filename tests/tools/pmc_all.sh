@@ -16,6 +16,6 @@ P p2 "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ
 P p3 FETCH_SIZE || exit 1
 P p4 WRITE_SIZE || exit 1
 P p5 "SQC_ICACHE_HITS SQC_ICACHE_MISSES GRBM_GUI_ACTIVE" || exit 1
-python tests/tools/sq_summary.py $o/p1 $o/p2 $o/p5 --out profiles/$r/sq_counters.json > $o/sq.txt || exit 1
+python tests/tools/sq_summary.py $o/p1 $o/p2 $o/p5 --out profiles/$r/t1_sq_counters.json > $o/sq.txt || exit 1
 python tests/tools/pmc_summary.py --fetch $o/p3 --write $o/p4 --out profiles/$r/pmc_traffic.json > $o/traffic.txt || exit 1
-mkdir -p $o/out && cp profiles/$r/sq_counters.json profiles/$r/pmc_traffic.json $o/out/
+mkdir -p $o/out && cp profiles/$r/t1_sq_counters.json profiles/$r/pmc_traffic.json $o/out/
