@@ -140,7 +140,6 @@ struct T2Tables {
     std::vector<TpDesc> tp;   // code-stream order
     int64_t tt_nodes = 0;
     int max_prec_blocks = 0;  // code-blocks of the largest precinct
-    int max_prec_nodes = 0;   // tag-tree nodes of the largest precinct
 };
 // Tables for tiles [tile0, tile1) of `P` (blocks rebased by -block0: a
 // tile-split rank's blocks are its sub-plan's).

@@ -970,9 +970,23 @@ __global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a, T1ItemArgs ia
     if (in) {
         const int kc = kcut;
         const double wgt = a.weight[b];
-        for (int p = 0; p < P; p++) {
-            const size_t i = (size_t)b * 32 + p;
-            if (plane_bin(a.dref[i] + a.dsig[i], wgt, a.est[i]) >= kc) { pmin = p; break; }
+        // planes 8 at a time: their loads in flight together
+        bool found = false;
+        for (int p0 = 0; p0 < P && !found; p0 += 8) {
+            int64_t dd[8];
+            uint32_t e[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const size_t i = (size_t)b * 32 + min(p0 + j, 31);
+                dd[j] = a.dref[i] + a.dsig[i];
+                e[j] = a.est[i];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (!found && p0 + j < P && plane_bin(dd[j], wgt, e[j]) >= kc) {
+                    pmin = p0 + j;
+                    found = true;
+                }
         }
         a.pmin[b] = (uint8_t)pmin;
     }
@@ -995,7 +1009,7 @@ struct HullArgs {
     uint8_t *nhull;
     uint8_t *hpass;   // [block][kMaxPasses+1]
     uint64_t *hkey;   // [block][kMaxPasses+1]
-    int64_t *hdist;   // [block][kMaxPasses+1] cumulative distortion at each hull point
+    int64_t *hdist;   // [block][kMaxPasses+1] HullPt: the stack's distortion and rate at each point
     unsigned long long *hbytes;  // [kPcrdBins] segment bytes per slope bin (zeroed by k_quant)
     uint32_t *hcount;            // [kPcrdBins] segments per slope bin
 };
@@ -1006,76 +1020,100 @@ __device__ __forceinline__ int pcrd_bin(uint64_t key) {
     return b < 0 ? 0 : (b >= kPcrdBins ? kPcrdBins - 1 : b);
 }
 
+// hull stack entry beside the output arrays (pass index, slope key): the
+// cumulative distortion and the rate at the point, so a pop is one round
+// trip (no pass-index -> rate chain)
+struct HullPt {
+    int64_t d;
+    int32_t r, pad;
+};
+static_assert(sizeof(HullPt) == 16, "HullPt layout");
+
 __device__ __forceinline__ void hull_one(const HullArgs &a, int b, unsigned long long *lb, uint32_t *lc) {
-    int np = a.npasses[b];
+    const int np = a.npasses[b];
     const int32_t *R = a.rates + (size_t)b * kMaxPasses;
     const int64_t *Dd = a.dists + (size_t)b * kMaxPasses;
     uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
     uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
-    // the hull stack lives in the output arrays themselves (pass index,
-    // slope bits) plus the cumulative distortion of each hull point in hd,
-    // so the lane keeps no per-pass arrays (no scratch memory)
-    int64_t *hd = a.hdist + (size_t)b * (kMaxPasses + 1);
-    double wgt = a.weight[b];
+    // the hull stack lives in the output arrays themselves plus hs, so the
+    // lane keeps no per-pass arrays (no scratch memory); its top entry (key,
+    // cumulative distortion, rate) also lives in registers, so only a pop
+    // reads the stack back
+    HullPt *hs = (HullPt *)a.hdist + (size_t)b * (kMaxPasses + 1);
+    const double wgt = a.weight[b];
     int nh = 1;
     hp[0] = 0;
     hk[0] = 0;
-    hd[0] = 0;
-    // the stack's top entry (key, cumulative distortion, rate at its pass)
-    // also lives in registers, so only a pop reads the stack back; the next
-    // pass's rate and distortion are loaded one pass ahead
     uint64_t tk = 0;
     int64_t td = 0;
     int32_t tr = 0;
     int64_t Dn = 0;
-    int32_t Rnx = np ? R[0] : 0;
-    int64_t Dnx = np ? Dd[0] : 0;
-    for (int n = 1; n <= np; n++) {
-        const int32_t Rn = Rnx;
-        Dn += Dnx;
-        if (n < np) {
-            Rnx = R[n];
-            Dnx = Dd[n];
+    // The workgroup's slope-bin histogram follows the stack: a push adds its
+    // segment (key, bytes), a pop takes it back out, so what remains is the
+    // final hull's segments (no pass over the hull afterwards)
+    auto seg = [&](uint64_t key, int32_t bytes, int sign) {
+        const int bn = pcrd_bin(key);
+        atomicAdd(&lb[bn], (unsigned long long)(int64_t)(sign * bytes));
+        atomicAdd(&lc[bn], (uint32_t)sign);
+    };
+    // passes 8 at a time: their rate and distortion loads in flight together
+    for (int n0 = 0; n0 < np; n0 += 8) {
+        int32_t r8[8];
+        int64_t d8[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int i = min(n0 + j, np - 1);
+            r8[j] = R[i];
+            d8[j] = Dd[i];
         }
-        for (;;) {
-            const int64_t dD = Dn - td;
-            const int32_t dR = Rn - tr;
-            bool pop = false;
-            double s = 0.0;
-            if (dD <= 0) break;
-            if (dR <= 0) pop = true;
-            else {
-                s = (double)dD * wgt / (double)dR;
-                pop = nh >= 2 && s >= __longlong_as_double((long long)tk);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int n = n0 + j + 1;
+            if (n > np) break;
+            const int32_t Rn = r8[j];
+            Dn += d8[j];
+            for (;;) {
+                const int64_t dD = Dn - td;
+                const int32_t dR = Rn - tr;
+                bool pop = false;
+                double s = 0.0;
+                if (dD <= 0) break;
+                if (dR <= 0) pop = true;
+                else {
+                    s = (double)dD * wgt / (double)dR;
+                    pop = nh >= 2 && s >= __longlong_as_double((long long)tk);
+                }
+                if (pop) {
+                    nh--;
+                    const int32_t rpop = tr;
+                    const uint64_t kpop = tk;
+                    if (nh <= 1) {
+                        tk = 0;
+                        td = 0;
+                        tr = 0;
+                    } else {
+                        const HullPt e = hs[nh - 1];
+                        tk = hk[nh - 1];
+                        td = e.d;
+                        tr = e.r;
+                    }
+                    seg(kpop, rpop - tr, -1);
+                    continue;
+                }
+                seg((uint64_t)__double_as_longlong(s), Rn - tr, 1);
+                tk = (uint64_t)__double_as_longlong(s);
+                td = Dn;
+                tr = Rn;
+                hp[nh] = (uint8_t)n;
+                hk[nh] = tk;
+                hs[nh].d = Dn;
+                hs[nh].r = Rn;
+                nh++;
+                break;
             }
-            if (pop) {
-                nh--;
-                const int hh = hp[nh - 1];
-                tk = hk[nh - 1];
-                td = hd[nh - 1];
-                tr = hh ? R[hh - 1] : 0;
-                continue;
-            }
-            tk = (uint64_t)__double_as_longlong(s);
-            td = Dn;
-            tr = Rn;
-            hp[nh] = (uint8_t)n;
-            hk[nh] = tk;
-            hd[nh] = Dn;
-            nh++;
-            break;
         }
     }
     a.nhull[b] = (uint8_t)nh;
-    // the hull's segments into the workgroup's slope-bin histogram
-    int32_t r0 = 0;
-    for (int i = 1; i < nh; i++) {
-        const int32_t r1 = R[hp[i] - 1];
-        const int bn = pcrd_bin(hk[i]);
-        atomicAdd(&lb[bn], (unsigned long long)(r1 - r0));
-        atomicAdd(&lc[bn], 1u);
-        r0 = r1;
-    }
 }
 
 constexpr int kHullThreads = 256;
@@ -1105,18 +1143,17 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
 // exactly the keys >= K' = min { k : S(k) <= budget } (split.cpp), and K' is
 // one above the first key not taken -- the rule's Kc (Kdu-Layer-Info).
 //
-// k_select finds K' per layer in one launch, no sort:
-//  1. every workgroup: suffix sums of the k_hull bin histogram; per layer the
-//     bin b whose segments straddle the budget (S over the bins above b fits,
-//     with b's bytes it does not);
-//  2. every workgroup, thread per code-block: the hull segments whose key falls
-//     in one of those bins are appended to that bin's candidate list;
-//  3. the last workgroup to arrive (agent-scope release / acquire ticket,
-//     cdna_hip_programming.md Guideline 16) resolves each layer inside its
-//     bin: the largest key v with (bytes above the bin) + (candidate bytes
-//     with key >= v) > budget is the first key not taken, K' = v + 1.
-// The ticket and list fill counters are zeroed by k_quant and left zero by
-// the last workgroup for the next launch (the device rate loop runs several).
+// Two launches, no sort:
+//  1. every workgroup of both: suffix sums of the k_hull bin histogram; per
+//     layer the bin b whose segments straddle the budget (S over the bins
+//     above b fits, with b's bytes it does not);
+//  2. k_select, thread per code-block: the hull segments whose key falls in
+//     one of those bins are appended to that bin's candidate list;
+//  3. k_select_resolve, a workgroup per layer: the largest key v with (bytes
+//     above the bin) + (candidate bytes with key >= v) > budget is the first
+//     key not taken, K' = v + 1.
+// The list fill counters are zeroed by k_quant and left zero by
+// k_select_resolve for the next k_select (the device rate loop runs several).
 struct SelectArgs {
     const int *halt;  // device rate loop: nothing to do once it has stopped
     int nblocks, layers;
@@ -1128,31 +1165,34 @@ struct SelectArgs {
     const int64_t *budget;
     uint64_t *lkey;   // candidate lists, capacity >= every hull segment
     uint32_t *lsize;
-    uint32_t *ctl;    // [0] arrival ticket, [1 + i] fill of list i
+    uint32_t *ctl;    // [1 + i] fill of list i ([0] unused)
     uint64_t *K, *Kc;
     int64_t *dbg;     // debug builds: [0] lists, [1 + i] list sizes, [33 + l] rounds, [65 + l] survivors
 };
 
 constexpr int kSelThreads = 1024, kSelBrute = 64;
-__global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
-    __shared__ unsigned long long sfx[kPcrdBins];  // S(bin): bytes of the bins >= bin
-    __shared__ int8_t binmap[kPcrdBins];           // bin -> candidate list (-1: none)
-    __shared__ uint64_t wsum[kSelThreads / 64 + 1];
-    __shared__ int lbin[kMaxLayers], lli[kMaxLayers];
-    __shared__ int64_t lneed[kMaxLayers];          // budget - bytes above the bin
-    __shared__ int list_bin[kMaxLayers];
-    __shared__ uint32_t list_off[kMaxLayers + 1];
-    __shared__ int nlist, last;
-    // last workgroup: the narrowing state and the survivors
-    __shared__ uint64_t rlo, rhi, rmax;
-    __shared__ int64_t rneed;
-    __shared__ uint32_t rcount;
-    __shared__ uint64_t bkey[kSelBrute];
-    __shared__ uint32_t bsize[kSelBrute];
-    __shared__ uint32_t hcnt[kPcrdBins];
-    const int tid = threadIdx.x, lane = tid & 63, L = a.layers;
-    if (a.halt && *a.halt) return;
-    // 1. suffix sums, 4 bins per thread
+// phase 1, run by every workgroup of both kernels (a few microseconds; no
+// hand-off through memory): suffix sums of the bin histogram, per layer the
+// bin and what it must supply, one candidate list per distinct bin
+struct SelBins {
+    unsigned long long sfx[kPcrdBins];  // S(bin): bytes of the bins >= bin
+    int8_t binmap[kPcrdBins];           // bin -> candidate list (-1: none)
+    uint64_t wsum[kSelThreads / 64 + 1];
+    int lbin[kMaxLayers], lli[kMaxLayers];
+    int64_t lneed[kMaxLayers];          // budget - bytes above the bin
+    int list_bin[kMaxLayers];
+    uint32_t list_off[kMaxLayers + 1];
+    int nlist;
+};
+__device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
+    const int tid = threadIdx.x, L = a.layers;
+    unsigned long long *sfx = sh.sfx;
+    int8_t *binmap = sh.binmap;
+    uint64_t *wsum = sh.wsum;
+    int *lbin = sh.lbin, *lli = sh.lli, *list_bin = sh.list_bin;
+    int64_t *lneed = sh.lneed;
+    uint32_t *list_off = sh.list_off;
+    // suffix sums, 4 bins per thread
     {
         uint64_t v[4], s = 0;
 #pragma unroll
@@ -1203,9 +1243,19 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
             lli[l] = i;
         }
         list_off[n] = o;
-        nlist = n;
+        sh.nlist = n;
     }
     __syncthreads();
+}
+
+__global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
+    __shared__ SelBins sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (a.halt && *a.halt) return;
+    select_bins(a, sh);
+    const int8_t *binmap = sh.binmap;
+    const uint32_t *list_off = sh.list_off;
+    const int nlist = sh.nlist;
     // 2. candidates of those bins, thread per code-block
     if (nlist > 0)
         for (int b = blockIdx.x * kSelThreads + tid; b < a.nblocks; b += gridDim.x * kSelThreads) {
@@ -1213,58 +1263,75 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
             const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
             const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
             const int32_t *R = a.rates + (size_t)b * kMaxPasses;
-            for (int i = 1; i < nh; i++) {
-                const uint64_t key = hk[i];
-                const int li = binmap[pcrd_bin(key)];
-                // one fill atomic per wave and list (a list's lanes take
-                // consecutive slots): same-word atomics serialise in L2
-                uint64_t todo = __ballot(li >= 0);
-                while (todo) {
-                    const int lead = __builtin_ctzll(todo);
-                    const int lj = __shfl(li, lead, 64);
-                    const uint64_t grp = __ballot(li == lj);
-                    uint32_t base = 0;
-                    if (lane == lead) base = atomicAdd(&a.ctl[1 + lj], (uint32_t)__popcll(grp));
-                    base = (uint32_t)__shfl((int)base, lead, 64);
-                    if (li == lj) {
-                        const uint32_t at = list_off[lj] + base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
-                        a.lkey[at] = key;
-                        a.lsize[at] = (uint32_t)(R[hp[i] - 1] - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
+            for (int i0 = 1; i0 < nh; i0 += 8) {  // 8 keys' loads in flight together
+                uint64_t k8[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) k8[j] = hk[min(i0 + j, nh - 1)];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int i = i0 + j;
+                    const uint64_t key = k8[j];
+                    const int li = i < nh ? binmap[pcrd_bin(key)] : -1;
+                    // one fill atomic per wave and list (a list's lanes take
+                    // consecutive slots): same-word atomics serialise in L2
+                    uint64_t todo = __ballot(li >= 0);
+                    while (todo) {
+                        const int lead = __builtin_ctzll(todo);
+                        const int lj = __shfl(li, lead, 64);
+                        const uint64_t grp = __ballot(li == lj);
+                        uint32_t base = 0;
+                        if (lane == lead) base = atomicAdd(&a.ctl[1 + lj], (uint32_t)__popcll(grp));
+                        base = (uint32_t)__shfl((int)base, lead, 64);
+                        if (li == lj) {
+                            const uint32_t at =
+                                list_off[lj] + base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+                            a.lkey[at] = key;
+                            a.lsize[at] = (uint32_t)(R[hp[i] - 1] - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
+                        }
+                        todo &= ~grp;
                     }
-                    todo &= ~grp;
                 }
             }
         }
-    // 3. publish (release, ticket); the last workgroup acquires and resolves
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t t = __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == gridDim.x - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    if (!last) return;
-    if (a.dbg && tid == 0) {
+}
+
+// 3. each layer in a workgroup of its own (grid = layers): the largest
+// candidate key v with (bytes above the bin) + (candidate bytes with key >= v)
+// > budget is the first key not taken, K' = v + 1.  Workgroup 0 also zeroes
+// the list fill counters for the next k_select (the device rate loop runs
+// several).
+__global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
+    __shared__ SelBins sh;
+    // the narrowing state and the survivors
+    __shared__ uint64_t rlo, rhi, rmax;
+    __shared__ int64_t rneed;
+    __shared__ uint32_t rcount;
+    __shared__ uint64_t bkey[kSelBrute];
+    __shared__ uint32_t bsize[kSelBrute];
+    __shared__ uint32_t hcnt[kPcrdBins];
+    const int tid = threadIdx.x, lane = tid & 63, l = blockIdx.x;
+    if (a.halt && *a.halt) return;
+    select_bins(a, sh);
+    uint64_t *wsum = sh.wsum;
+    const int *lbin = sh.lbin, *lli = sh.lli;
+    const int64_t *lneed = sh.lneed;
+    const uint32_t *list_off = sh.list_off;
+    const int nlist = sh.nlist;
+    if (l == 0 && tid <= nlist) a.ctl[tid] = 0u;  // (k_select has finished: stream order)
+    if (a.dbg && l == 0 && tid == 0) {
         a.dbg[0] = nlist;
         for (int i = 0; i < nlist; i++) a.dbg[1 + i] = list_off[i + 1] - list_off[i];
     }
-    // Each layer: the largest candidate key v with (bytes above the bin) +
-    // (candidate bytes with key >= v) > budget.  The key range is narrowed by
+    // The key range is narrowed by
     // 4096-way histograms (bytes and counts) over the candidates in range --
     // a bin is 2^47 keys wide, one round leaves a handful (a round starts
     // from the bin's own bounds and count: no pass for them) -- until at most
     // kSelBrute remain, whose totals are then summed directly.
-    uint64_t *hist = (uint64_t *)sfx;  // (the suffix sums are done with)
-    for (int l = 0; l < L; l++) {
+    uint64_t *hist = (uint64_t *)sh.sfx;  // (the suffix sums are done with)
+    {
         if (lbin[l] < 0) {
             if (tid == 0) a.K[l] = a.Kc[l] = 0ull;  // every segment fits
-            continue;
+            return;
         }
         const int li = lli[l];
         const uint32_t i0 = list_off[li], i1 = list_off[li + 1];
@@ -1338,7 +1405,6 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
                         a.dbg[65 + l] = cnt;
                     }
                 }
-                __syncthreads();
                 break;
             }
             // bytes and counts per 1/4096 of the key range; the sub-range the
@@ -1382,7 +1448,6 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
             __syncthreads();
         }
     }
-    if (tid <= nlist) a.ctl[tid] = 0u;  // ticket and fill counters, for the next launch
 }
 
 // Split path only (GpuEncoder::segments): every hull segment listed
@@ -1748,7 +1813,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<uint8_t>(nhull, nb, err)) return false;
     if (!ensure<uint8_t>(hpass, (size_t)nb * (kMaxPasses + 1), err)) return false;
     if (!ensure<uint64_t>(hkey, (size_t)nb * (kMaxPasses + 1), err)) return false;
-    if (!ensure<int64_t>(hdist, (size_t)nb * (kMaxPasses + 1), err)) return false;
+    if (!ensure<int64_t>(hdist, (size_t)nb * (kMaxPasses + 1) * 2, err)) return false;  // HullPt
     if (!ensure<int64_t>(budget, kMaxLayers, err)) return false;
     if (!ensure<uint8_t>(nl, (size_t)nb * plan.rc.layers, err)) return false;
     if (!ensure<int32_t>(lrate, (size_t)nb * plan.rc.layers, err)) return false;
@@ -2100,6 +2165,7 @@ void GpuEncoder::select_launch(const Plan &plan, const int *halt) {
     }
 #endif
     hipLaunchKernelGGL(k_select, dim3((nb + kSelThreads - 1) / kSelThreads), dim3(kSelThreads), 0, stream, sa);
+    hipLaunchKernelGGL(k_select_resolve, dim3(plan.rc.layers), dim3(kSelThreads), 0, stream, sa);
 }
 
 // lossless "-rate -": layer l's budget is total >> (L-1-l), total = every

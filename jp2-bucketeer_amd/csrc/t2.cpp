@@ -124,7 +124,6 @@ void t2_tables(const Plan &P, int tile0, int tile1, int block0, T2Tables &T) {
     T.tp.clear();
     T.tt_nodes = 0;
     T.max_prec_blocks = 0;
-    T.max_prec_nodes = 0;
     // tile-parts per tile, in tile order first
     std::vector<std::vector<TpDesc>> per_tile((size_t)std::max(0, tile1 - tile0));
     for (int t = tile0; t < tile1; t++) {
@@ -146,7 +145,6 @@ void t2_tables(const Plan &P, int tile0, int tile1, int block0, T2Tables &T) {
                         d.tt_off = (int32_t)T.tt_nodes;
                         d.nsop0 = nsop;
                         int blocks = 0;
-                        const int64_t nodes0 = T.tt_nodes;
                         for (int bi = 0; bi < pr.nb; bi++) {
                             const PrecBand &pb = pr.pb[bi];
                             d.first[bi] = pb.first - block0;
@@ -156,7 +154,6 @@ void t2_tables(const Plan &P, int tile0, int tile1, int block0, T2Tables &T) {
                             if (pb.ncw && pb.nch) T.tt_nodes += 2 * tree_nodes(pb.ncw, pb.nch);
                         }
                         T.max_prec_blocks = std::max(T.max_prec_blocks, blocks);
-                        T.max_prec_nodes = std::max(T.max_prec_nodes, (int)(T.tt_nodes - nodes0));
                         T.prec.push_back(d);
                         tp.nprec++;
                         nsop += L;

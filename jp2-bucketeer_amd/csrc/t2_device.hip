@@ -8,15 +8,16 @@
 // the oracle's (oracle/jp2_oracle.c encode_packet / write_codestream).
 //
 // Parallel structure.  A precinct's L packets share state (tag trees, each
-// block's Lblock and inclusion layer), so one lane codes one precinct's
-// packets in order; precincts are independent (C2: 2 880 per image, C5:
-// 51 153).  Sizing and emission run the same coder (template EMIT):
-//   k_t2_code<false>  header bytes + packet lengths        (every rate pass)
-//   k_t2_tparts       Psot / PLT bytes per tile-part       (every rate pass)
-//   k_t2_total        stream offsets, sums for the host    (every rate pass)
-//   k_t2_tp_emit      SOT + PLT + SOD, packet offsets      (final pass)
-//   k_t2_code<true>   SOP + header + EPH, body offsets     (final pass)
-//   k_t2_copy         code-block bytes into the bodies     (final pass)
+// block's Lblock and inclusion layer); precincts are independent (C2: 2 880
+// per image, C5: 51 153).  A wave codes a precinct, a lane per code-block,
+// with the tag trees in closed form (k_t2_wave); precincts of more than 64
+// blocks take the serial coder, a lane per precinct (k_t2_code + k_apply).
+// Sizing and emission run the same coder (template EMIT):
+//   k_t2_wave<false>  layer assignment, header bytes + packet lengths  (every rate pass)
+//   k_t2_total        tile-part sizes, stream offsets, sums for the host (every rate pass)
+//   k_t2_tp_emit      SOT + PLT + SOD, packet offsets                  (final pass)
+//   k_t2_wave<true>   SOP + header + EPH, body offsets                 (final pass)
+//   k_t2_copy         code-block bytes into the bodies                 (final pass)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -304,24 +305,39 @@ __global__ void __launch_bounds__(64) k_t2_code(T2Args a) {
 // --------------------------------------------------------------------------
 // k_t2_wave: one wave per precinct, lane j = the precinct's j-th code-block
 // (bands in order, raster order inside a band), for precincts of <= 64
-// blocks (the recipe's: at most 2 x 2 per band).  Per layer the lanes work
-// out, in parallel, everything of a block's contribution that is not a
-// tag-tree bit -- pass count codeword (Table B.4), Lblock increments, the
-// length field -- and lane 0 writes the header bits in block order (the tag
-// trees, whose nodes several blocks share, and the 0xFF bit stuffing are
-// serial by nature).  No global memory is touched inside the layer loop.
+// blocks (the recipe's: at most 2 x 2 per band).  Every header bit of a
+// packet is worked out by the lanes in parallel -- the tag-tree bits
+// included -- and laid out in LDS by a prefix sum of the lanes' bit counts;
+// the 0xFF bit stuffing then runs a lane per packet.  No global memory is
+// touched inside the layer loop.
+//
+// Tag trees in closed form (what tree_encode's walk amounts to; k_t2_code
+// keeps the walk).  Inclusion tree, packet l (threshold l+1): a leaf is
+// coded in every non-empty packet up to its inclusion layer, so a node is
+// visited in every non-empty packet up to the last of its leaves'; entering
+// packet l its state is low = min(v, tp), known = (v < tp), tp = 1 + the
+// last non-empty packet before l (0: none), and its parent leaves it the
+// lower bound min(pv, l+1) (pv <= v; the root's pv: 0).  Only the first
+// visiting leaf (block order) writes the node's bits: nz = min(v, l+1) -
+// max(min(v, tp), min(pv, l+1)) "0"s, then a "1" if tp <= v <= l.  The
+// nodes a leaf writes are a suffix of its root-to-leaf path, whose "0"s add
+// up to at most l+1.  Zero bit-plane tree (threshold unbounded), coded when
+// a leaf is first included: a node writes (v - pv) "0"s and a "1" on its
+// first visit ever, by the leaf of its subtree included first (earliest
+// layer, then block order); those nodes are a suffix of that leaf's
+// root-to-leaf path.
 // The sizing pass (EMIT = false) also assigns each block its passes per layer
 // from the thresholds K (what k_apply does for the serial kernel) and writes
 // nl / lrate for the emission pass and k_t2_copy.
 // --------------------------------------------------------------------------
-constexpr int kT2Waves = 4;  // precincts per workgroup
-constexpr int kWaveNodes = 256;  // tag-tree nodes of one k_t2_wave precinct (LDS)
+constexpr int kT2Waves = 4;     // precincts per workgroup
+constexpr int kTreeLev = 7;     // levels of a tag tree over <= 64 leaves
+constexpr int kBitWords = 512;  // pending packet headers in LDS, per wave
+constexpr int kWaveMaxMb = 48;  // a leaf's zero bit-plane path stays within 64 bits (host check)
 struct T2LaneShared {
-    uint8_t nl[kMaxLayers][64];     // cumulative passes per layer
-    int32_t lr[kMaxLayers][64];     // cumulative bytes per layer
-    uint8_t n[64], first[64];       // tree_set staging: zero bit-planes, first layer
-    uint32_t tt[kWaveNodes];        // tag-tree nodes (the host picks k_t2_wave only when they fit)
-    uint32_t hdr;                   // header bytes of the packet (lane 0 -> all)
+    uint8_t nl[kMaxLayers][64];  // cumulative passes per layer
+    int32_t lr[kMaxLayers][64];  // cumulative bytes per layer
+    uint32_t bits[kBitWords];    // header bits of the pending packets, MSB first, a zero word after each
 };
 
 // the lanes of one wave see each other's LDS writes in program order (the
@@ -333,14 +349,41 @@ __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("" ::: "memory");
 }
 
-// put up to 64 bits (nb <= 64) through the 32-bit-at-a-time writer
+// OR the nb (0..64) low bits of v, MSB first, into the LDS bit string at bit p
+__device__ __forceinline__ void lds_put_bits(uint32_t *buf, uint32_t p, uint64_t v, int nb) {
+    if (nb <= 0) return;
+    const uint64_t x = v << (64 - nb);
+    const int sh = (int)(p & 31u);
+    uint32_t *w = buf + (p >> 5);
+    const uint64_t hi = x >> sh;
+    const uint32_t w0 = (uint32_t)(hi >> 32), w1 = (uint32_t)hi, w2 = sh ? (uint32_t)((x << (64 - sh)) >> 32) : 0u;
+    if (w0) atomicOr(w, w0);
+    if (w1) atomicOr(w + 1, w1);
+    if (w2) atomicOr(w + 2, w2);
+}
+
+// B.10.1 bit stuffing of the header bit string [p0, p0 + nbits) (DevBits):
+// 8 bits a byte, 7 after an 0xFF, a 0 byte if it would end in 0xFF.  The
+// string is followed by a zero word, so the two-word window never reads
+// another packet's bits.  Returns the byte count (EMIT: bytes to o).
 template <bool EMIT>
-__device__ __forceinline__ void put64(DevBits<EMIT> &w, uint64_t v, int nb) {
-    if (nb > 32) {
-        w.put((uint32_t)(v >> 32), nb - 32);
-        nb = 32;
+__device__ __forceinline__ uint32_t stuff_header(const uint32_t *buf, uint32_t p0, uint32_t nbits, uint8_t *o) {
+    uint32_t q = 0, nbytes = 0, byte = 0;
+    int cap = 8;
+    while (q < nbits) {
+        const uint32_t p = p0 + q;
+        const uint64_t win = ((uint64_t)buf[p >> 5] << 32) | buf[(p >> 5) + 1];
+        byte = (uint32_t)(win >> (64 - cap - (int)(p & 31u))) & ((1u << cap) - 1u);
+        if (EMIT) o[nbytes] = (uint8_t)byte;
+        nbytes++;
+        q += (uint32_t)cap;
+        cap = byte == 0xFFu ? 7 : 8;
     }
-    if (nb > 0) w.put((uint32_t)v & (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)), nb);
+    if (byte == 0xFFu) {
+        if (EMIT) o[nbytes] = 0;
+        nbytes++;
+    }
+    return nbytes;
 }
 
 template <bool EMIT>
@@ -358,8 +401,12 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
     const int nbt = c0 + c1 + c2;
     const bool own = lane < nbt;
     const int bi = lane < c0 ? 0 : (lane < c0 + c1 ? 1 : 2);
-    const int leaf = lane - (bi == 0 ? 0 : (bi == 1 ? c0 : c0 + c1));
-    const int b = own ? d.first[bi] + leaf : 0;
+    const int leaf = own ? lane - (bi == 0 ? 0 : (bi == 1 ? c0 : c0 + c1)) : 0;
+    // (the band's fields by select: an indexed PrecDesc would live in scratch)
+    const int bfirst = bi == 0 ? d.first[0] : (bi == 1 ? d.first[1] : d.first[2]);
+    const int bcw = bi == 0 ? d.ncw[0] : (bi == 1 ? d.ncw[1] : d.ncw[2]);
+    const int bch = bi == 0 ? d.nch[0] : (bi == 1 ? d.nch[1] : d.nch[2]);
+    const int b = own ? bfirst + leaf : 0;
     int zero_planes = 0;
     if (own) {
         zero_planes = a.blocks[b].Mb - a.P[b];
@@ -383,7 +430,12 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
             // rate loads together (two load round trips per group, not two
             // per layer)
             int at = 0;  // last hull point with key >= K (point 0: nothing)
-            auto key = [&](int i) { return i < 8 ? k8[i] : hk[i]; };
+            auto key = [&](int i) {  // (k8 by select: an indexed k8 would live in scratch)
+                uint64_t r = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) r = i == t ? k8[t] : r;
+                return i < 8 ? r : hk[i];
+            };
             for (int l0 = 0; l0 < L; l0 += 8) {
                 int atv[8];
 #pragma unroll
@@ -423,115 +475,179 @@ __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
             }
         }
     }
-    // tag trees in LDS (an LDS pointer, so no flat access): inclusion layer
-    // and zero bit-planes of every leaf
-    int nodes = 0, toff[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        toff[k] = nodes;
-        if (k < d.nb && d.ncw[k] && d.nch[k]) nodes += 2 * tree_size(d.ncw[k], d.nch[k]);
-    }
-    uint32_t *tt = S.tt;
-    int firstl = L;
+    int firstl = L;  // inclusion layer (L: never)
     if (own)
         for (int l = 0; l < L; l++)
             if (S.nl[l][lane] > 0) {
                 firstl = l;
                 break;
             }
-    S.first[lane] = (uint8_t)firstl;
-    S.n[lane] = (uint8_t)zero_planes;  // (staged for lane 0's tree_set)
-    wave_lds_sync();
-    if (lane == 0) {
-        for (int i = 0; i < nodes; i++) tt[i] = 0xFFu;  // value 255 = unset, low 0, not known
-        for (int j = 0; j < nbt; j++) {
-            const int jb = j < c0 ? 0 : (j < c0 + c1 ? 1 : 2);
-            const int jl = j - (jb == 0 ? 0 : (jb == 1 ? c0 : c0 + c1));
-            const int w = d.ncw[jb], h = d.nch[jb];
-            uint32_t *ti = tt + toff[jb], *tz = ti + tree_size(w, h);
-            tree_set(ti, w, h, jl, S.first[j]);
-            tree_set(tz, w, h, jl, S.n[j]);
-        }
+    // the leaf's tag-tree path: per level the lanes under the same node, the
+    // node's inclusion and zero bit-plane values, and the node's first
+    // zero-bit-plane visitor (inclusion layer << 6 | lane)
+    const int cw0 = own ? bcw : 1, ch0 = own ? bch : 1;
+    const int lx = leaf % cw0, ly = leaf / cw0;
+    int nlev = 1;
+    for (int w = cw0, h = ch0; w != 1 || h != 1; w = (w + 1) >> 1, h = (h + 1) >> 1) nlev++;
+    const int key = (bi << 16) | (ly << 8) | lx;
+    uint64_t imask[kTreeLev];
+    int ival[kTreeLev], zval[kTreeLev], zbest[kTreeLev];
+#pragma unroll
+    for (int k = 0; k < kTreeLev; k++) {
+        imask[k] = 0;
+        ival[k] = L;
+        zval[k] = 255;
+        zbest[k] = 0x7FFFFFFF;
     }
+    for (int j = 0; j < nbt; j++) {
+        const int kj = __builtin_amdgcn_readlane(key, j);
+        const int fj = __builtin_amdgcn_readlane(firstl, j), zj = __builtin_amdgcn_readlane(zero_planes, j);
+        const int xj = kj & 0xFF, yj = (kj >> 8) & 0xFF;
+        const bool band = (kj >> 16) == bi;
+#pragma unroll
+        for (int k = 0; k < kTreeLev; k++)
+            if (band && (xj >> k) == (lx >> k) && (yj >> k) == (ly >> k)) {
+                imask[k] |= 1ull << j;
+                ival[k] = min(ival[k], fj);
+                zval[k] = min(zval[k], zj);
+                if (fj < L) zbest[k] = min(zbest[k], (fj << 6) | j);
+            }
+    }
+    const int myz = (firstl << 6) | lane;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t *buf = S.bits;
+    for (int i = lane; i < kBitWords; i += 64) buf[i] = 0;
     wave_lds_sync();
-    int incl = -1, lb = 3;  // the lane's block: inclusion layer, Lblock
+    int lb = 3;  // the lane's block: Lblock
     const uint32_t fixed = (a.sop ? 6u : 0u) + (a.eph ? 2u : 0u);
-    for (int l = 0; l < L; l++) {
-        // this block's part of packet l, all but the tag-tree bits
+    // pending packets [l0, l) occupy buf[0, used); lane i holds packet l0 + i's
+    // first word, bit count and body bytes (all wave-uniform but the lane ones)
+    uint32_t used = 0, pws = 0, pnb = 0, pbody = 0;
+    int l0 = 0;
+    int tp = 0;  // 1 + the last non-empty packet (wave-uniform)
+    for (int l = 0; l <= L; l++) {
         int n = 0, len = 0;
-        if (own) {
-            n = (int)S.nl[l][lane] - (l ? (int)S.nl[l - 1][lane] : 0);
-            len = S.lr[l][lane] - (l ? S.lr[l - 1][lane] : 0);
-        }
-        uint64_t p1v = 0;
-        int p1n = 0, p2n = 0;
-        const bool first_time = incl < 0;
-        if (n > 0) {
-            uint32_t cv;
-            int cn;
-            if (n == 1) { cv = 0u; cn = 1; }
-            else if (n == 2) { cv = 2u; cn = 2; }
-            else if (n <= 5) { cv = (3u << 2) | (uint32_t)(n - 3); cn = 4; }
-            else if (n <= 36) { cv = (15u << 5) | (uint32_t)(n - 6); cn = 9; }
-            else { cv = (511u << 7) | (uint32_t)(n - 37); cn = 16; }
-            const int nbits0 = lb + dev_floor_log2(n);
-            const int need = len > 0 ? 32 - __clz(len) : 0;  // bit length of len
-            const int extra = need > nbits0 ? need - nbits0 : 0;
-            lb += extra;
-            p1v = ((uint64_t)cv << (extra + 1)) | (((1ull << extra) - 1ull) << 1);
-            p1n = cn + extra + 1;
-            p2n = lb + dev_floor_log2(n);
-        }
-        const bool nonempty = __ballot(n > 0) != 0ull;
-        if (n > 0 && first_time) incl = l;
-        // body bytes before this block in the packet (blocks in order)
-        const int lin = n > 0 ? len : 0;
-        int body_before = (int)wave_incl_scan((uint32_t)lin) - lin;
-        const int body = __shfl(body_before + lin, 63, 64);
-        wave_lds_sync();
-        const size_t pk = (size_t)pi * L + l;
-        if (lane == 0) {
-            uint8_t *o = nullptr;
-            if (EMIT) {
-                o = a.out + a.pk_off[pk];
-                if (a.sop) {
-                    const uint32_t ns = (uint32_t)(d.nsop0 + l) & 0xFFFFu;
-                    o[0] = 0xFF; o[1] = 0x91; o[2] = 0; o[3] = 4; o[4] = (uint8_t)(ns >> 8); o[5] = (uint8_t)ns;
-                    o += 6;
+        uint64_t I = 0, Z = 0, p1v = 0;  // inclusion bits, zero bit-plane bits, pass count codeword
+        int nI = 0, nZ = 0, p1n = 0, p2n = 0;
+        uint32_t nbits = 0, need = 0, off = 0, body = 0;
+        if (l < L) {
+            // this block's part of packet l
+            if (own) {
+                n = (int)S.nl[l][lane] - (l ? (int)S.nl[l - 1][lane] : 0);
+                len = S.lr[l][lane] - (l ? S.lr[l - 1][lane] : 0);
+            }
+            if (n > 0) {
+                uint32_t cv;
+                int cn;
+                if (n == 1) { cv = 0u; cn = 1; }
+                else if (n == 2) { cv = 2u; cn = 2; }
+                else if (n <= 5) { cv = (3u << 2) | (uint32_t)(n - 3); cn = 4; }
+                else if (n <= 36) { cv = (15u << 5) | (uint32_t)(n - 6); cn = 9; }
+                else { cv = (511u << 7) | (uint32_t)(n - 37); cn = 16; }
+                const int nbits0 = lb + dev_floor_log2(n);
+                const int bl = len > 0 ? 32 - __clz(len) : 0;  // bit length of len
+                const int extra = bl > nbits0 ? bl - nbits0 : 0;
+                lb += extra;
+                p1v = ((uint64_t)cv << (extra + 1)) | (((1ull << extra) - 1ull) << 1);
+                p1n = cn + extra + 1;
+                p2n = lb + dev_floor_log2(n);
+            }
+            const bool nonempty = __ballot(n > 0) != 0ull;
+            const bool visitor = own && firstl >= l;  // not yet included: codes the inclusion tree
+            const uint64_t vis = __ballot(visitor);
+            if (nonempty && own) {
+                if (visitor) {
+#pragma unroll
+                    for (int k = kTreeLev - 1; k >= 0; k--) {
+                        if (k >= nlev || (imask[k] & vis & below)) continue;
+                        const int v = ival[k], pv = k + 1 < nlev ? ival[k + 1 < kTreeLev ? k + 1 : k] : 0;
+                        const int nz = max(0, min(v, l + 1) - max(min(v, tp), min(pv, l + 1)));
+                        const int one = (v >= tp && v <= l) ? 1 : 0;
+                        I = (I << (nz + one)) | (uint64_t)one;
+                        nI += nz + one;
+                    }
+                    if (n > 0)  // first inclusion: the zero bit-plane path
+#pragma unroll
+                        for (int k = kTreeLev - 1; k >= 0; k--) {
+                            if (k >= nlev || zbest[k] != myz) continue;
+                            const int z = zval[k] - (k + 1 < nlev ? zval[k + 1 < kTreeLev ? k + 1 : k] : 0);
+                            Z = (Z << (z + 1)) | 1u;
+                            nZ += z + 1;
+                        }
+                } else {
+                    I = n > 0 ? 1u : 0u;
+                    nI = 1;
                 }
             }
-            DevBits<EMIT> w;
-            w.init(o);
-            w.bit(nonempty ? 1 : 0);
-            if (nonempty)
-                for (int j = 0; j < nbt; j++) {
-                    const int jb = j < c0 ? 0 : (j < c0 + c1 ? 1 : 2);
-                    const int jl = j - (jb == 0 ? 0 : (jb == 1 ? c0 : c0 + c1));
-                    const int cw = d.ncw[jb], ch = d.nch[jb];
-                    uint32_t *ti = tt + toff[jb], *tz = ti + tree_size(cw, ch);
-                    // block j's fields from lane j's registers (no LDS round trip)
-                    const int nj = __builtin_amdgcn_readlane(n, j);
-                    const bool ft = __builtin_amdgcn_readlane(first_time ? 1 : 0, j) != 0;
-                    if (ft) tree_encode(ti, cw, ch, jl, l + 1, w);
-                    else w.bit(nj > 0 ? 1 : 0);
-                    if (nj <= 0) continue;
-                    if (ft) tree_encode(tz, cw, ch, jl, 1 << 20, w);
-                    const uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(p1v >> 32), j) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)p1v, j);
-                    put64(w, pv, __builtin_amdgcn_readlane(p1n, j));
-                    put64(w, (uint64_t)(uint32_t)__builtin_amdgcn_readlane(len, j), __builtin_amdgcn_readlane(p2n, j));
-                }
-            w.flush();
-            if (EMIT) {
-                if (a.eph) { o[w.nbytes] = 0xFF; o[w.nbytes + 1] = 0x92; }
-                S.hdr = (a.sop ? 6u : 0u) + w.nbytes + (a.eph ? 2u : 0u);
-            } else {
-                a.pk_len[pk] = fixed + w.nbytes + (uint32_t)body;
-            }
+            if (nonempty) tp = l + 1;
+            const uint32_t T = (uint32_t)(nI + nZ + p1n + p2n);
+            off = wave_incl_scan(T) - T;
+            nbits = 1u + (uint32_t)__shfl((int)(off + T), 63, 64);
+            const uint32_t lin = n > 0 ? (uint32_t)len : 0u;
+            body = (uint32_t)__shfl((int)wave_incl_scan(lin), 63, 64);
+            need = (nbits + 31u) / 32u + 1u;  // + the zero word
+            if (!nonempty) nbits = 1;
         }
-        wave_lds_sync();
-        // body pieces follow the header, in block order
-        if (EMIT && n > 0) a.blkdst[(size_t)b * L + l] = a.pk_off[pk] + S.hdr + (uint64_t)body_before;
+        if (l == L || used + need > (uint32_t)kBitWords) {
+            // stuff the pending packets, a lane each
+            wave_lds_sync();
+            uint32_t hdr = 0;
+            if (lane < l - l0) {
+                const size_t pk = (size_t)pi * L + l0 + lane;
+                uint8_t *o = nullptr;
+                if (EMIT) {
+                    o = a.out + a.pk_off[pk];
+                    if (a.sop) {
+                        const uint32_t ns = (uint32_t)(d.nsop0 + l0 + lane) & 0xFFFFu;
+                        o[0] = 0xFF; o[1] = 0x91; o[2] = 0; o[3] = 4; o[4] = (uint8_t)(ns >> 8); o[5] = (uint8_t)ns;
+                        o += 6;
+                    }
+                }
+                const uint32_t nbytes = stuff_header<EMIT>(buf, pws * 32u, pnb, o);
+                if (EMIT) {
+                    if (a.eph) { o[nbytes] = 0xFF; o[nbytes + 1] = 0x92; }
+                    hdr = fixed + nbytes;
+                } else {
+                    a.pk_len[pk] = fixed + nbytes + pbody;
+                }
+            }
+            if (EMIT)  // body pieces follow each header, in block order
+                for (int l2 = l0; l2 < l; l2++) {
+                    int n2 = 0, len2 = 0;
+                    if (own) {
+                        n2 = (int)S.nl[l2][lane] - (l2 ? (int)S.nl[l2 - 1][lane] : 0);
+                        len2 = S.lr[l2][lane] - (l2 ? S.lr[l2 - 1][lane] : 0);
+                    }
+                    const uint32_t lin2 = n2 > 0 ? (uint32_t)len2 : 0u;
+                    const uint32_t before = wave_incl_scan(lin2) - lin2;
+                    const uint32_t h2 = (uint32_t)__builtin_amdgcn_readlane((int)hdr, l2 - l0);
+                    const size_t pk2 = (size_t)pi * L + l2;
+                    if (n2 > 0) a.blkdst[(size_t)b * L + l2] = a.pk_off[pk2] + h2 + before;
+                }
+            wave_lds_sync();
+            for (uint32_t i = lane; i < used; i += 64) buf[i] = 0;
+            wave_lds_sync();
+            used = 0;
+            l0 = l;
+            if (l == L) break;
+        }
+        // packet l at buf[used]: the "packet present" bit, then each block's bits
+        const uint32_t p = used * 32u;
+        if (lane == 0 && nbits > 1) atomicOr(&buf[used], 0x80000000u);
+        uint32_t q = p + 1u + off;
+        lds_put_bits(buf, q, I, nI);
+        q += (uint32_t)nI;
+        lds_put_bits(buf, q, Z, nZ);
+        q += (uint32_t)nZ;
+        lds_put_bits(buf, q, p1v, p1n);
+        q += (uint32_t)p1n;
+        lds_put_bits(buf, q, (uint64_t)(uint32_t)len, p2n);
+        if (lane == l - l0) {
+            pws = used;
+            pnb = nbits;
+            pbody = body;
+        }
+        used += need;
     }
 }
 
@@ -831,7 +947,10 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
     const int L = plan.rc.layers;
     t2_nprec = (int)T.prec.size();
     t2_ntp = (int)T.tp.size();
-    t2_wave = T.max_prec_blocks <= 64 && T.max_prec_nodes <= kWaveNodes;  // k_t2_wave (else the serial k_t2_code + k_apply)
+    // k_t2_wave (else the serial k_t2_code + k_apply)
+    int max_mb = 0;
+    for (const BlockDesc &bd : plan.blocks) max_mb = std::max(max_mb, (int)bd.Mb);
+    t2_wave = T.max_prec_blocks <= 64 && max_mb <= kWaveMaxMb;
     const size_t npk = (size_t)t2_nprec * L;
     if (!ensure_t2<PrecDesc>(t2prec, T.prec.size(), err) || !ensure_t2<TpDesc>(t2tp, T.tp.size(), err) ||
         !ensure_t2<uint32_t>(t2tt, (size_t)T.tt_nodes, err) || !ensure_t2<int8_t>(t2lblock, nb, err) ||
