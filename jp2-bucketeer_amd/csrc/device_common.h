@@ -157,11 +157,20 @@ __device__ __forceinline__ void rate_step(RateState *rs, const T2Summary *sum, i
 }
 
 // Files each block's coded planes in k_t1_cm3's per-depth work lists
-// (T1ItemArgs, gpu_encoder.h); called by every lane of a thread-per-block
-// kernel (`valid` false past the last block), one atomic per wave and depth.
-template <typename ItemArgs>
-__device__ __forceinline__ void emit_t1_items(const ItemArgs &a, int b, bool valid, int P, int pmin) {
-    const int lane = threadIdx.x & 63;
+// (T1ItemArgs, gpu_encoder.h); called by every thread of a thread-per-block
+// kernel of NT threads (`valid` false past the last block).  The workgroup
+// counts its entries per depth (a ballot per wave and depth), one lane per
+// depth reserves the workgroup's run of each list with one atomic -- all
+// depths' atomics in flight together, not one round trip per depth and wave
+// -- and every block writes its entries at its rank inside the run.
+struct ItemScratch {
+    uint32_t cnt[16][64];  // [wave][depth] entries; then the wave's offset in the list
+};
+template <int NT, typename ItemArgs>
+__device__ __forceinline__ void emit_t1_items(const ItemArgs &a, int b, bool valid, int P, int pmin, ItemScratch &sc) {
+    static_assert(NT % 64 == 0 && NT / 64 <= 16, "emit_t1_items: 64..1024 threads");
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t c = valid ? (uint32_t)(P - pmin) : 0u;
     if (valid) {
         a.acc[b] = (unsigned long long)c << 40;
@@ -175,13 +184,32 @@ __device__ __forceinline__ void emit_t1_items(const ItemArgs &a, int b, bool val
     for (int o = 32; o > 0; o >>= 1) cw = max(cw, (uint32_t)__shfl_xor((int)cw, o, 64));
     const int kw = min(__builtin_amdgcn_readfirstlane((int)cw), a.kmax);
     const uint64_t lt = (1ull << lane) - 1ull;
+    // this wave's entries per depth (depths >= kw: none)
+    for (int k = lane; k < 64; k += 64) sc.cnt[wv][k] = 0u;
     for (int k = 0; k < kw; k++) {
         const uint64_t m = __ballot(c > (uint32_t)k);
-        const int leader = __builtin_ctzll(m);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.dfill[k], (uint32_t)__popcll(m));
-        base = (uint32_t)__shfl((int)base, leader, 64);
-        if (c > (uint32_t)k) a.dlist[(size_t)k * a.nb + base + (uint32_t)__popcll(m & lt)] = b;
+        if (lane == 0) sc.cnt[wv][k] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // lane k: depth k's run for the workgroup
+        const int k = threadIdx.x;
+        uint32_t tot = 0, wc[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            wc[w] = sc.cnt[w][k];
+            tot += wc[w];
+        }
+        uint32_t base = (tot && k < a.kmax) ? atomicAdd(&a.dfill[k], tot) : 0u;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            sc.cnt[w][k] = base;
+            base += wc[w];
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < kw; k++) {
+        const uint64_t m = __ballot(c > (uint32_t)k);
+        if (c > (uint32_t)k) a.dlist[(size_t)k * a.nb + sc.cnt[wv][k] + (uint32_t)__popcll(m & lt)] = b;
     }
 }
 

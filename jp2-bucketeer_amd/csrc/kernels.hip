@@ -935,12 +935,9 @@ __device__ __forceinline__ int plane_cut(const unsigned long long *hist, int64_t
 #pragma unroll
     for (int i = 0; i < kPer; i++) { h[i] = hist[lane * kPer + i]; part += h[i]; }
     // exclusive suffix sum over lanes: bins above this lane's range
-    unsigned long long above = 0;
-    for (int o = 1; o < 64; o++) {
-        const int src = lane + o;
-        const unsigned long long v = (unsigned long long)__shfl((long long)part, src < 64 ? src : 63, 64);
-        above += src < 64 ? v : 0ull;
-    }
+    const uint64_t inc = wave_incl_scan64(part);
+    const unsigned long long above =
+        (uint64_t)__shfl((long long)inc, 63, 64) - inc;
     int cnt = 0;
     unsigned long long acc = above;
 #pragma unroll
@@ -958,6 +955,7 @@ __device__ __forceinline__ int plane_cut(const unsigned long long *hist, int64_t
 // (every workgroup finds the cut from the histogram itself: no launch for it)
 __global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a, T1ItemArgs ia, int64_t goal) {
     __shared__ int kcut;
+    __shared__ ItemScratch sc;
     if (threadIdx.x < 64) {
         const int kc = plane_cut(a.hist, goal);
         if (threadIdx.x == 0) kcut = kc;
@@ -990,7 +988,7 @@ __global__ void __launch_bounds__(256) k_plane_pmin(PredictArgs a, T1ItemArgs ia
         }
         a.pmin[b] = (uint8_t)pmin;
     }
-    emit_t1_items(ia, b, in, P, pmin);
+    emit_t1_items<256>(ia, b, in, P, pmin, sc);
 }
 
 // --------------------------------------------------------------------------

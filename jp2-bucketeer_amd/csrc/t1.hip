@@ -925,11 +925,12 @@ void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
 }
 // no slope prediction: every plane coded (pmin = 0), the work lists filled
 __global__ void __launch_bounds__(256) k_t1_items(T1ItemArgs a) {
+    __shared__ ItemScratch sc;
     const int b = blockIdx.x * 256 + threadIdx.x;
     const bool in = b < a.nb;
     const int P = in ? a.P[b] : 0;
     if (in) a.pmin[b] = 0;
-    emit_t1_items(a, b, in, P, 0);
+    emit_t1_items<256>(a, b, in, P, 0, sc);
 }
 void launch_t1_items(const T1ItemArgs &a, hipStream_t st) {
     if (a.nb > 0) hipLaunchKernelGGL(k_t1_items, dim3((a.nb + 255) / 256), dim3(256), 0, st, a);
