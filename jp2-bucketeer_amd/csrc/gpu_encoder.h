@@ -187,7 +187,7 @@ class GpuEncoder {
     // debug: JP2HIP_DUMP_DIR=<dir> writes every stage's device buffer
     bool dump(const char *dir, const char *name, const DevBuf &b, size_t bytes, std::string &err);
     bool apply_thresholds(const Plan &plan, const int *halt, std::string &err);
-    void select_launch(const Plan &plan, const int *halt);
+    void select_launch(const Plan &plan, const int *halt, const RateState *init = nullptr, RateState *rs = nullptr);
     T2Args t2_args(const Plan &plan) const;
     // tier-2 sizing; with rs (device rate loop) k_t2_total also runs the
     // loop's step, leaving state + summary at out_rs (host-mapped)
@@ -219,7 +219,7 @@ class GpuEncoder {
     // fills, candidate lists
     DevBuf pcrd_hb, pcrd_hc, sel_ctl, sel_key, sel_size;
     // device tier-2 (t2_device.hip)
-    DevBuf hdist, rstate;
+    DevBuf hdist, rstate, t2ticket;
     RateState *h_rs = nullptr;      // host-mapped: rate state, then the T2Summary (k_rate_step)
     RateState *d_rs_out = nullptr;  // its device address
     DevBuf t2prec, t2tp, t2tt, t2lblock, t2incl, t2pklen, t2pkoff, t2tplen, t2tphdr, t2tpoff, t2blkdst, t2out, t2sum;

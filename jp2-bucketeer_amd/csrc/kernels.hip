@@ -1010,6 +1010,13 @@ struct HullArgs {
     int64_t *hdist;   // [block][kMaxPasses+1] HullPt: the stack's distortion and rate at each point
     unsigned long long *hbytes;  // [kPcrdBins] segment bytes per slope bin (zeroed by k_quant)
     uint32_t *hcount;            // [kPcrdBins] segments per slope bin
+    // the tier-1 totals of T2Summary (t1_bytes, coded_passes, decisions,
+    // skipped; zeroed by k_quant), summed here once per encode instead of by
+    // every rate iteration's totals
+    const int32_t *lengths;
+    const unsigned long long *acc;
+    const uint8_t *pmin;
+    T2Summary *sum;
 };
 
 // slope-key bin: monotone in the key (positive doubles order like their bits)
@@ -1124,7 +1131,25 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
     }
     __syncthreads();
     const int b = blockIdx.x * kHullThreads + threadIdx.x;
-    if (b < a.nblocks) hull_one(a, b, lb, lc);
+    int64_t tb = 0, tp = 0, nd = 0;
+    bool sk = false;
+    if (b < a.nblocks) {
+        hull_one(a, b, lb, lc);
+        tb = a.lengths[b];
+        tp = a.npasses[b];
+        nd = (int64_t)(a.acc[b] & ((1ull << 40) - 1ull));  // decisions (k_t1_cm3)
+        sk = a.pmin[b] > 0;
+    }
+    tb = wave_sum64(tb);
+    tp = wave_sum64(tp);
+    nd = wave_sum64(nd);
+    sk = __any(sk);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd((unsigned long long *)&a.sum->t1_bytes, (unsigned long long)tb);
+        atomicAdd((unsigned long long *)&a.sum->coded_passes, (unsigned long long)tp);
+        atomicAdd((unsigned long long *)&a.sum->decisions, (unsigned long long)nd);
+        if (sk) atomicOr(&a.sum->skipped, 1);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < kPcrdBins; i += kHullThreads)
         if (lc[i]) {
@@ -1154,6 +1179,13 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
 // k_select_resolve for the next k_select (the device rate loop runs several).
 struct SelectArgs {
     const int *halt;  // device rate loop: nothing to do once it has stopped
+    // device rate loop, first iteration: the budgets come from `init` (every
+    // workgroup derives them), and k_select's workgroup 0 writes the loop's
+    // state and budgets (what a separate init launch did)
+    int init_on;
+    RateState init;
+    RateState *rs;
+    int64_t *budget_w;
     int nblocks, layers;
     const uint8_t *nhull, *hpass;
     const uint64_t *hkey;
@@ -1209,7 +1241,8 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
     __syncthreads();
     if (tid < L) {
         // (a negative budget takes nothing, as 0 does: every segment has bytes)
-        const int64_t T = a.budget[tid] < 0 ? 0 : a.budget[tid];
+        const int64_t B = a.init_on ? (a.init.budget < 0 ? 0 : a.init.budget) >> (L - 1 - tid) : a.budget[tid];
+        const int64_t T = B < 0 ? 0 : B;
         int b = -1;
         if ((int64_t)sfx[0] > T) {  // the largest bin b with S(b) > T
             int lo = 0, hi = kPcrdBins - 1;
@@ -1249,7 +1282,18 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
 __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
     __shared__ SelBins sh;
     const int tid = threadIdx.x, lane = tid & 63;
-    if (a.halt && *a.halt) return;
+    if (!a.init_on && a.halt && *a.halt) return;
+    if (a.init_on && blockIdx.x == 0 && tid == 0) {  // the rate loop's state (rate_step continues it)
+        RateState r = a.init;
+        r.it = 0;
+        r.halt = 0;
+        r.safety = 0;
+        r.iters = 0;
+        r.cs_bytes = 0;
+        if (r.budget < 0) r.budget = 0;
+        *a.rs = r;
+        rate_budgets(r, a.layers, a.budget_w);
+    }
     select_bins(a, sh);
     const int8_t *binmap = sh.binmap;
     const uint32_t *list_off = sh.list_off;
@@ -1308,7 +1352,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
     __shared__ uint32_t bsize[kSelBrute];
     __shared__ uint32_t hcnt[kPcrdBins];
     const int tid = threadIdx.x, lane = tid & 63, l = blockIdx.x;
-    if (a.halt && *a.halt) return;
+    if (a.halt && *a.halt) return;  // (k_select has reset it on a first iteration)
     select_bins(a, sh);
     uint64_t *wsum = sh.wsum;
     const int *lbin = sh.lbin, *lli = sh.lli;
@@ -1594,7 +1638,7 @@ GpuEncoder::~GpuEncoder() {
                      &segval, &thr, &items, &slotoff, &pcrd_hb, &pcrd_hc, &sel_ctl, &sel_key, &sel_size,
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
-                     &t2blkdst, &t2out, &t2sum, &hdist, &rstate,
+                     &t2blkdst, &t2out, &t2sum, &hdist, &rstate, &t2ticket,
                      &t1fill, &dbgsel};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
@@ -1854,7 +1898,11 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         front_gen = plan.gen;
     }
     // (the error word is zeroed by k_quant, which every encode with blocks runs)
-    if (!nb) HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
+    if (!nb) {
+        HIPCHECK(hipMemsetAsync(this->err.ptr, 0, sizeof(int), stream));
+        if (!ensure<T2Summary>(t2sum, 1, err)) return false;
+        HIPCHECK(hipMemsetAsync(t2sum.ptr, 0, sizeof(T2Summary), stream));  // (k_hull's totals: none)
+    }
 
     HIPCHECK(hipEventRecord(ev[0], stream));
     HIPCHECK(hipEventRecord(ev[1], stream));
@@ -1949,6 +1997,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.nzero[4] = 4;
     qa.zero[5] = (uint32_t *)this->err.ptr;
     qa.nzero[5] = 1;
+    // the tier-1 totals k_hull sums (t1_bytes .. skipped: contiguous)
+    if (!ensure<T2Summary>(t2sum, 1, err)) return false;
+    qa.zero[7] = (uint32_t *)&((T2Summary *)t2sum.ptr)->t1_bytes;
+    qa.nzero[7] = (uint32_t)((offsetof(T2Summary, skipped) + sizeof(int32_t) - offsetof(T2Summary, t1_bytes)) / 4);
     if (skip_target > 0) {
         if (!ensure<unsigned long long>(hist, kSlopeBins, err)) return false;
         qa.zero[6] = (uint32_t *)hist.ptr;
@@ -2076,6 +2128,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ha.hdist = (int64_t *)hdist.ptr;
     ha.hbytes = (unsigned long long *)pcrd_hb.ptr;
     ha.hcount = (uint32_t *)pcrd_hc.ptr;
+    ha.lengths = (const int32_t *)lengths.ptr;
+    ha.acc = (const unsigned long long *)ordkey.ptr;
+    ha.pmin = (const uint8_t *)pmin.ptr;
+    ha.sum = (T2Summary *)t2sum.ptr;
     REPEAT_IF(4) if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + kHullThreads - 1) / kHullThreads), dim3(kHullThreads), 0, stream, ha);
     HIPCHECK(hipGetLastError());
     // candidate lists: room for every hull segment (the bound sum(3 Mb - 2))
@@ -2136,7 +2192,7 @@ bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets, s
 }
 
 // k_select for the budgets in `budget` (thresholds -> thr[0..L), Kc -> thr[kMaxLayers..))
-void GpuEncoder::select_launch(const Plan &plan, const int *halt) {
+void GpuEncoder::select_launch(const Plan &plan, const int *halt, const RateState *init, RateState *rs) {
     const int nb = (int)plan.blocks.size();
     if (!nb) return;
     SelectArgs sa;
@@ -2155,6 +2211,10 @@ void GpuEncoder::select_launch(const Plan &plan, const int *halt) {
     sa.ctl = (uint32_t *)sel_ctl.ptr;
     sa.K = (uint64_t *)thr.ptr;
     sa.Kc = (uint64_t *)thr.ptr + kMaxLayers;
+    sa.init_on = init != nullptr;
+    if (init) sa.init = *init;
+    sa.rs = rs;
+    sa.budget_w = (int64_t *)budget.ptr;
     sa.dbg = nullptr;
 #ifdef JP2HIP_DEBUG_DUMPS
     if (getenv("JP2HIP_DUMP_DIR")) {
@@ -2224,23 +2284,13 @@ bool GpuEncoder::apply_thresholds(const Plan &plan, const int *halt, std::string
     return true;
 }
 
-// Device rate loop (RateState, jp2hip_internal.h; the step itself is
-// rate_step in device_common.h, run by k_t2_total)
-__global__ void k_rate_init(RateState *rs, RateState init, int L, int64_t *budget) {
-    RateState r = init;
-    r.it = 0;
-    r.halt = 0;
-    r.safety = 0;
-    r.iters = 0;
-    r.cs_bytes = 0;
-    if (r.budget < 0) r.budget = 0;
-    *rs = r;
-    rate_budgets(r, L, budget);
-}
+// Device rate loop (RateState, jp2hip_internal.h): the first k_select of a
+// restart writes the initial state; the step itself is rate_step in
+// device_common.h, run by the sizing totals (t2_total_body: the last
+// workgroup of k_t2_wave<false>, or k_t2_total)
 bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart, int batch, bool profile,
                            StageTimes &st, RateState &rs, T2Summary &sum, std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    const int L = plan.rc.layers;
     if (!ensure<RateState>(rstate, 1, err)) return false;
     if (!h_rs) {  // host-mapped: k_rate_step writes the state and summary here
         HIPCHECK(hipHostMalloc((void **)&h_rs, sizeof(RateState) + sizeof(T2Summary), hipHostMallocMapped));
@@ -2251,10 +2301,10 @@ bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart
     RateState *d = (RateState *)rstate.ptr;
     const int *halt = &d->halt;
     HIPCHECK(hipEventRecord(ev[6], stream));
-    if (restart) hipLaunchKernelGGL(k_rate_init, dim3(1), dim3(1), 0, stream, d, init, L, (int64_t *)budget.ptr);
     (void)o_sum;
     for (int i = 0; i < batch; i++) {
-        select_launch(plan, halt);
+        // (the first k_select of a restart also initialises the loop's state)
+        select_launch(plan, halt, (restart && i == 0) ? &init : nullptr, d);
         if (!apply_thresholds(plan, halt, err)) return false;
         t2_size_launch(plan, true, halt, d, o_rs);
     }

@@ -386,13 +386,10 @@ __device__ __forceinline__ uint32_t stuff_header(const uint32_t *buf, uint32_t p
     return nbytes;
 }
 
+// precinct pi's L packets, by one wave (k_t2_wave)
 template <bool EMIT>
-__global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a) {
-    __shared__ T2LaneShared lds[kT2Waves];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int pi = blockIdx.x * kT2Waves + wv;
-    if (pi >= a.nprec || (!EMIT && a.halt && *a.halt)) return;  // (wave-uniform)
-    T2LaneShared &S = lds[wv];
+__device__ __forceinline__ void t2_wave_precinct(const T2Args &a, T2LaneShared &S, int pi) {
+    const int lane = threadIdx.x & 63;
     const PrecDesc d = a.prec[pi];
     const int L = a.L;
     // lane -> (band, leaf, block)
@@ -701,25 +698,41 @@ __device__ __forceinline__ void tpart_size(const T2Args &a, int t) {
 // the host needs as per-thread partials reduced through one LDS table (a wave
 // sum each, then the waves' partials): no thread walks a serial loop over
 // the others' results.
-constexpr int kTotThreads = 1024, kTotWaves = kTotThreads / 64;
 constexpr int kTotSums = kMaxLayers + 5;  // layers, tp headers, t1 bytes, passes, decisions, skipped
-__global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, int nblocks, const int32_t *lengths,
-                                                          const uint8_t *npasses, const uint8_t *pmin, const int *t1err,
-                                                          const uint64_t *kc, const unsigned long long *acc,
-                                                          T2Summary *sum, RateStepArgs rate) {
-    __shared__ uint64_t wsum[kTotWaves + 1];
-    __shared__ int64_t red[kTotWaves][kTotSums];
-    if (a.halt && *a.halt) return;  // the whole workgroup
+// what the sizing totals read besides T2Args
+struct T2TotalArgs {
+    int nblocks;
+    const int32_t *lengths;
+    const uint8_t *npasses, *pmin;
+    const int *t1err;
+    const uint64_t *kc;
+    const unsigned long long *acc;
+    T2Summary *sum;
+    RateStepArgs rate;
+    uint32_t *ticket;  // k_t2_wave<false> with the totals fused: arrival counter (left 0)
+};
+
+// One workgroup of NT threads: tile-part sizes (a thread per tile-part, or a
+// contiguous run of them), their offsets by a workgroup scan, and every sum
+// the host needs as per-thread partials reduced through one LDS table (a wave
+// sum each, then the waves' partials): no thread walks a serial loop over
+// the others' results.  Run by k_t2_total, or by the last workgroup of
+// k_t2_wave<false> to arrive.  T1: also the tier-1 totals (k_hull has
+// already summed them into *sum once per encode; k_t2_total re-sums them).
+template <int NT, bool T1>
+__device__ __forceinline__ void t2_total_body(const T2Args &a, const T2TotalArgs &ta, uint64_t *wsum,
+                                              int64_t (*red)[kTotSums]) {
+    constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int L = a.L;
-    const int chunk = (a.ntp + kTotThreads - 1) / kTotThreads;
+    const int chunk = (a.ntp + NT - 1) / NT;
     const int t0 = min(a.ntp, tid * chunk), t1 = min(a.ntp, t0 + chunk);
     for (int t = t0; t < t1; t++) tpart_size(a, t);
     uint64_t s = 0, hdr = 0;
     for (int t = t0; t < t1; t++) s += a.tp_len[t];
     uint64_t tot;
-    uint64_t o = wg_excl_scan64<kTotThreads>(s, wsum, tot);
-    if (tid == 0) sum->part_bytes = (int64_t)tot;
+    uint64_t o = wg_excl_scan64<NT>(s, wsum, tot);
+    if (tid == 0) ta.sum->part_bytes = (int64_t)tot;
     for (int t = t0; t < t1; t++) {
         a.tp_off[t] = o;
         o += a.tp_len[t];
@@ -729,7 +742,7 @@ __global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, int nblocks,
     int64_t lay[kMaxLayers];
 #pragma unroll
     for (int l = 0; l < kMaxLayers; l++) lay[l] = 0;
-    for (int pq = tid; pq < a.nprec; pq += kTotThreads) {
+    for (int pq = tid; pq < a.nprec; pq += NT) {
         const uint32_t *pl = a.pk_len + (size_t)pq * L;
 #pragma unroll
         for (int l = 0; l < kMaxLayers; l++)
@@ -738,21 +751,22 @@ __global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, int nblocks,
     // tier-1 totals (acc: decisions per block in the low 40 bits, k_t1_cm3),
     // 4 blocks' loads in flight per thread
     int64_t tb = 0, tp = 0, nd = 0, skipped = 0;
-    for (int b0 = 0; b0 < nblocks; b0 += 4 * kTotThreads) {
+    if (T1)
+    for (int b0 = 0; b0 < ta.nblocks; b0 += 4 * NT) {
         int32_t ln[4];
         uint32_t np[4], pm[4];
         unsigned long long kk[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int b = min(b0 + u * kTotThreads + tid, nblocks - 1);
-            ln[u] = lengths[b];
-            np[u] = npasses[b];
-            kk[u] = acc[b];
-            pm[u] = pmin[b];
+            const int b = min(b0 + u * NT + tid, ta.nblocks - 1);
+            ln[u] = ta.lengths[b];
+            np[u] = ta.npasses[b];
+            kk[u] = ta.acc[b];
+            pm[u] = ta.pmin[b];
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)
-            if (b0 + u * kTotThreads + tid < nblocks) {
+            if (b0 + u * NT + tid < ta.nblocks) {
                 tb += ln[u];
                 tp += np[u];
                 nd += (int64_t)(kk[u] & ((1ull << 40) - 1ull));
@@ -768,28 +782,72 @@ __global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, int nblocks,
     for (int l = 0; l < kMaxLayers; l++)
         if (l < L) wave_put(l, lay[l]);
     wave_put(kMaxLayers + 0, (int64_t)hdr);
-    wave_put(kMaxLayers + 1, tb);
-    wave_put(kMaxLayers + 2, tp);
-    wave_put(kMaxLayers + 3, nd);
-    wave_put(kMaxLayers + 4, skipped);
+    if (T1) {
+        wave_put(kMaxLayers + 1, tb);
+        wave_put(kMaxLayers + 2, tp);
+        wave_put(kMaxLayers + 3, nd);
+        wave_put(kMaxLayers + 4, skipped);
+    }
     __syncthreads();
-    if (tid < kTotSums && (tid >= kMaxLayers || tid < L)) {
+    if (tid < (T1 ? kTotSums : kMaxLayers + 1) && (tid >= kMaxLayers || tid < L)) {
         int64_t v = 0;
 #pragma unroll
-        for (int w = 0; w < kTotWaves; w++) v += red[w][tid];
-        if (tid < kMaxLayers) sum->layer_bytes[tid] = v;
-        else if (tid == kMaxLayers + 0) sum->tp_hdr_bytes = v;
-        else if (tid == kMaxLayers + 1) sum->t1_bytes = v;
-        else if (tid == kMaxLayers + 2) sum->coded_passes = v;
-        else if (tid == kMaxLayers + 3) sum->decisions = v;
-        else sum->skipped = v != 0;
+        for (int w = 0; w < NW; w++) v += red[w][tid];
+        if (tid < kMaxLayers) ta.sum->layer_bytes[tid] = v;
+        else if (tid == kMaxLayers + 0) ta.sum->tp_hdr_bytes = v;
+        else if (tid == kMaxLayers + 1) ta.sum->t1_bytes = v;
+        else if (tid == kMaxLayers + 2) ta.sum->coded_passes = v;
+        else if (tid == kMaxLayers + 3) ta.sum->decisions = v;
+        else ta.sum->skipped = v != 0;
     }
-    if (tid < L) sum->kc[tid] = kc ? kc[tid] : 0ull;
-    if (tid == 0) sum->err = *t1err;
-    if (rate.rs) {
+    if (tid < L) ta.sum->kc[tid] = ta.kc ? ta.kc[tid] : 0ull;
+    if (tid == 0) ta.sum->err = *ta.t1err;
+    if (ta.rate.rs) {
         __syncthreads();  // every field of *sum written
-        if (tid == 0) rate_step(rate.rs, sum, L, rate.budget, rate.out_rs, rate.out_sum);
+        if (tid == 0) rate_step(ta.rate.rs, ta.sum, L, ta.rate.budget, ta.rate.out_rs, ta.rate.out_sum);
     }
+}
+
+constexpr int kTotThreads = 1024, kTotWaves = kTotThreads / 64;
+__global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, T2TotalArgs ta) {
+    __shared__ uint64_t wsum[kTotWaves + 1];
+    __shared__ int64_t red[kTotWaves][kTotSums];
+    if (a.halt && *a.halt) return;  // the whole workgroup
+    t2_total_body<kTotThreads, true>(a, ta, wsum, red);
+}
+
+// Packets, a wave per precinct (t2_wave_precinct).  The sizing pass with
+// ta.ticket set also runs the totals: every workgroup publishes its packet
+// lengths (release, arrival ticket) and the last to arrive acquires them and
+// runs t2_total_body -- one launch less per rate iteration (cdna_hip_
+// programming.md Guideline 16; no workgroup waits for another).
+template <bool EMIT>
+__global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a, T2TotalArgs ta) {
+    __shared__ T2LaneShared lds[kT2Waves];
+    __shared__ uint64_t wsum[kT2Waves + 1];
+    __shared__ int64_t red[kT2Waves][kTotSums];
+    __shared__ int last;
+    const int wv = threadIdx.x >> 6;
+    const int pi = blockIdx.x * kT2Waves + wv;
+    if (!EMIT && a.halt && *a.halt) return;  // (the whole grid)
+    if (pi < a.nprec) t2_wave_precinct<EMIT>(a, lds[wv], pi);
+    if (EMIT || !ta.ticket) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(ta.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *ta.ticket = 0u;  // for the next launch
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    t2_total_body<64 * kT2Waves, false>(a, ta, wsum, red);
 }
 
 // SOT + PLT + SOD of each tile-part, and where each of its packets starts
@@ -960,6 +1018,10 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
         !ensure_t2<uint64_t>(t2blkdst, (size_t)nb * L, err) || !ensure_t2<T2Summary>(t2sum, 1, err))
         return false;
     if (!h_sum) HIPCHECK(hipHostMalloc((void **)&h_sum, sizeof(T2Summary), hipHostMallocDefault));
+    if (!t2ticket.ptr) {  // k_t2_wave<false>'s arrival counter: zero once, left zero by every launch
+        if (!ensure_t2<uint32_t>(t2ticket, 1, err)) return false;
+        HIPCHECK(hipMemsetAsync(t2ticket.ptr, 0, sizeof(uint32_t), stream));
+    }
     if (plan.gen && plan.gen == t2_gen) return true;  // resident (same plan, same tables)
     t2_gen = 0;
     if (!h2d(t2prec.ptr, T.prec.data(), sizeof(PrecDesc) * T.prec.size(), err) ||
@@ -982,16 +1044,29 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt,
 #ifndef JP2HIP_REPEAT_STAGE
 #define JP2HIP_REPEAT_STAGE 0  // stage-cost experiments only (kernels.hip)
 #endif
-    for (int rep_ = 0; rep_ < (JP2HIP_REPEAT_STAGE == 5 ? 2 : 1); rep_++)
-    if (t2_nprec && t2_wave)
-        hipLaunchKernelGGL(k_t2_wave<false>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
-                           stream, a);
-    else if (t2_nprec)
-        hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
-    hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(kTotThreads), 0, stream, a, nb, (const int32_t *)lengths.ptr,
-                       (const uint8_t *)npasses.ptr, (const uint8_t *)pmin.ptr, (const int *)this->err.ptr,
-                       with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr,
-                       (const unsigned long long *)ordkey.ptr, (T2Summary *)t2sum.ptr, ra);
+    T2TotalArgs ta;
+    ta.nblocks = nb;
+    ta.lengths = (const int32_t *)lengths.ptr;
+    ta.npasses = (const uint8_t *)npasses.ptr;
+    ta.pmin = (const uint8_t *)pmin.ptr;
+    ta.t1err = (const int *)this->err.ptr;
+    ta.kc = with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr;
+    ta.acc = (const unsigned long long *)ordkey.ptr;
+    ta.sum = (T2Summary *)t2sum.ptr;
+    ta.rate = ra;
+    ta.ticket = nullptr;
+    for (int rep_ = 0; rep_ < (JP2HIP_REPEAT_STAGE == 5 ? 2 : 1); rep_++) {
+        if (t2_nprec && t2_wave) {
+            // the totals run in the last workgroup to finish (no k_t2_total launch)
+            ta.ticket = (uint32_t *)t2ticket.ptr;
+            hipLaunchKernelGGL(k_t2_wave<false>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
+                               stream, a, ta);
+        } else {
+            ta.ticket = nullptr;
+            if (t2_nprec) hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
+            hipLaunchKernelGGL(k_t2_total, dim3(1), dim3(kTotThreads), 0, stream, a, ta);
+        }
+    }
 }
 
 bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTimes &st, T2Summary &sum,
@@ -1030,7 +1105,7 @@ bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, u
     if (t2_ntp) hipLaunchKernelGGL(k_t2_tp_emit, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
     if (t2_nprec && t2_wave)
         hipLaunchKernelGGL(k_t2_wave<true>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
-                           stream, a);
+                           stream, a, T2TotalArgs{});
     else if (t2_nprec)
         hipLaunchKernelGGL(k_t2_code<true>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
     if (nb) hipLaunchKernelGGL(k_t2_copy, dim3((nb + 3) / 4), dim3(256), 0, stream, a, nb, (const uint8_t *)t1out.ptr);
