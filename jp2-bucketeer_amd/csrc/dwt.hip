@@ -17,9 +17,9 @@
 //       band is read from the TIFF strips resident in HBM (level shift, RCT
 //       or ICT for this component), so level 1 reads s bytes/sample and
 //       writes 4: exactly the B_dwt term.
-//   k_dwt_tail<REV>  the remaining levels once a level's region fits in
-//       64 KiB of LDS (128x128 words): one workgroup per tile-component runs
-//       every remaining level in LDS and writes only final coefficients.
+//   k_dwt_tail<REV>  the remaining levels once a level's region is at most
+//       64 x 64: one small workgroup per tile-component runs every remaining
+//       level in LDS and writes only final coefficients.
 //
 // Each coefficient is computed with the same expressions, in the same order,
 // as oracle/jp2_oracle.c (fwd53_1d / fwd97_1d, oracle_fdwt): the halo rows
@@ -753,13 +753,19 @@ struct DwtTailArgs {
 // The level's input is dense (row stride = its width): the LL scratch of the
 // previous level, then `ll`.  Same expressions in the same order as the
 // oracle (bit-exact).
-constexpr int kTailThreads = 1024;
-constexpr int kTailRG = 16;                                   // rows per vertical item
-constexpr int kTailWords = 16384 + 64 * 4 + kPadL + kPadR;    // padded rows of a <= 128 x 128 level
+// The tail starts at the first level of <= 64 x 64 samples (the recipe's
+// 512^2 and 1024^2 tiles reach it at levels 4 and 5): a workgroup of 256
+// threads and 21 KB of LDS.  Sized for 128 x 128 levels it took 1 024
+// threads and 82 KB -- half a CU -- and under the bench's load such a
+// workgroup waited ~1.5 ms for a CU to free that much (C2 bench +7-9 %).
+constexpr int kTailThreads = 256;
+constexpr int kTailRG = 16;                                  // rows per vertical item
+constexpr int kTailWords = 4096 + 64 * 4 + kPadL + kPadR;    // padded rows of a <= 64 x 64 level
+constexpr int kTailLL = 1024;                                // the LL of a <= 64 x 64 level
 template <bool REV>
 __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t rows_[kTailWords];  // vertical output, padded rows
-    __shared__ int32_t ll[kDwtLdsWords / 4];                             // the next level's input (dense)
+    __shared__ int32_t ll[kTailLL];                                      // the next level's input (dense)
     const int tc = blockIdx.x, tid = threadIdx.x;
     int sh = a.level - 1;
     int W = (a.tc_w[tc] + (1 << sh) - 1) >> sh;
@@ -912,7 +918,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
     for (int lv = 1; lv <= p.levels; lv++) {
         const int maxW = (p.plane_w + (1 << (lv - 1)) - 1) >> (lv - 1);
         const int maxH = (p.plane_h + (1 << (lv - 1)) - 1) >> (lv - 1);
-        if (lv >= 2 && ((maxW + 1) / 2) * ((maxH + 1) / 2) <= kDwtLdsWords / 4 &&
+        if (lv >= 2 && ((maxW + 1) / 2) * ((maxH + 1) / 2) <= kTailLL &&
             lds_row_stride(maxW) * maxH + kPadL + kPadR <= kTailWords) {
             DwtTailArgs t;
             t.src = scratch[(lv - 1) & 1];
