@@ -1034,7 +1034,7 @@ struct HullPt {
 };
 static_assert(sizeof(HullPt) == 16, "HullPt layout");
 
-__device__ __forceinline__ void hull_one(const HullArgs &a, int b, unsigned long long *lb, uint32_t *lc) {
+__device__ __forceinline__ void hull_one(const HullArgs &a, int b, uint32_t *lb, uint32_t *lc) {
     const int np = a.npasses[b];
     const int32_t *R = a.rates + (size_t)b * kMaxPasses;
     const int64_t *Dd = a.dists + (size_t)b * kMaxPasses;
@@ -1058,7 +1058,7 @@ __device__ __forceinline__ void hull_one(const HullArgs &a, int b, unsigned long
     // final hull's segments (no pass over the hull afterwards)
     auto seg = [&](uint64_t key, int32_t bytes, int sign) {
         const int bn = pcrd_bin(key);
-        atomicAdd(&lb[bn], (unsigned long long)(int64_t)(sign * bytes));
+        atomicAdd(&lb[bn], (uint32_t)(sign * bytes));
         atomicAdd(&lc[bn], (uint32_t)sign);
     };
     // passes 8 at a time: their rate and distortion loads in flight together
@@ -1123,7 +1123,9 @@ __device__ __forceinline__ void hull_one(const HullArgs &a, int b, unsigned long
 
 constexpr int kHullThreads = 256;
 __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
-    __shared__ unsigned long long lb[kPcrdBins];
+    // a workgroup's bytes per bin fit 32 bits (256 blocks of < 100 KB; the
+    // pops' transient negatives wrap and cancel): 32 KB of LDS, not 48
+    __shared__ uint32_t lb[kPcrdBins];
     __shared__ uint32_t lc[kPcrdBins];
     for (int i = threadIdx.x; i < kPcrdBins; i += kHullThreads) {
         lb[i] = 0;
@@ -1153,7 +1155,7 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
     __syncthreads();
     for (int i = threadIdx.x; i < kPcrdBins; i += kHullThreads)
         if (lc[i]) {
-            atomicAdd(&a.hbytes[i], lb[i]);
+            atomicAdd(&a.hbytes[i], (unsigned long long)lb[i]);
             atomicAdd(&a.hcount[i], lc[i]);
         }
 }
@@ -1200,7 +1202,10 @@ struct SelectArgs {
     int64_t *dbg;     // debug builds: [0] lists, [1 + i] list sizes, [33 + l] rounds, [65 + l] survivors
 };
 
-constexpr int kSelThreads = 1024, kSelBrute = 64;
+// 256 threads a workgroup (4 waves): under load a 1 024-thread workgroup
+// waits for 16 free wave slots on one CU
+constexpr int kSelThreads = 256, kSelBrute = 64;
+constexpr int kSelPer = kPcrdBins / kSelThreads;  // bins per thread in the scans
 // phase 1, run by every workgroup of both kernels (a few microseconds; no
 // hand-off through memory): suffix sums of the bin histogram, per layer the
 // bin and what it must supply, one candidate list per distinct bin
@@ -1222,21 +1227,21 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
     int *lbin = sh.lbin, *lli = sh.lli, *list_bin = sh.list_bin;
     int64_t *lneed = sh.lneed;
     uint32_t *list_off = sh.list_off;
-    // suffix sums, 4 bins per thread
+    // suffix sums, kSelPer bins per thread
     {
-        uint64_t v[4], s = 0;
+        uint64_t v[kSelPer], s = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) s += (v[i] = a.hbytes[4 * tid + i]);
+        for (int i = 0; i < kSelPer; i++) s += (v[i] = a.hbytes[kSelPer * tid + i]);
         uint64_t tot;
         const uint64_t pre = wg_excl_scan64<kSelThreads>(s, wsum, tot);
         uint64_t S = tot - pre;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            sfx[4 * tid + i] = S;
+        for (int i = 0; i < kSelPer; i++) {
+            sfx[kSelPer * tid + i] = S;
             S -= v[i];
         }
 #pragma unroll
-        for (int i = 0; i < 4; i++) binmap[4 * tid + i] = -1;
+        for (int i = 0; i < kSelPer; i++) binmap[kSelPer * tid + i] = -1;
     }
     __syncthreads();
     if (tid < L) {
@@ -1467,22 +1472,22 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
             }
             __syncthreads();
             {
-                uint64_t v[4], sm = 0;
+                uint64_t v[kSelPer], sm = 0;
 #pragma unroll
-                for (int i = 0; i < 4; i++) sm += (v[i] = hist[4 * tid + i]);
+                for (int i = 0; i < kSelPer; i++) sm += (v[i] = hist[kSelPer * tid + i]);
                 uint64_t tot;
                 const uint64_t pre = wg_excl_scan64<kSelThreads>(sm, wsum, tot);
-                uint64_t S = tot - pre;  // bytes of the sub-ranges >= 4 tid
+                uint64_t S = tot - pre;  // bytes of the sub-ranges >= kSelPer tid
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
+                for (int i = 0; i < kSelPer; i++) {
                     // the largest sub-range s with S(s) > need: S(s) > need >= S(s + 1)
                     const uint64_t Sn = S - v[i];
                     if ((int64_t)S > need && (int64_t)Sn <= need) {
-                        const uint64_t lo = flo + ((uint64_t)(4 * tid + i) << shift);
+                        const uint64_t lo = flo + ((uint64_t)(kSelPer * tid + i) << shift);
                         rlo = lo;
                         rhi = lo + ((1ull << shift) - 1ull) > fhi ? fhi : lo + ((1ull << shift) - 1ull);
                         rneed = need - (int64_t)Sn;
-                        rcount = hcnt[4 * tid + i];
+                        rcount = hcnt[kSelPer * tid + i];
                     }
                     S = Sn;
                 }

@@ -334,11 +334,26 @@ constexpr int kT2Waves = 4;     // precincts per workgroup
 constexpr int kTreeLev = 7;     // levels of a tag tree over <= 64 leaves
 constexpr int kBitWords = 512;  // pending packet headers in LDS, per wave
 constexpr int kWaveMaxMb = 48;  // a leaf's zero bit-plane path stays within 64 bits (host check)
+// One wave's slice of k_t2_wave's dynamic LDS, sized by the layer count
+// (t2_lane_bytes): L = 6 takes 4 KB a wave, 16 KB a workgroup -- sized for
+// 32 layers it was 48 KB, and under load a workgroup waited for a CU to free
+// that much.
 struct T2LaneShared {
-    uint8_t nl[kMaxLayers][64];  // cumulative passes per layer
-    int32_t lr[kMaxLayers][64];  // cumulative bytes per layer
-    uint32_t bits[kBitWords];    // header bits of the pending packets, MSB first, a zero word after each
+    int32_t *lr;    // [L][64] cumulative bytes per layer
+    uint32_t *bits; // [kBitWords] header bits of the pending packets, MSB first, a zero word after each
+    uint8_t *nl;    // [L][64] cumulative passes per layer
 };
+__host__ __device__ constexpr size_t t2_lane_bytes(int L) {
+    return ((size_t)L * 64 * 5 + (size_t)kBitWords * 4 + 15) & ~(size_t)15;
+}
+__device__ __forceinline__ T2LaneShared t2_lane(uint8_t *dyn, int L, int wv) {
+    uint8_t *p = dyn + (size_t)wv * t2_lane_bytes(L);
+    T2LaneShared S;
+    S.lr = (int32_t *)p;
+    S.bits = (uint32_t *)(p + (size_t)L * 64 * 4);
+    S.nl = p + (size_t)L * 64 * 4 + (size_t)kBitWords * 4;
+    return S;
+}
 
 // the lanes of one wave see each other's LDS writes in program order (the
 // LDS performs a wave's operations in issue order); this only keeps the
@@ -388,7 +403,7 @@ __device__ __forceinline__ uint32_t stuff_header(const uint32_t *buf, uint32_t p
 
 // precinct pi's L packets, by one wave (k_t2_wave)
 template <bool EMIT>
-__device__ __forceinline__ void t2_wave_precinct(const T2Args &a, T2LaneShared &S, int pi) {
+__device__ __forceinline__ void t2_wave_precinct(const T2Args &a, const T2LaneShared &S, int pi) {
     const int lane = threadIdx.x & 63;
     const PrecDesc d = a.prec[pi];
     const int L = a.L;
@@ -459,23 +474,23 @@ __device__ __forceinline__ void t2_wave_precinct(const T2Args &a, T2LaneShared &
                     const int l = l0 + j;
                     if (l >= L) break;
                     const int32_t r = ncv[j] ? rv[j] : 0;
-                    S.nl[l][lane] = (uint8_t)ncv[j];
-                    S.lr[l][lane] = r;
+                    S.nl[l * 64 + lane] = (uint8_t)ncv[j];
+                    S.lr[l * 64 + lane] = r;
                     gnl[l] = (uint8_t)ncv[j];
                     glr[l] = r;
                 }
             }
         } else {
             for (int l = 0; l < L; l++) {
-                S.nl[l][lane] = gnl[l];
-                S.lr[l][lane] = glr[l];
+                S.nl[l * 64 + lane] = gnl[l];
+                S.lr[l * 64 + lane] = glr[l];
             }
         }
     }
     int firstl = L;  // inclusion layer (L: never)
     if (own)
         for (int l = 0; l < L; l++)
-            if (S.nl[l][lane] > 0) {
+            if (S.nl[l * 64 + lane] > 0) {
                 firstl = l;
                 break;
             }
@@ -530,8 +545,8 @@ __device__ __forceinline__ void t2_wave_precinct(const T2Args &a, T2LaneShared &
         if (l < L) {
             // this block's part of packet l
             if (own) {
-                n = (int)S.nl[l][lane] - (l ? (int)S.nl[l - 1][lane] : 0);
-                len = S.lr[l][lane] - (l ? S.lr[l - 1][lane] : 0);
+                n = (int)S.nl[l * 64 + lane] - (l ? (int)S.nl[(l - 1) * 64 + lane] : 0);
+                len = S.lr[l * 64 + lane] - (l ? S.lr[(l - 1) * 64 + lane] : 0);
             }
             if (n > 0) {
                 uint32_t cv;
@@ -612,8 +627,8 @@ __device__ __forceinline__ void t2_wave_precinct(const T2Args &a, T2LaneShared &
                 for (int l2 = l0; l2 < l; l2++) {
                     int n2 = 0, len2 = 0;
                     if (own) {
-                        n2 = (int)S.nl[l2][lane] - (l2 ? (int)S.nl[l2 - 1][lane] : 0);
-                        len2 = S.lr[l2][lane] - (l2 ? S.lr[l2 - 1][lane] : 0);
+                        n2 = (int)S.nl[l2 * 64 + lane] - (l2 ? (int)S.nl[(l2 - 1) * 64 + lane] : 0);
+                        len2 = S.lr[l2 * 64 + lane] - (l2 ? S.lr[(l2 - 1) * 64 + lane] : 0);
                     }
                     const uint32_t lin2 = n2 > 0 ? (uint32_t)len2 : 0u;
                     const uint32_t before = wave_incl_scan(lin2) - lin2;
@@ -823,14 +838,14 @@ __global__ void __launch_bounds__(kTotThreads) k_t2_total(T2Args a, T2TotalArgs 
 // programming.md Guideline 16; no workgroup waits for another).
 template <bool EMIT>
 __global__ void __launch_bounds__(64 * kT2Waves) k_t2_wave(T2Args a, T2TotalArgs ta) {
-    __shared__ T2LaneShared lds[kT2Waves];
+    extern __shared__ __attribute__((aligned(16))) uint8_t t2dyn[];  // kT2Waves * t2_lane_bytes(L)
     __shared__ uint64_t wsum[kT2Waves + 1];
     __shared__ int64_t red[kT2Waves][kTotSums];
     __shared__ int last;
     const int wv = threadIdx.x >> 6;
     const int pi = blockIdx.x * kT2Waves + wv;
     if (!EMIT && a.halt && *a.halt) return;  // (the whole grid)
-    if (pi < a.nprec) t2_wave_precinct<EMIT>(a, lds[wv], pi);
+    if (pi < a.nprec) t2_wave_precinct<EMIT>(a, t2_lane(t2dyn, a.L, wv), pi);
     if (EMIT || !ta.ticket) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1059,8 +1074,8 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt,
         if (t2_nprec && t2_wave) {
             // the totals run in the last workgroup to finish (no k_t2_total launch)
             ta.ticket = (uint32_t *)t2ticket.ptr;
-            hipLaunchKernelGGL(k_t2_wave<false>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
-                               stream, a, ta);
+            hipLaunchKernelGGL(k_t2_wave<false>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves),
+                               kT2Waves * t2_lane_bytes(a.L), stream, a, ta);
         } else {
             ta.ticket = nullptr;
             if (t2_nprec) hipLaunchKernelGGL(k_t2_code<false>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
@@ -1104,8 +1119,8 @@ bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, u
     HIPCHECK(hipEventRecord(ev[8], stream));
     if (t2_ntp) hipLaunchKernelGGL(k_t2_tp_emit, dim3((t2_ntp + 63) / 64), dim3(64), 0, stream, a);
     if (t2_nprec && t2_wave)
-        hipLaunchKernelGGL(k_t2_wave<true>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves), 0,
-                           stream, a, T2TotalArgs{});
+        hipLaunchKernelGGL(k_t2_wave<true>, dim3((t2_nprec + kT2Waves - 1) / kT2Waves), dim3(64 * kT2Waves),
+                           kT2Waves * t2_lane_bytes(a.L), stream, a, T2TotalArgs{});
     else if (t2_nprec)
         hipLaunchKernelGGL(k_t2_code<true>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
     if (nb) hipLaunchKernelGGL(k_t2_copy, dim3((nb + 3) / 4), dim3(256), 0, stream, a, nb, (const uint8_t *)t1out.ptr);
