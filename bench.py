@@ -25,6 +25,15 @@ import time
 
 import numpy as np
 
+# device -> pinned host copies on the DMA engines: without it the runtime
+# copies with blit kernels, which under load wait for CUs like any kernel
+# (the code-stream D2H took 1.3 ms per image in the bench's kernel trace,
+# 0.13 ms alone): +5-6 % C2 (tests/tools/sdma_ab.sh, profiles/r03/ab/sdma.txt).
+# Read when the HSA runtime starts, so it is set before anything can start
+# it; the deployment sets it the same way.  (Under
+# rocprofv3 the runtime starts before Python does: traces show blit copies.)
+os.environ.setdefault("HSA_ENABLE_SDMA", "1")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jp2-bucketeer_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -639,12 +648,6 @@ def main():
     # initialises HIP.  Sweep: profiles/r02/hwq_sweep.txt
     if not os.environ.get("JP2HIP_KEEP_HW_QUEUES"):
         os.environ["GPU_MAX_HW_QUEUES"] = str(max(4, min(32, args.inflight + 4)))
-    # device -> pinned host copies on the DMA engines: without it the runtime
-    # copies with blit kernels, which under load wait for CUs like any kernel
-    # (the code-stream D2H took 1.3 ms per image in the bench's kernel trace,
-    # 0.13 ms alone): +5-6 % C2 (tests/tools/sdma_ab.sh, gpurun_out/sdma).
-    # The deployment sets it the same way.
-    os.environ.setdefault("HSA_ENABLE_SDMA", "1")
     if args.workload == "c4":
         res = run_c4(args)
         if res is not None:

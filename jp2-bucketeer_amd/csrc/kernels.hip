@@ -1206,12 +1206,13 @@ struct SelectArgs {
 // waits for 16 free wave slots on one CU
 constexpr int kSelThreads = 256, kSelBrute = 64;
 constexpr int kSelPer = kPcrdBins / kSelThreads;  // bins per thread in the scans
+// k_select_resolve narrows a layer's key range 1 024 ways per round
+constexpr int kResLog2 = 10, kResBins = 1 << kResLog2, kResPer = kResBins / kSelThreads;
 // phase 1, run by every workgroup of both kernels (a few microseconds; no
 // hand-off through memory): suffix sums of the bin histogram, per layer the
 // bin and what it must supply, one candidate list per distinct bin
 struct SelBins {
-    unsigned long long sfx[kPcrdBins];  // S(bin): bytes of the bins >= bin
-    int8_t binmap[kPcrdBins];           // bin -> candidate list (-1: none)
+    uint64_t csfx[kSelThreads + 1];     // bytes of the bins >= kSelPer * t (t = 0 .. kSelThreads)
     uint64_t wsum[kSelThreads / 64 + 1];
     int lbin[kMaxLayers], lli[kMaxLayers];
     int64_t lneed[kMaxLayers];          // budget - bytes above the bin
@@ -1219,29 +1220,24 @@ struct SelBins {
     uint32_t list_off[kMaxLayers + 1];
     int nlist;
 };
+// The suffix sums are kept per thread chunk (kSelPer bins), 2 KB of LDS
+// instead of a 32 KB table per bin (and no 4 KB bin -> list map): a layer's
+// bin is found by a binary search over the chunks, then a walk down its
+// chunk's bins (re-read from L2).
 __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
     const int tid = threadIdx.x, L = a.layers;
-    unsigned long long *sfx = sh.sfx;
-    int8_t *binmap = sh.binmap;
-    uint64_t *wsum = sh.wsum;
+    uint64_t *csfx = sh.csfx;
     int *lbin = sh.lbin, *lli = sh.lli, *list_bin = sh.list_bin;
     int64_t *lneed = sh.lneed;
     uint32_t *list_off = sh.list_off;
-    // suffix sums, kSelPer bins per thread
     {
-        uint64_t v[kSelPer], s = 0;
+        uint64_t s = 0;
 #pragma unroll
-        for (int i = 0; i < kSelPer; i++) s += (v[i] = a.hbytes[kSelPer * tid + i]);
+        for (int i = 0; i < kSelPer; i++) s += a.hbytes[kSelPer * tid + i];
         uint64_t tot;
-        const uint64_t pre = wg_excl_scan64<kSelThreads>(s, wsum, tot);
-        uint64_t S = tot - pre;
-#pragma unroll
-        for (int i = 0; i < kSelPer; i++) {
-            sfx[kSelPer * tid + i] = S;
-            S -= v[i];
-        }
-#pragma unroll
-        for (int i = 0; i < kSelPer; i++) binmap[kSelPer * tid + i] = -1;
+        const uint64_t pre = wg_excl_scan64<kSelThreads>(s, sh.wsum, tot);
+        csfx[tid] = tot - pre;
+        if (tid == 0) csfx[kSelThreads] = 0;
     }
     __syncthreads();
     if (tid < L) {
@@ -1249,17 +1245,29 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
         const int64_t B = a.init_on ? (a.init.budget < 0 ? 0 : a.init.budget) >> (L - 1 - tid) : a.budget[tid];
         const int64_t T = B < 0 ? 0 : B;
         int b = -1;
-        if ((int64_t)sfx[0] > T) {  // the largest bin b with S(b) > T
-            int lo = 0, hi = kPcrdBins - 1;
+        int64_t above = 0;  // S(b + 1)
+        if ((int64_t)csfx[0] > T) {
+            // the largest chunk whose suffix sum exceeds T ...
+            int lo = 0, hi = kSelThreads - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if ((int64_t)sfx[mid] > T) lo = mid;
+                if ((int64_t)csfx[mid] > T) lo = mid;
                 else hi = mid - 1;
             }
-            b = lo;
+            // ... then its largest bin b with S(b) > T
+            uint64_t S = csfx[lo + 1];
+            for (int i = kSelPer - 1; i >= 0; i--) {
+                const uint64_t Sb = S + a.hbytes[kSelPer * lo + i];
+                if ((int64_t)Sb > T) {
+                    b = kSelPer * lo + i;
+                    break;
+                }
+                S = Sb;
+            }
+            above = (int64_t)S;
         }
         lbin[tid] = b;
-        lneed[tid] = b < 0 ? 0 : T - (int64_t)(b + 1 < kPcrdBins ? sfx[b + 1] : 0ull);
+        lneed[tid] = b < 0 ? 0 : T - above;
     }
     __syncthreads();
     if (tid == 0) {  // one candidate list per distinct bin
@@ -1273,7 +1281,6 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
                 list_bin[n] = lbin[l];
                 list_off[n] = o;
                 o += a.hcount[lbin[l]];
-                binmap[lbin[l]] = (int8_t)n;
                 n++;
             }
             lli[l] = i;
@@ -1300,8 +1307,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
         rate_budgets(r, a.layers, a.budget_w);
     }
     select_bins(a, sh);
-    const int8_t *binmap = sh.binmap;
     const uint32_t *list_off = sh.list_off;
+    const int *list_bin = sh.list_bin;
     const int nlist = sh.nlist;
     // 2. candidates of those bins, thread per code-block
     if (nlist > 0)
@@ -1318,7 +1325,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
                 for (int j = 0; j < 8; j++) {
                     const int i = i0 + j;
                     const uint64_t key = k8[j];
-                    const int li = i < nh ? binmap[pcrd_bin(key)] : -1;
+                    int li = -1;
+                    if (i < nh) {
+                        const int bn = pcrd_bin(key);
+                        for (int q = 0; q < nlist; q++) li = list_bin[q] == bn ? q : li;
+                    }
                     // one fill atomic per wave and list (a list's lanes take
                     // consecutive slots): same-word atomics serialise in L2
                     uint64_t todo = __ballot(li >= 0);
@@ -1355,7 +1366,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
     __shared__ uint32_t rcount;
     __shared__ uint64_t bkey[kSelBrute];
     __shared__ uint32_t bsize[kSelBrute];
-    __shared__ uint32_t hcnt[kPcrdBins];
+    __shared__ uint64_t hist[kResBins];
+    __shared__ uint32_t hcnt[kResBins];
     const int tid = threadIdx.x, lane = tid & 63, l = blockIdx.x;
     if (a.halt && *a.halt) return;  // (k_select has reset it on a first iteration)
     select_bins(a, sh);
@@ -1370,11 +1382,10 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
         for (int i = 0; i < nlist; i++) a.dbg[1 + i] = list_off[i + 1] - list_off[i];
     }
     // The key range is narrowed by
-    // 4096-way histograms (bytes and counts) over the candidates in range --
+    // 1 024-way histograms (bytes and counts) over the candidates in range --
     // a bin is 2^47 keys wide, one round leaves a handful (a round starts
     // from the bin's own bounds and count: no pass for them) -- until at most
     // kSelBrute remain, whose totals are then summed directly.
-    uint64_t *hist = (uint64_t *)sh.sfx;  // (the suffix sums are done with)
     {
         if (lbin[l] < 0) {
             if (tid == 0) a.K[l] = a.Kc[l] = 0ull;  // every segment fits
@@ -1456,8 +1467,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
             }
             // bytes and counts per 1/4096 of the key range; the sub-range the
             // budget falls in
-            const int shift = max(0, 64 - __builtin_clzll(fhi - flo) - 12);
-            for (int i = tid; i < kPcrdBins; i += kSelThreads) {
+            const int shift = max(0, 64 - __builtin_clzll(fhi - flo) - kResLog2);
+            for (int i = tid; i < kResBins; i += kSelThreads) {
                 hist[i] = 0ull;
                 hcnt[i] = 0u;
             }
@@ -1472,22 +1483,22 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
             }
             __syncthreads();
             {
-                uint64_t v[kSelPer], sm = 0;
+                uint64_t v[kResPer], sm = 0;
 #pragma unroll
-                for (int i = 0; i < kSelPer; i++) sm += (v[i] = hist[kSelPer * tid + i]);
+                for (int i = 0; i < kResPer; i++) sm += (v[i] = hist[kResPer * tid + i]);
                 uint64_t tot;
                 const uint64_t pre = wg_excl_scan64<kSelThreads>(sm, wsum, tot);
-                uint64_t S = tot - pre;  // bytes of the sub-ranges >= kSelPer tid
+                uint64_t S = tot - pre;  // bytes of the sub-ranges >= kResPer tid
 #pragma unroll
-                for (int i = 0; i < kSelPer; i++) {
+                for (int i = 0; i < kResPer; i++) {
                     // the largest sub-range s with S(s) > need: S(s) > need >= S(s + 1)
                     const uint64_t Sn = S - v[i];
                     if ((int64_t)S > need && (int64_t)Sn <= need) {
-                        const uint64_t lo = flo + ((uint64_t)(kSelPer * tid + i) << shift);
+                        const uint64_t lo = flo + ((uint64_t)(kResPer * tid + i) << shift);
                         rlo = lo;
                         rhi = lo + ((1ull << shift) - 1ull) > fhi ? fhi : lo + ((1ull << shift) - 1ull);
                         rneed = need - (int64_t)Sn;
-                        rcount = hcnt[kSelPer * tid + i];
+                        rcount = hcnt[kResPer * tid + i];
                     }
                     S = Sn;
                 }

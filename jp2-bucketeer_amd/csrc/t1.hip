@@ -684,8 +684,12 @@ struct MqShared {
     uint32_t cxs[20 * 64];                 // 19 contexts + CX_PAD, lane-interleaved (modeller)
     uint32_t mqt[94];                      // state table
     uint32_t rings[64 * 17];               // coder: 64-byte ring per lane at a 68-byte stride (banks)
-    uint32_t bbase[kOrderBuckets + 1];     // lane order: bucket bases
-    uint32_t code[2][kMqChunk][64];        // modeller -> coder, double-buffered
+    // (the bucket bases are done with before the first chunk: one LDS slot,
+    // 19.1 KB a workgroup, 8 per CU instead of 7)
+    union {
+        uint32_t bbase[kOrderBuckets + 1];  // lane order: bucket bases
+        uint32_t code[2][kMqChunk][64];     // modeller -> coder, double-buffered
+    };
     int32_t segs[2][64];                   // passes closed before the chunk (per lane)
     uint32_t finA[64];                     // the interval register at the end (mq_flush)
     int32_t blk[64];                       // the lane's block, -1 none
