@@ -663,7 +663,7 @@ struct QuantArgs {
     uint32_t nzero[8];
 };
 
-constexpr int kQuantWaves = 4;  // code-blocks (waves) per workgroup
+constexpr int kQuantWaves = 2;  // code-blocks (waves) per workgroup
 template <bool REV>
 __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     extern __shared__ uint64_t lds_planes[];  // [wave][plane][lane], a.max_mb planes per wave

@@ -48,7 +48,7 @@ __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
     return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
 }
 
-constexpr int kCmWaves = 4;  // items per workgroup
+constexpr int kCmWaves = 2;  // items per workgroup
 
 // MQ lane order: blocks by decreasing decision count, so the lanes of an MQ
 // wave carry similar work.  The order only groups blocks (it changes no
@@ -204,7 +204,7 @@ __device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, u
 // to the plan's item bound).
 // --------------------------------------------------------------------------
 constexpr int kRingBytes = 2048;
-constexpr int kCm3Blocks = 2048;  // workgroups (4 waves each) at most
+constexpr int kCm3Blocks = 4096;  // workgroups (2 waves each) at most
 
 __device__ __forceinline__ uint32_t spread4(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
 // spread4(nib) << k, as one 24-bit multiply (k <= 4: nib << k < 2^24)
