@@ -183,36 +183,46 @@ def tiff_layout(data: bytes):
     return lay, keep
 
 
+class _PinnedBuffer:
+    """Owns one *out buffer of the encode calls; returns it to jp2hip's pool
+    (jp2hip_free) when the last holder -- the Output or a view of it -- goes."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        try:
+            lib().jp2hip_free(self.ptr)
+        except Exception:
+            pass
+
+
 class Output:
     """An encode's file bytes, left where the library wrote them (pinned host
-    memory from jp2hip's pool) instead of copied into a Python bytes object;
-    released by close() or when collected."""
+    memory from jp2hip's pool) instead of copied into a Python bytes object.
+    close() (or collection) releases the Output's hold; the buffer goes back
+    to the pool once no view() of it is alive either, so a view never sees
+    another encode's bytes."""
 
     def __init__(self, ptr, n: int):
-        self._p = ptr
+        self._buf = _PinnedBuffer(ptr)
         self._n = n
 
     def __len__(self):
         return self._n
 
     def view(self) -> memoryview:
-        if not self._p:
+        if self._buf is None:
             raise ValueError("released output")
-        return memoryview((c_uint8 * self._n).from_address(ctypes.addressof(self._p.contents)))
+        arr = (c_uint8 * self._n).from_address(ctypes.addressof(self._buf.ptr.contents))
+        arr._jp2hip_owner = self._buf  # the view keeps the pinned buffer alive
+        return memoryview(arr)
 
     def tobytes(self) -> bytes:
         return bytes(self.view())
 
     def close(self):
-        if self._p:
-            lib().jp2hip_free(self._p)
-            self._p = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        self._buf = None
 
 
 class Encoder:

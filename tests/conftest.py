@@ -50,5 +50,6 @@ def golden_image(name, testjpx_pixels):
         "synth_gray16_1024": lambda: im.synth_u16(1024, 1024, comps=1, seed=5),
         "c2_synth_rgb8_6000x4000": lambda: im.synth_rgb8(4000, 6000, seed=1234),
         "c2_testjpx_tiled_6000x4000": lambda: im.testjpx_tiled(testjpx_pixels),
+        "c5_gray16_4096x4096": lambda: im.synth_gray16_rows(0, 4096, 4096),
     }
     return table[name]()

@@ -25,6 +25,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 import imaging as im  # noqa: E402
 
+# usage: make_golden.py            -- everything (about 15 minutes)
+#        make_golden.py NAME ...   -- only these lossy cases / "c5_full"
+
 PREC = "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]"
 
 
@@ -52,7 +55,32 @@ def opj_psnr_at(img, bits, target_bytes, levels=6):
     return len(cs), im.psnr(img, dec, bits)
 
 
-def main():
+def c5_full_sha(w=40000, h=30000):
+    """SHA-256 of the oracle's file for the full C5 image (BASELINE.json
+    configs[4]: 40000x30000 Gray16, 7 levels, lossy 3 bpp, JPX), so the GPU
+    tile-split encode is compared with the oracle without running it there
+    (about 8 minutes and 20 GB of RAM here)."""
+    import hashlib
+    import oracle_lib as ol
+    img = im.synth_gray16_rows(0, h, w)
+    cs = ol.encode(img, ol.recipe(False, levels=7))
+    return {"name": "c5_gray16_40000x30000_jpx", "oracle_bytes": len(cs),
+            "oracle_sha256": hashlib.sha256(cs).hexdigest()}
+
+
+def main(only=None):
+    if only:
+        # recompute the named lossy cases / the C5 file only, keep the rest
+        g = json.load(open(os.path.join(HERE, "golden.json")))
+        pix = im.decode_opj(open(os.path.join(HERE, "test.jpx"), "rb").read(), ".j2k")
+        if "c5_full" in only:
+            g["c5_full"] = c5_full_sha()
+            print(g["c5_full"])
+        g["lossy"] = [c for c in g["lossy"] if c["name"] not in only]
+        g["lossy"] += lossy_cases(pix, only)
+        with open(os.path.join(HERE, "golden.json"), "w") as f:
+            json.dump(g, f, indent=1)
+        return
     g = {}
     tj = open(os.path.join(HERE, "test.jpx"), "rb").read()
     pix = im.decode_opj(tj, ".j2k")
@@ -70,34 +98,11 @@ def main():
         "tp_order": [[t[0], t[2], t[3]] for t in im.tile_parts(tj)],
         "min_size_assert": 30000,   # KakaduConverterTest.java:107
     }
-    # lossy yardsticks: opj at exactly the oracle's output size
-    sys.path.insert(0, os.path.dirname(HERE))
-    import oracle_lib as ol
-    cases = []
-    for name, img, bits, lv in [
-        ("synth_rgb8_1024x1536", im.synth_rgb8(1024, 1536, seed=1234), 8, 6),
-        ("testjpx_rgb_crop_1024", pix[:1024, :1024, :3].copy(), 8, 6),
-        ("synth_gray16_1024", im.synth_u16(1024, 1024, comps=1, seed=5), 16, 7),
-        # full-size C2 (BASELINE.json configs[1]) in both SURVEY.md 8(d)
-        # content classes; the oracle file's SHA-256 pins the GPU output
-        ("c2_synth_rgb8_6000x4000", im.synth_rgb8(4000, 6000, seed=1234), 8, 6),
-        ("c2_testjpx_tiled_6000x4000", im.testjpx_tiled(pix), 8, 6),
-    ]:
-        rc = ol.recipe(False, levels=lv, format=0)
-        cs = ol.encode(img, rc)
-        dec = im.decode_opj(cs, ".j2k")
-        ps = im.psnr(img, dec, bits)
-        n_opj, ps_opj = opj_psnr_at(img, bits, len(cs), lv)
-        import hashlib
-        cases.append({"name": name, "bits": bits, "levels": lv, "oracle_bytes": len(cs),
-                      "oracle_sha256": hashlib.sha256(cs).hexdigest(),
-                      "oracle_psnr": round(ps, 4), "opj_bytes": n_opj, "opj_psnr": round(ps_opj, 4),
-                      "bpp": round(8.0 * len(cs) / (img.shape[0] * img.shape[1]), 5)})
-        print(cases[-1])
-    g["lossy"] = cases
+    g["lossy"] = lossy_cases(pix)
     # lossless at full C4 size (BASELINE.json configs[3]: one 5000x7000 RGB8
     # batch image, seed 0, JPX as the batch writes it): the oracle file's
     # SHA-256 pins the GPU batch output without running the oracle there
+    import oracle_lib as ol
     img = im.synth_rgb8(7000, 5000, seed=0)
     cs = ol.encode(img, ol.recipe(True))
     assert np.array_equal(im.decode_pillow(cs), img)
@@ -105,10 +110,47 @@ def main():
     g["lossless"] = [{"name": "c4_synth_rgb8_5000x7000_seed0_jpx", "oracle_bytes": len(cs),
                       "oracle_sha256": hashlib.sha256(cs).hexdigest()}]
     print(g["lossless"])
+    g["c5_full"] = c5_full_sha()
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(g, f, indent=1)
     print(json.dumps(g["testjpx"], indent=1))
 
 
+LOSSY_SOURCES = {
+    "synth_rgb8_1024x1536": (lambda pix: im.synth_rgb8(1024, 1536, seed=1234), 8, 6),
+    "testjpx_rgb_crop_1024": (lambda pix: pix[:1024, :1024, :3].copy(), 8, 6),
+    "synth_gray16_1024": (lambda pix: im.synth_u16(1024, 1024, comps=1, seed=5), 16, 7),
+    # full-size C2 (BASELINE.json configs[1]) in both SURVEY.md 8(d)
+    # content classes; the oracle file's SHA-256 pins the GPU output
+    "c2_synth_rgb8_6000x4000": (lambda pix: im.synth_rgb8(4000, 6000, seed=1234), 8, 6),
+    "c2_testjpx_tiled_6000x4000": (lambda pix: im.testjpx_tiled(pix), 8, 6),
+    # C5's recipe (7 levels, lossy 3 bpp) and content generator on a 4096^2
+    # window of the map scan: the Gray16 class's opj +-0.1 dB yardstick
+    "c5_gray16_4096x4096": (lambda pix: im.synth_gray16_rows(0, 4096, 4096), 16, 7),
+}
+
+
+def lossy_cases(pix, only=None):
+    """Lossy yardsticks: opj at exactly the oracle's output size."""
+    import hashlib
+    import oracle_lib as ol
+    cases = []
+    for name, (make, bits, lv) in LOSSY_SOURCES.items():
+        if only and name not in only:
+            continue
+        img = make(pix)
+        rc = ol.recipe(False, levels=lv, format=0)
+        cs = ol.encode(img, rc)
+        dec = im.decode_opj(cs, ".j2k")
+        ps = im.psnr(img, dec, bits)
+        n_opj, ps_opj = opj_psnr_at(img, bits, len(cs), lv)
+        cases.append({"name": name, "bits": bits, "levels": lv, "oracle_bytes": len(cs),
+                      "oracle_sha256": hashlib.sha256(cs).hexdigest(),
+                      "oracle_psnr": round(ps, 4), "opj_bytes": n_opj, "opj_psnr": round(ps_opj, 4),
+                      "bpp": round(8.0 * len(cs) / (img.shape[0] * img.shape[1]), 5)})
+        print(cases[-1])
+    return cases
+
+
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -226,3 +226,40 @@ def test_factory_without_gpu_or_kakadu(monkeypatch):
 def test_encoder_fails_loudly_without_gpu():
     with pytest.raises(jp2hip.Jp2hipError, match="no HIP device"):
         jp2hip.Encoder(0)
+
+
+def test_output_view_keeps_the_pinned_buffer_alive(monkeypatch):
+    """a view of an Output must outlive the Output (and its
+    close()) without the buffer going back to jp2hip's pool under it."""
+    import ctypes
+    import gc
+    freed = []
+
+    class FakeLib:
+        def jp2hip_free(self, p):
+            freed.append(ctypes.addressof(p.contents))
+
+    monkeypatch.setattr(_lib, "lib", lambda: FakeLib())
+    store = (ctypes.c_uint8 * 8)(*b"JP2HIP!!")
+    ptr = ctypes.cast(store, ctypes.POINTER(ctypes.c_uint8))
+    v = _lib.Output(ptr, 8).view()  # the temporary Output is dropped at once
+    gc.collect()
+    assert freed == [] and bytes(v) == b"JP2HIP!!"
+    del v
+    gc.collect()
+    assert freed == [ctypes.addressof(store)]
+    freed.clear()
+    o = _lib.Output(ptr, 8)
+    v = o.view()
+    o.close()
+    gc.collect()
+    assert freed == [] and bytes(v[:3]) == b"JP2"
+    with pytest.raises(ValueError):
+        o.view()
+    v.release()
+    del v
+    gc.collect()
+    assert len(freed) == 1
+    o2 = _lib.Output(ptr, 8)
+    o2.close()
+    assert len(freed) == 2

@@ -90,15 +90,23 @@ def test_testjpx_pixels_lossless(encoder, testjpx_pixels, golden):
     assert len(got) > g["min_size_assert"]
 
 
-@pytest.mark.parametrize("case", range(5))
-def test_golden_lossy_cases(encoder, golden, testjpx_pixels, case):
-    """Every lossy golden case (1024-class crops, and full-size C2 in both
-    content classes): the GPU file's SHA-256 is the oracle file's (committed
+def _golden_lossy_names():
+    import json
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return [c["name"] for c in json.load(f)["lossy"]]
+
+
+@pytest.mark.parametrize("name", _golden_lossy_names())
+def test_golden_lossy_cases(encoder, golden, testjpx_pixels, name):
+    """Every lossy golden case (1024-class crops, full-size C2 in both
+    content classes, a 4096^2 window of C5's Gray16 map scan at C5's
+    7-level recipe): the GPU file's SHA-256 is the oracle file's (committed
     by tests/golden/make_golden.py), and its PSNR is within 0.1 dB of
     opj_compress at the same bytes."""
     import hashlib
     from conftest import golden_image
-    c = golden["lossy"][case]
+    c = [x for x in golden["lossy"] if x["name"] == name][0]
     img = golden_image(c["name"], testjpx_pixels)
     rc = jp2hip.recipe(jp2hip.LOSSY, levels=c["levels"], format=jp2hip.FORMAT_J2K)
     got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSY, rc)

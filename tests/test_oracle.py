@@ -9,6 +9,8 @@
 * edge cases the reference path meets: ragged tiles, tiny images, 1/2/4
   components, 16-bit, levels 0..7, JP2/JPX wrappers.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -77,14 +79,22 @@ def test_oracle_com_markers_follow_kakadu_layout(testjpx_pixels, testjpx_bytes):
     assert abs(last - len(cs)) / len(cs) < 0.05
 
 
-@pytest.mark.parametrize("case", range(5))
-def test_oracle_lossy_within_0p1db_of_opj(case, golden, testjpx_pixels):
+def _golden_lossy_names():
+    import json
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return [c["name"] for c in json.load(f)["lossy"]]
+
+
+@pytest.mark.parametrize("name", _golden_lossy_names())
+def test_oracle_lossy_within_0p1db_of_opj(name, golden, testjpx_pixels):
     """The lossy yardstick (north_star): PSNR within 0.1 dB of opj_compress at
-    the same bytes -- 1024-class crops and full-size C2 in both SURVEY.md 8(d)
-    content classes (synthetic scan, test.jpx pixels mirror-tiled)."""
+    the same bytes -- 1024-class crops, full-size C2 in both SURVEY.md 8(d)
+    content classes (synthetic scan, test.jpx pixels mirror-tiled) and a
+    4096^2 window of C5's Gray16 map scan at C5's 7-level recipe."""
     import hashlib
     from conftest import golden_image
-    c = golden["lossy"][case]
+    c = [x for x in golden["lossy"] if x["name"] == name][0]
     img = golden_image(c["name"], testjpx_pixels)
     cs = ol.encode(img, ol.recipe(False, levels=c["levels"], format=0))
     assert len(cs) == c["oracle_bytes"]            # deterministic
