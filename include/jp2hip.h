@@ -117,7 +117,8 @@ typedef struct jp2hip_stats {
     double t1_ms;         /* EBCOT tier-1 kernels                             */
     double pcrd_ms;       /* hull + threshold selection kernels               */
     double d2h_ms;        /* metadata + compressed bytes download             */
-    double t2_ms;         /* host tier-2 / codestream assembly                */
+    double t2_ms;         /* tier-2 on the device: packet headers, tile-part  */
+                          /* sizing and code-stream emission                  */
     int64_t codeblocks;
     int64_t coded_passes;
     int64_t t1_bytes;     /* MQ bytes produced by tier-1 (before truncation)  */
@@ -146,6 +147,14 @@ int jp2hip_device_count(void);
  * non-gfx950 device may hold a low ordinal). */
 int jp2hip_device_ordinals(int32_t *ordinals, int32_t max);
 
+/* "" when the process environment suits the contexts alive in it, else
+ * what to change: GPU_MAX_HW_QUEUES below the live context count (contexts
+ * sharing a hardware queue run their kernels one after another) or
+ * HSA_ENABLE_SDMA not 1 (the code-stream download becomes a blit kernel
+ * that waits for CUs under load).  Both must be set before the library
+ * loads; a converter logs this once after creating its contexts. */
+const char *jp2hip_env_check(void);
+
 /* Fill the Bucketeer recipe for JP2HIP_LOSSY / JP2HIP_LOSSLESS. */
 void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion);
 
@@ -169,7 +178,9 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
  * Strips may be uncompressed, LZW (5), Deflate (8, 32946; zlib streams) or
  * PackBits (32773), with or without
  * horizontal differencing (Predictor 2); compressed strips are decoded on
- * the GPU (one lane per strip) before ingest.  For a compressed file
+ * the GPU before ingest (LZW segment-parallel: a wave finds a strip's
+ * Clear-code segments, a wave per segment resolves its codes; Deflate and
+ * PackBits a wave per strip).  For a compressed file
  * `offsets` receives 2 * nstrips entries: the strip offsets, then their byte
  * counts (layout->strip_bytes points at the second half).  Tiled TIFFs
  * (TileWidth/TileLength) are described the same way, one entry per tile,
@@ -228,6 +239,26 @@ int jp2hip_encode_device_split(jp2hip_ctx *ctx, const void *d_src, size_t src_le
                                const jp2hip_recipe *recipe, const jp2hip_split *split,
                                uint8_t **out, size_t *out_len, uint64_t *file_offset,
                                uint64_t *file_len, jp2hip_stats *stats);
+
+/* The tile-split behind Converter.convert (Converter.java:22 ->
+ * jp2hip_encode_file / jp2hip_encode_tiff on ctx): gives ctx `n` peer
+ * contexts, one on each HIP ordinal in `ordinals` (created here, owned by ctx;
+ * an ordinal may repeat, or be ctx's own device).  From then on an image of at
+ * least `min_pixels` pixels (width x height) given to ctx is encoded as a
+ * tile-split over world = n + 1 ranks -- ctx is rank 0, peer i rank i + 1 --
+ * each rank a thread of this call: it reads its band's strips from the TIFF
+ * (mapped, not read whole), uploads them to its own GPU, and writes its part
+ * at its offset of the output file; the ranks' exchanges are summed on the
+ * host (no caller callback, no RCCL needed in-process).  The file is
+ * byte-identical to the single-GPU encode.  Smaller images take the
+ * single-GPU path.  n = 0 removes the peers.  Not to be called while ctx is
+ * encoding.  Returns 0 or < 0. */
+int jp2hip_split_peers(jp2hip_ctx *ctx, const int32_t *ordinals, int32_t n, int64_t min_pixels);
+
+/* Width x height of a TIFF file from its header (the file is mapped, not
+ * read), or < 0 with jp2hip_last_error(): lets a converter route an
+ * oversized image to its split context before converting it. */
+int64_t jp2hip_tiff_pixels(const char *tiff_path_utf8);
 
 /* Host-only: global layer thresholds from this rank's hull segments (slope
  * keys descending, inclusive byte sums) -- the exchange step of the split

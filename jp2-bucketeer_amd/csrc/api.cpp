@@ -9,8 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstddef>
@@ -22,6 +24,9 @@
 #include <thread>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "gpu_encoder.h"
@@ -46,6 +51,14 @@ struct jp2hip_ctx {
     jp2hip_config cfg;
     int threads = 1;
     PlanCache pc;
+    // tile-split members (jp2hip_split_peers): images of at least
+    // split_min_pixels are encoded by this context (rank 0) and these
+    // (ranks 1..), owned here
+    std::vector<jp2hip_ctx *> peers;
+    int64_t split_min_pixels = 0;
+    ~jp2hip_ctx() {
+        for (jp2hip_ctx *p : peers) jp2hip_destroy(p);
+    }
 };
 
 namespace {
@@ -817,6 +830,259 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     return 0;
 }
 
+// ---- tile-split inside the library (jp2hip_split_peers) ----
+// The ranks of one encode are threads of this process, one per member
+// context (each with its own GPU and stream); their exchanges (split.cpp,
+// encode_split_core) are summed here on the host: a few hundred vectors of at
+// most 1 025 int64 per image, nothing that needs RCCL.  A rank that fails
+// before an exchange, or returns, aborts the group, so no rank waits forever
+// in an exchange another rank will never join.
+class HostGroup {
+  public:
+    explicit HostGroup(int world) : world_(world) {}
+    int reduce(int64_t *v, int n) {
+        std::unique_lock<std::mutex> lk(mu_);
+        if (aborted_ || n < 0) return -1;
+        if (arrived_ == 0) {
+            acc_.assign((size_t)n, 0);
+            n_ = n;
+        } else if (n != n_) {  // ranks out of step: a bug, never a wrong sum
+            aborted_ = true;
+            cv_.notify_all();
+            return -1;
+        }
+        for (int i = 0; i < n; i++) acc_[(size_t)i] += v[i];
+        const uint64_t g = gen_;
+        if (++arrived_ == world_) {
+            res_[g & 1].swap(acc_);  // generation g+2 reuses it only after every rank copied it
+            arrived_ = 0;
+            gen_++;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lk, [&] { return gen_ != g || aborted_; });
+            if (gen_ == g) return -1;  // aborted before this exchange completed
+        }
+        std::copy(res_[g & 1].begin(), res_[g & 1].begin() + n, v);
+        return 0;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu_);
+        aborted_ = true;
+        cv_.notify_all();
+    }
+    static int call(void *user, int64_t *v, int32_t n) { return static_cast<HostGroup *>(user)->reduce(v, n); }
+
+  private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int world_, arrived_ = 0, n_ = 0;
+    uint64_t gen_ = 0;
+    bool aborted_ = false;
+    std::vector<int64_t> acc_, res_[2];
+};
+
+// The strips (or compressed strips / tiles, whole) that image rows
+// [row0, row1) read, as (file offset, bytes, strip-table index): what one rank
+// uploads.  The C++ form of jp2hip.split.band_strips.
+struct BandCopy {
+    uint64_t src, n;
+    size_t idx;
+};
+bool band_units(const jp2hip_layout &lay, size_t flen, int row0, int row1, std::vector<BandCopy> &cp,
+                std::string &err) {
+    cp.clear();
+    if (row1 <= row0) return true;
+    const bool packed = lay.compression > 1 || lay.tile_width > 0, tiled = lay.tile_width > 0;
+    const int uh = tiled ? lay.tile_height : lay.rows_per_strip;
+    if (uh <= 0 || lay.width <= 0 || lay.height <= 0 || (packed && !lay.strip_bytes) || !lay.strip_offsets) {
+        err = "layout: bad strip table";
+        return false;
+    }
+    const int planes = lay.planar == 2 ? lay.components : 1;
+    const int64_t across = tiled ? (lay.width + (int64_t)lay.tile_width - 1) / lay.tile_width : 1;
+    const int64_t urows = (lay.height + (int64_t)uh - 1) / uh, per_plane = across * urows;
+    if (per_plane * planes > lay.nstrips) {
+        err = tiled ? "layout: too few tiles" : "layout: too few strips";
+        return false;
+    }
+    const uint64_t row_bytes = (uint64_t)lay.width * (uint64_t)(lay.planar == 2 ? 1 : lay.components) * (lay.bits / 8);
+    const int64_t u0 = row0 / uh, u1 = std::min<int64_t>(urows, (row1 + (int64_t)uh - 1) / uh);
+    for (int p = 0; p < planes; p++)
+        for (int64_t u = u0; u < u1; u++)
+            for (int64_t x = 0; x < across; x++) {
+                const size_t i = (size_t)(p * per_plane + u * across + x);
+                const uint64_t o = lay.strip_offsets[i];
+                const uint64_t n = packed ? lay.strip_bytes[i]
+                                          : (uint64_t)std::min<int64_t>(uh, lay.height - u * uh) * row_bytes;
+                if (o > flen || n > flen - o) {
+                    err = "tiff: strip " + std::to_string(i) + " out of range";
+                    return false;
+                }
+                cp.push_back({o, n, i});
+            }
+    return true;
+}
+
+struct RankResult {
+    int rc = -1;
+    std::string err;
+    uint8_t *part = nullptr;
+    size_t part_len = 0;
+    uint64_t off = 0, flen = 0;
+    jp2hip_stats st;
+};
+
+// One rank of a host-driven tile-split: gather the band's strips from the
+// TIFF in host memory into pinned memory, upload them to member `m`, run the
+// split encode, and (fd >= 0) write the part at its offset of the output file.
+void split_rank(jp2hip_ctx *m, int rank, int world, HostGroup &grp, const uint8_t *file, size_t flen,
+                const jp2hip_layout &lay, int conversion, const jp2hip_recipe &rc, int fd, double t0,
+                RankResult &o) {
+    std::memset(&o.st, 0, sizeof o.st);
+    int r0 = 0, r1 = 0;
+    jp2hip_split_rows(lay.height, rc.tile_h, rc.flush_period, rank, world, &r0, &r1);
+    std::vector<BandCopy> cp;
+    if (!band_units(lay, flen, r0, r1, cp, o.err)) {
+        grp.abort();
+        return;
+    }
+    size_t tot = 0;
+    for (const BandCopy &c : cp) tot += c.n;
+    uint8_t *h = out_alloc(std::max<size_t>(tot, 1));  // pinned: the upload is one DMA
+    if (!h) {
+        o.err = "out of (pinned) host memory";
+        grp.abort();
+        return;
+    }
+    const bool packed = lay.compression > 1 || lay.tile_width > 0;
+    std::vector<uint64_t> offs((size_t)lay.nstrips * (packed ? 2 : 1), 0);
+    size_t pos = 0;
+    for (const BandCopy &c : cp) {
+        std::memcpy(h + pos, file + c.src, c.n);
+        offs[c.idx] = pos;
+        if (packed) offs[(size_t)lay.nstrips + c.idx] = c.n;
+        pos += c.n;
+    }
+    jp2hip_layout bl = lay;
+    bl.strip_offsets = offs.data();
+    bl.strip_bytes = packed ? offs.data() + lay.nstrips : nullptr;
+    {
+        std::lock_guard<std::mutex> lk(m->mu);
+        if (!m->gpu.upload_source(h, std::max<size_t>(tot, 1), o.err)) {
+            grp.abort();
+        } else {
+            jp2hip_split sp{rank, world, &HostGroup::call, &grp};
+            o.rc = encode_split_core(m, m->gpu.source(), std::max<size_t>(tot, 1), &bl, conversion, &rc, &sp,
+                                     &o.part, &o.part_len, &o.off, &o.flen, &o.st, t0);
+            if (o.rc != 0) o.err = g_err;
+            grp.abort();  // harmless after the last exchange; wakes the others after a failure
+        }
+        (void)hipStreamSynchronize(m->gpu.get_stream());  // the upload has read `h`
+    }
+    out_free(h);
+    if (o.rc == 0 && fd >= 0) {
+        size_t done = 0;
+        while (done < o.part_len) {
+            const ssize_t k = pwrite(fd, o.part + done, o.part_len - done, (off_t)(o.off + done));
+            if (k <= 0) {
+                o.rc = -1;
+                o.err = "cannot write output";
+                break;
+            }
+            done += (size_t)k;
+        }
+    }
+}
+
+// A whole-image encode split across ctx (rank 0) and its peers: the TIFF
+// bytes are in host memory; the result goes to `fd` (each rank writes its
+// part) or, fd < 0, into one pinned buffer *out.
+int encode_split_host(jp2hip_ctx *ctx, const uint8_t *file, size_t flen, const jp2hip_layout &lay, int conversion,
+                      const jp2hip_recipe *recipe, int fd, uint8_t **out, size_t *out_len, jp2hip_stats *stats,
+                      double t0) {
+    if (conversion != JP2HIP_LOSSY && conversion != JP2HIP_LOSSLESS)
+        return fail("conversion must be JP2HIP_LOSSY (0) or JP2HIP_LOSSLESS (1)");
+    const jp2hip_recipe rc = recipe_of(recipe, conversion);
+    std::vector<jp2hip_ctx *> members{ctx};
+    members.insert(members.end(), ctx->peers.begin(), ctx->peers.end());
+    const int world = (int)members.size();
+    HostGroup grp(world);
+    std::vector<RankResult> res((size_t)world);
+    std::vector<std::thread> th;
+    for (int r = 1; r < world; r++)
+        th.emplace_back([&, r] {
+            split_rank(members[(size_t)r], r, world, grp, file, flen, lay, conversion, rc, fd, t0, res[(size_t)r]);
+        });
+    split_rank(ctx, 0, world, grp, file, flen, lay, conversion, rc, fd, t0, res[0]);
+    for (std::thread &t : th) t.join();
+    // report the rank that failed first-hand, not one that saw the abort
+    const RankResult *bad = nullptr;
+    for (const RankResult &r : res)
+        if (r.rc != 0 && (!bad || (bad->err.rfind("split:", 0) == 0 && r.err.rfind("split:", 0) != 0))) bad = &r;
+    if (bad) {
+        const std::string e = bad->err.empty() ? "split: encode failed" : bad->err;
+        for (RankResult &r : res) out_free(r.part);
+        return fail(e);
+    }
+    const uint64_t total = res[0].flen;
+    if (fd < 0) {
+        uint8_t *buf = out_alloc((size_t)total);
+        if (!buf) {
+            for (RankResult &r : res) out_free(r.part);
+            return fail("out of (pinned) host memory");
+        }
+        for (const RankResult &r : res) std::memcpy(buf + r.off, r.part, r.part_len);
+        *out = buf;
+        *out_len = (size_t)total;
+    }
+    for (RankResult &r : res) out_free(r.part);
+    if (stats) {
+        *stats = res[0].st;
+        for (int r = 1; r < world; r++) {
+            stats->codeblocks += res[(size_t)r].st.codeblocks;
+            stats->coded_passes += res[(size_t)r].st.coded_passes;
+            stats->t1_bytes += res[(size_t)r].st.t1_bytes;
+            stats->mq_decisions += res[(size_t)r].st.mq_decisions;
+            stats->host_waits = std::max(stats->host_waits, res[(size_t)r].st.host_waits);
+        }
+        stats->out_bytes = (int64_t)total;
+        stats->total_ms = now_ms() - t0;
+    }
+    return 0;
+}
+
+bool wants_split(const jp2hip_ctx *ctx, const jp2hip_layout &lay) {
+    return !ctx->peers.empty() && (int64_t)lay.width * lay.height >= ctx->split_min_pixels;
+}
+
+// A read-only mapping of a whole file (the split path reads each rank's band
+// of a multi-GB TIFF straight from the page cache, in parallel).
+struct MappedFile {
+    int fd = -1;
+    const uint8_t *p = nullptr;
+    size_t n = 0;
+    bool open(const char *path) {
+        fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) return false;
+        struct stat sb;
+        if (fstat(fd, &sb) != 0 || sb.st_size <= 0) return false;
+        n = (size_t)sb.st_size;
+        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) return false;
+        p = (const uint8_t *)m;
+        return true;
+    }
+    ~MappedFile() {
+        if (p) munmap((void *)p, n);
+        if (fd >= 0) ::close(fd);
+    }
+};
+
+std::string temp_name(const char *out_path) {
+    return std::string(out_path) + ".part-" + std::to_string((long)getpid()) + "-" +
+           std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000);
+}
+
 }  // namespace
 
 extern "C" {
@@ -855,6 +1121,27 @@ void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
     if (recipe) default_recipe(recipe, conversion);
 }
 
+// Contexts alive in this process, for jp2hip_env_check.
+static std::atomic<int> g_live_contexts{0};
+
+const char *jp2hip_env_check(void) {
+    thread_local std::string msg;
+    msg.clear();
+    const char *q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int queues = q && *q ? std::atoi(q) : 4;  // HIP's default
+    const int live = g_live_contexts.load();
+    if (live > queues)
+        msg += "GPU_MAX_HW_QUEUES=" + std::to_string(queues) + " is below the " + std::to_string(live) +
+               " contexts of this process (contexts sharing a hardware queue run their kernels one after "
+               "another; set it to contexts per GPU + 4 before the library loads); ";
+    const char *sd = std::getenv("HSA_ENABLE_SDMA");
+    if (!sd || std::strcmp(sd, "1") != 0)
+        msg += "HSA_ENABLE_SDMA is not 1 (the code-stream download then runs as a blit kernel that "
+               "waits for CUs under load); ";
+    if (!msg.empty()) msg.resize(msg.size() - 2);
+    return msg.c_str();
+}
+
 int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg) {
     if (!out) return fail("null output pointer");
     *out = nullptr;
@@ -879,10 +1166,15 @@ int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg) {
         return fail(err);
     }
     *out = c;
+    g_live_contexts++;
     return 0;
 }
 
-void jp2hip_destroy(jp2hip_ctx *ctx) { delete ctx; }
+void jp2hip_destroy(jp2hip_ctx *ctx) {
+    if (!ctx) return;
+    g_live_contexts--;  // its peers count themselves down as they go
+    delete ctx;
+}
 
 int jp2hip_tiff_layout(const uint8_t *tiff, size_t len, jp2hip_layout *layout, uint64_t *offsets,
                        int32_t max_offsets) {
@@ -919,6 +1211,8 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
     jp2hip_layout lay;
     std::vector<uint64_t> offs;
     if (parse_tiff(tiff, len, &lay, offs)) return -1;
+    if (wants_split(ctx, lay))
+        return encode_split_host(ctx, tiff, len, lay, conversion, recipe, -1, out, out_len, stats, t0);
     std::lock_guard<std::mutex> lk(ctx->mu);
     std::string err;
     double th = now_ms();
@@ -930,24 +1224,31 @@ int jp2hip_encode_tiff(jp2hip_ctx *ctx, const uint8_t *tiff, size_t len, int con
 int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path, const char *out_path, int conversion,
                        const jp2hip_recipe *recipe, jp2hip_stats *stats) {
     if (!ctx || !tiff_path || !out_path) return fail("null argument");
-    FILE *f = std::fopen(tiff_path, "rb");
-    if (!f) return fail(std::string("cannot open TIFF: ") + tiff_path);
-    std::vector<uint8_t> buf;
-    if (std::fseek(f, 0, SEEK_END) == 0) {
-        long n = std::ftell(f);
-        if (n > 0) {
-            buf.resize((size_t)n);
-            std::fseek(f, 0, SEEK_SET);
-            if (std::fread(buf.data(), 1, buf.size(), f) != buf.size()) buf.clear();
-        }
+    const double t0 = now_ms();
+    MappedFile mf;
+    if (!mf.open(tiff_path)) {
+        if (mf.fd < 0) return fail(std::string("cannot open TIFF: ") + tiff_path);
+        return fail(std::string("cannot read TIFF: ") + tiff_path);
     }
-    std::fclose(f);
-    if (buf.empty()) return fail(std::string("cannot read TIFF: ") + tiff_path);
+    jp2hip_layout lay;
+    std::vector<uint64_t> offs;
+    if (parse_tiff(mf.p, mf.n, &lay, offs)) return -1;
+    const std::string tmp = temp_name(out_path);
+    if (wants_split(ctx, lay)) {
+        // every rank writes its part at its offset of the temp file
+        const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+        if (fd < 0) return fail(std::string("cannot write output: ") + out_path);
+        const int rc = encode_split_host(ctx, mf.p, mf.n, lay, conversion, recipe, fd, nullptr, nullptr, stats, t0);
+        const bool closed = ::close(fd) == 0;
+        if (rc != 0 || !closed || std::rename(tmp.c_str(), out_path) != 0) {
+            std::remove(tmp.c_str());
+            return rc != 0 ? -1 : fail(std::string("cannot write output: ") + out_path);
+        }
+        return 0;
+    }
     uint8_t *out = nullptr;
     size_t olen = 0;
-    if (jp2hip_encode_tiff(ctx, buf.data(), buf.size(), conversion, recipe, &out, &olen, stats)) return -1;
-    std::string tmp = std::string(out_path) + ".part-" + std::to_string((long)getpid()) + "-" +
-                      std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000);
+    if (jp2hip_encode_tiff(ctx, mf.p, mf.n, conversion, recipe, &out, &olen, stats)) return -1;
     FILE *o = std::fopen(tmp.c_str(), "wb");
     if (!o) {
         out_free(out);
@@ -960,6 +1261,39 @@ int jp2hip_encode_file(jp2hip_ctx *ctx, const char *tiff_path, const char *out_p
         std::remove(tmp.c_str());
         return fail(std::string("cannot write output: ") + out_path);
     }
+    if (stats) stats->total_ms = now_ms() - t0;
+    return 0;
+}
+
+int64_t jp2hip_tiff_pixels(const char *tiff_path) {
+    if (!tiff_path) return fail("null argument");
+    MappedFile mf;
+    if (!mf.open(tiff_path)) return fail(std::string("cannot open TIFF: ") + tiff_path);
+    jp2hip_layout lay;
+    std::vector<uint64_t> offs;
+    if (parse_tiff(mf.p, mf.n, &lay, offs)) return -1;
+    return (int64_t)lay.width * lay.height;
+}
+
+int jp2hip_split_peers(jp2hip_ctx *ctx, const int32_t *ordinals, int32_t n, int64_t min_pixels) {
+    if (!ctx || n < 0 || (n > 0 && !ordinals)) return fail("null argument");
+    if (n > 64) return fail("split: at most 64 peers");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<jp2hip_ctx *> made;
+    for (int i = 0; i < n; i++) {
+        jp2hip_config c = ctx->cfg;
+        c.device = ordinals[i];
+        jp2hip_ctx *p = nullptr;
+        if (jp2hip_create(&p, &c) != 0) {
+            const std::string e = std::string("split peer on device ") + std::to_string(ordinals[i]) + ": " + g_err;
+            for (jp2hip_ctx *q : made) jp2hip_destroy(q);
+            return fail(e);
+        }
+        made.push_back(p);
+    }
+    for (jp2hip_ctx *p : ctx->peers) jp2hip_destroy(p);
+    ctx->peers = made;
+    ctx->split_min_pixels = std::max<int64_t>(0, min_pixels);
     return 0;
 }
 

@@ -70,7 +70,8 @@ EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_device
            "jp2hip_batch_create", "jp2hip_batch_submit", "jp2hip_batch_wait", "jp2hip_batch_pending",
            "jp2hip_batch_destroy",
            # tile-split path (csrc/split.cpp + api.cpp; bound in jp2hip.split)
-           "jp2hip_split_rows", "jp2hip_encode_device_split", "jp2hip_split_thresholds")
+           "jp2hip_split_rows", "jp2hip_encode_device_split", "jp2hip_split_thresholds",
+           "jp2hip_split_peers", "jp2hip_tiff_pixels", "jp2hip_env_check")
 
 
 # int (*)(void *user, int64_t *values, int32_t n): in-place sum over ranks, 0 ok
@@ -118,6 +119,10 @@ def lib():
                                              POINTER(Recipe), POINTER(Split),
                                              POINTER(POINTER(c_uint8)), POINTER(c_size_t),
                                              POINTER(c_uint64), POINTER(c_uint64), POINTER(Stats)]
+    L.jp2hip_split_peers.argtypes = [c_void_p, POINTER(c_int32), c_int32, c_int64]
+    L.jp2hip_env_check.restype = c_char_p
+    L.jp2hip_tiff_pixels.argtypes = [c_char_p]
+    L.jp2hip_tiff_pixels.restype = c_int64
     L.jp2hip_split_thresholds.argtypes = [POINTER(c_uint64), POINTER(c_int64), c_int64,
                                           POINTER(c_int64), c_int32, POINTER(Split),
                                           POINTER(c_uint64)]
@@ -150,6 +155,20 @@ def device_ordinals() -> list[int]:
     buf = (c_int32 * n)()
     n = min(n, int(lib().jp2hip_device_ordinals(buf, n)))
     return [int(buf[i]) for i in range(n)]
+
+
+def env_check() -> str:
+    """"" or what the process environment should change for the contexts
+    alive in it (jp2hip_env_check: GPU_MAX_HW_QUEUES, HSA_ENABLE_SDMA)."""
+    return lib().jp2hip_env_check().decode()
+
+
+def tiff_pixels(path) -> int:
+    """Width x height of a TIFF file, from its header (jp2hip_tiff_pixels)."""
+    n = int(lib().jp2hip_tiff_pixels(os.fsencode(path)))
+    if n < 0:
+        raise Jp2hipError(last_error())
+    return n
 
 
 def recipe(conversion: int, **overrides) -> Recipe:
@@ -309,6 +328,14 @@ class Encoder:
         if rc != 0:
             raise Jp2hipError(last_error())
         return self._take(out, n), off.value, flen.value, st
+
+    def split_peers(self, ordinals: list[int], min_pixels: int = 0):
+        """Tile-split this encoder's images of >= min_pixels pixels across
+        itself and one peer context per entry of ``ordinals``
+        (jp2hip_split_peers); ``[]`` removes the peers."""
+        arr = (c_int32 * max(1, len(ordinals)))(*ordinals)
+        if lib().jp2hip_split_peers(self._h, arr, len(ordinals), min_pixels) != 0:
+            raise Jp2hipError(last_error())
 
     def encode_file(self, tiff_path: str, out_path: str, conversion: int,
                     rcp: Recipe | None = None):

@@ -16,6 +16,7 @@ runs in-process on MI355X through libjp2hip instead of a kdu_compress child.
 from __future__ import annotations
 
 import enum
+import logging
 import os
 import shutil
 import subprocess
@@ -98,19 +99,28 @@ class OpenJPEGConverter(Converter):
 
 class GpuConverter(Converter):
     """MI355X converter: libjp2hip in-process, a pool of contexts (images in
-    flight) on every visible gfx950 device.
+    flight) on every visible gfx950 device, plus one split context whose peers
+    cover ``split_devices`` (default: every device, when there are several):
+    an image of at least ``split_min_pixels`` (default 256 MP, or
+    ``JP2HIP_SPLIT_MIN_PIXELS``) is tile-split across those GPUs inside
+    jp2hip_encode_file (jp2hip_split_peers), a smaller one takes a pool
+    context.
 
     Safe for concurrent callers (the reference runs one ImageWorkerVerticle
     thread, MainVerticle.java:229-231; raising that count gives each call its
-    own GPU context from the pool).
+    own GPU context from the pool; oversized images take turns on the split
+    context).
     """
 
     WORKING_DIR_NAME = "jp2hip"
+    SPLIT_MIN_PIXELS = 256_000_000
 
-    def __init__(self, devices: list[int] | None = None, host_threads: int = 0, per_gpu: int = 1):
+    def __init__(self, devices: list[int] | None = None, host_threads: int = 0, per_gpu: int = 1,
+                 split_devices: list[int] | None = None, split_min_pixels: int | None = None):
         self.tmp_dir = Path(tempfile.gettempdir()) / self.WORKING_DIR_NAME
         self._pool, self._free = [], []
         self._cv = threading.Condition()
+        self._split, self._split_lock, self.split_world = None, threading.Lock(), 1
         self.unavailable = None  # reason every convert() fails with (GPU absent / init failed)
         try:
             self.tmp_dir.mkdir(parents=True, exist_ok=True)
@@ -118,16 +128,28 @@ class GpuConverter(Converter):
             raise IOError(BUCKETEER_002.format(self.tmp_dir)) from e
         if devices is None:
             devices = _lib.device_ordinals()
+        if split_devices is None:
+            split_devices = list(devices) if len(devices) > 1 else []
+        if split_min_pixels is None:
+            split_min_pixels = int(os.environ.get("JP2HIP_SPLIT_MIN_PIXELS", self.SPLIT_MIN_PIXELS))
+        self.split_min_pixels = split_min_pixels
         try:
             self._pool = [_lib.Encoder(d, host_threads) for _ in range(max(1, per_gpu)) for d in devices]
+            if len(split_devices) > 1:
+                self._split = _lib.Encoder(split_devices[0], host_threads)
+                self._split.split_peers(list(split_devices[1:]), split_min_pixels)
+                self.split_world = len(split_devices)
         except _lib.Jp2hipError as e:
-            for enc in self._pool:
-                enc.close()
+            self.close()
             self._pool = []
             raise IOError(BUCKETEER_001.format(f"(GPU converter init: {e})")) from e
         if not self._pool:
             raise IOError(BUCKETEER_001.format("(no gfx950 device)"))
         self._free = list(self._pool)
+        # the slow configurations the library can see (queues, SDMA): logged once
+        self.env_advice = _lib.env_check()
+        if self.env_advice:
+            logging.getLogger(__name__).warning("libjp2hip: %s", self.env_advice)
 
     @classmethod
     def unavailable_converter(cls, reason: str) -> "GpuConverter":
@@ -138,6 +160,7 @@ class GpuConverter(Converter):
         c = cls.__new__(cls)
         c.tmp_dir = Path(tempfile.gettempdir()) / cls.WORKING_DIR_NAME
         c._pool, c._free, c._cv = [], [], threading.Condition()
+        c._split, c._split_lock, c.split_world = None, threading.Lock(), 1
         c.unavailable = reason
         return c
 
@@ -159,18 +182,27 @@ class GpuConverter(Converter):
         jpx = self.tmp_dir / _jpx_name(image_id)
         if not os.access(jpx.parent, os.W_OK):
             raise IOError(BUCKETEER_002.format(jpx))
-        enc = self._acquire()
         try:
-            enc.encode_file(str(tiff.absolute()), str(jpx), int(Conversion(conversion)))
+            big = self._split is not None and _lib.tiff_pixels(str(tiff.absolute())) >= self.split_min_pixels
+            if big:
+                with self._split_lock:
+                    self._split.encode_file(str(tiff.absolute()), str(jpx), int(Conversion(conversion)))
+                return jpx
+            enc = self._acquire()
+            try:
+                enc.encode_file(str(tiff.absolute()), str(jpx), int(Conversion(conversion)))
+            finally:
+                self._release(enc)
         except (_lib.Jp2hipError, ValueError) as e:
             raise IOError(BUCKETEER_001.format(image_id) + f": {e}") from e
-        finally:
-            self._release(enc)
         return jpx
 
     def close(self):
         for e in self._pool:
             e.close()
+        if self._split is not None:
+            self._split.close()
+            self._split = None
 
 
 class ConverterFactory:

@@ -263,3 +263,27 @@ def test_output_view_keeps_the_pinned_buffer_alive(monkeypatch):
     o2 = _lib.Output(ptr, 8)
     o2.close()
     assert len(freed) == 2
+
+
+def test_tiff_pixels_reads_only_the_header(tmp_path):
+    """jp2hip_tiff_pixels: a converter's routing check (split context for
+    oversized images) -- no GPU needed, errors through jp2hip_last_error."""
+    img = im.synth_rgb8(37, 53, seed=1)
+    p = tmp_path / "熵.tif"
+    p.write_bytes(im.tiff_bytes(img))
+    assert jp2hip._lib.tiff_pixels(p) == 37 * 53
+    bad = tmp_path / "bad.tif"
+    bad.write_bytes(b"II*\0garbage")
+    with pytest.raises(jp2hip.Jp2hipError):
+        jp2hip._lib.tiff_pixels(bad)
+    with pytest.raises(jp2hip.Jp2hipError, match="cannot open"):
+        jp2hip._lib.tiff_pixels(tmp_path / "missing.tif")
+
+
+def test_env_check_names_the_slow_settings(monkeypatch):
+    """jp2hip_env_check reads the process environment at the call (no
+    contexts exist without a GPU, so only the SDMA advice can show)."""
+    monkeypatch.delenv("HSA_ENABLE_SDMA", raising=False)
+    assert "HSA_ENABLE_SDMA" in jp2hip._lib.env_check()
+    monkeypatch.setenv("HSA_ENABLE_SDMA", "1")
+    assert jp2hip._lib.env_check() == ""
