@@ -200,6 +200,58 @@ def cpu_reference_opj(img):
                       "Appendix A recipe"}
 
 
+def cpu_reference_opj_lossless(crop_h=4096, crop_w=2048):
+    """The lossless CPU baseline (the conversion the reference's service runs,
+    ImageWorkerVerticle.java:64): opj_compress lossless 5/3 with C3's recipe
+    (1024^2 tiles, Appendix A mapping) on a BOUNDED sample -- a 4096x2048 crop
+    of the C3 image per process, `nproc` concurrent processes on this run's
+    host cores (a full 80 MP C3 image takes opj ~140 s per core, far past the
+    bench's budget).  value = processes x crop MP / wall time."""
+    import imaging as im
+    tool = im.opj("opj_compress")
+    if tool is None:
+        return None
+    cores, model = host_cpu()
+    crop = np.ascontiguousarray(make_image("c3", seed=2)[:crop_h, :crop_w])
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "c3crop.tif")
+        with open(src, "wb") as f:
+            f.write(im.tiff_bytes(crop))
+        cmd = [tool, "-i", src, "-n", "7", "-t", "1024,1024", "-b", "64,64", "-p", "RPCL", "-SOP", "-EPH", "-PLT",
+               "-TP", "R", "-c", "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]",
+               "-r", "64,32,16,8,4,1"]
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen(cmd + ["-o", os.path.join(d, f"o{i}.j2k")], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL) for i in range(cores)]
+        ok = all(p.wait() == 0 for p in ps)
+        dt = time.perf_counter() - t0
+    if not ok:
+        return None
+    mp = cores * crop_h * crop_w / 1e6
+    return {"value": round(mp / dt, 3), "unit": "MP/s", "cores": cores, "kind": "reference",
+            "tool": "opj_compress 2.4.0 (north_star's stand-in for the proprietary kdu_compress)",
+            "cpu_model": model, "seconds": round(dt, 2),
+            "sample": f"{cores} concurrent processes, each a {crop_w}x{crop_h} crop of the C3 image "
+                      "(RGB16), lossless 5/3, C3 recipe (1024^2 tiles)"}
+
+
+def d2h_peak(nbytes=256 << 20, reps=5):
+    """Device -> pinned host copy rate (GB/s) on this box: the bound of a
+    lossless encode, whose code-stream (~34 bpp for C3) must cross PCIe."""
+    import torch
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    best = 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        h.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
+    return best
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN/pmc_traffic.json, made by tests/tools/pmc_summary.py from two
@@ -331,8 +383,10 @@ def run(args):
     value = world * mp * total / dt_max
     # PCIe-inclusive: TIFF bytes in pinned host memory -> jp2hip_encode_tiff
     # (header parse, H2D of the 72 MB file, encode) -> JPX bytes in host memory
-    dt_h, _ = timed(lambda e: e.encode_tiff_ptr(h_src.data_ptr(), h_src.numel(), jp2hip.LOSSY, rc, copy=False))
-    dt_h_max = barrier_max(world, dt_h, device)
+    dt_h_max = None
+    if not args.no_pcie:
+        dt_h, _ = timed(lambda e: e.encode_tiff_ptr(h_src.data_ptr(), h_src.numel(), jp2hip.LOSSY, rc, copy=False))
+        dt_h_max = barrier_max(world, dt_h, device)
     res = None
     if rank == 0:
         flat = stages
@@ -380,10 +434,11 @@ def run(args):
                        "rate_iterations": int(max(a["rate_iterations"] for a in alone))},
             # the same steps with the TIFF in pinned host memory and the H2D
             # inside the timed span (PCIe-inclusive rate)
-            "value_pcie_inclusive": {"value": round(world * mp * total / dt_h_max, 3), "unit": "MP/s",
-                                     "ms_per_step": round(dt_h_max * 1e3 / args.steps, 3),
-                                     "timed_span": "TIFF bytes in pinned host memory -> jp2hip_encode_tiff (parse, "
-                                                   "H2D, encode) -> JPX bytes in host memory"},
+            "value_pcie_inclusive": ({"value": round(world * mp * total / dt_h_max, 3), "unit": "MP/s",
+                                      "ms_per_step": round(dt_h_max * 1e3 / args.steps, 3),
+                                      "timed_span": "TIFF bytes in pinned host memory -> jp2hip_encode_tiff (parse, "
+                                                    "H2D, encode) -> JPX bytes in host memory"}
+                                     if dt_h_max else None),
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(ach * 1e9 / HBM_PEAK, 5),
@@ -431,10 +486,13 @@ def c5_band(rank, world, threads=16):
     from ctypes import POINTER, c_uint64, cast
 
     import imaging as im
+    import jp2hip
     from jp2hip import split as js
     from jp2hip._lib import Layout
     w, h, rps = C5["w"], C5["h"], C5["rps"]
-    r0, r1 = js.split_rows(h, C5["tile"], rank, world, 1024)
+    # the band the encoder reads: its own recipe's tile height and flush period
+    rc = jp2hip.recipe(jp2hip.LOSSY, levels=C5["levels"])
+    r0, r1 = js.split_rows(h, rc.tile_h, rank, world, rc.flush_period)
     buf = np.empty((r1 - r0, w), "<u2")
     groups = list(range(r0, r1, C5["tile"]))
 
@@ -631,12 +689,18 @@ def main():
                     help="images per step (default: --inflight); value = MP of every image / time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lossless", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive C2 leg")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="C2 timed leg only: no PCIe-inclusive leg, lossless C3/C4, file-span, C5 or CPU "
+                         "baselines (the profiled configuration)")
     ap.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2",
                     help="c2: the headline (replicas); c4: CSV batch through the native per-GPU queue; "
                          "c5: one oversized image tile-split across ranks")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    if args.no_extras:
+        args.no_pcie = args.no_lossless = args.no_cpu_baseline = True
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}")
     # one hardware queue per in-flight context plus a few for the runtime's
@@ -666,8 +730,15 @@ def main():
         if not args.no_lossless:
             res["lossless_c3"] = lossless_c3(enc)
             res["lossless_c4"] = lossless_c4(local_device())
+        if not args.no_extras:
+            res["value_file_span"] = c2_file_span(local_device())
+            res["c5"] = c5_single_gpu(enc)
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_reference_opj(img)
+            res["cpu_baseline_lossless"] = cpu_reference_opj_lossless()
+            if res.get("lossless_c3") and res["cpu_baseline_lossless"]:
+                res["lossless_c3"]["vs_cpu_baseline_lossless"] = round(
+                    res["lossless_c3"]["mp_per_s_inflight_c_api"] / res["cpu_baseline_lossless"]["value"], 2)
             res["cpu_not_a_reference"] = cpu_oracle_not_a_reference(img)
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -737,16 +808,26 @@ def lossless_c3(enc, steps=2, inflight=4, n_each=3):
     value = npx / 1e6 * n_each * inflight / dt
     # SURVEY.md 8(d) full path at the measured bpp: B_dwt + 4C + 3 bpp / 8
     b_path = dwt_bytes_per_px(3, 2, 6) + 4 * 3 + 3 * bpp / 8
+    # the bound that matters for lossless: every code-stream byte (~34 bpp
+    # for C3) crosses PCIe to the host; device->pinned-host peak measured here
+    d2h = d2h_peak()
+    out_gbs = value * 1e6 * bpp / 8 / 1e9
     res.update({"inflight": inflight, "images": n_each * inflight, "mp_per_s_inflight_c_api": round(value, 3),
+                "roofline_pcie": {"bound": "pcie_d2h", "achieved": round(out_gbs, 2), "peak": round(d2h, 2),
+                                  "unit": "GB/s", "frac": round(out_gbs / d2h, 4),
+                                  "def": "code-stream bytes/s leaving the GPU (MP/s x bpp / 8) / measured "
+                                         "device->pinned-host copy rate"},
                 "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
                                   "achieved": round(b_path * value * 1e6 / 1e9, 2), "peak": HBM_PEAK / 1e9,
-                                  "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}})
+                                  "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5),
+                                  "note": "not the bound of a lossless encode: see roofline_pcie"}})
     for e in encs[1:]:
         e.close()
     return res
 
 
-def c4_batch(device, rows=16, ndistinct=2, contexts=8):
+def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=None, reader_threads=4,
+             uploader_threads=4, shape=(7000, 5000)):
     """C4 (configs[3]) on one GPU, reduced: a Bucketeer batch CSV of `rows`
     synthetic 5000x7000 RGB8 TIFFs (cycling over `ndistinct` files, as
     SURVEY.md 8(d) prescribes for the 10k-row batch) through the native batch
@@ -758,13 +839,16 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8):
     from concurrent.futures import ThreadPoolExecutor
 
     import imaging as im
+    import jp2hip
     from jp2hip import batch as jb
+    conv = jp2hip.LOSSLESS if conversion is None else conversion
+    make = make or (lambda i: im.synth_rgb8(7000, 5000, seed=i))
     work = tempfile.mkdtemp(prefix="jp2hip_c4_")
     try:
         def gen(i):
             pth = os.path.join(work, f"synth{i:02d}.tif")
             with open(pth, "wb") as f:
-                f.write(im.tiff_bytes(im.synth_rgb8(7000, 5000, seed=i), rows_per_strip=64))
+                f.write(im.tiff_bytes(make(i), rows_per_strip=64))
             return pth
 
         with ThreadPoolExecutor(ndistinct) as ex:
@@ -778,23 +862,24 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8):
         items = jb.read_batch_csv(csv_path, path_prefix=work)
         out_dir = os.path.join(work, "out")
         os.makedirs(out_dir, exist_ok=True)
-        with jb.BatchQueue(device=device, contexts=contexts) as q:
+        with jb.BatchQueue(device=device, contexts=contexts, reader_threads=reader_threads,
+                           uploader_threads=uploader_threads) as q:
             for k, it in enumerate(items[:contexts]):  # warm-up: device buffers of every context
-                q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k))
+                q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k), conv)
             q.drain()
             t0 = time.perf_counter()
             for it in items:
-                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)))
+                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)), conv)
             res = q.drain()
             dt = time.perf_counter() - t0
         ok = sum(1 for r in res if r["status"] == 0)
-        return 5000 * 7000 / 1e6 * ok / dt, dt, res
+        return shape[0] * shape[1] / 1e6 * ok / dt, dt, res
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
 
 def lossless_c4(device):
-    rows = 16
+    rows = 320
     value, dt, res = c4_batch(device, rows=rows)
     ok = [r for r in res if r["status"] == 0]
     bpp = 8 * float(np.mean([r["out_bytes"] for r in ok])) / (5000 * 7000) if ok else 0.0
@@ -806,6 +891,76 @@ def lossless_c4(device):
             "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
                               "achieved": round(b_path * value * 1e6 / 1e9, 2), "peak": HBM_PEAK / 1e9,
                               "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}}
+
+
+def c2_file_span(device, images=512, contexts=16):
+    """SURVEY.md 8(d)'s span for the headline workload: C2 (lossy 3 bpp) from
+    TIFF files on disk to JPX files written, through the native per-GPU queue
+    (reader threads: file -> pinned buffer + header parse; `contexts` encodes
+    in flight; uploader threads: atomic JPX write, stub upload reading every
+    byte, delete-after-upload), `images` images cycling over 4 distinct files,
+    timed from the first submit to the last upload."""
+    import imaging as im
+    import jp2hip
+    value, dt, res = c4_batch(device, rows=images, ndistinct=4, contexts=contexts, conversion=jp2hip.LOSSY,
+                              make=lambda i: im.synth_rgb8(4000, 6000, seed=1234 + i), reader_threads=8,
+                              uploader_threads=8, shape=(4000, 6000))
+    ok = [r for r in res if r["status"] == 0]
+    return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok),
+            "seconds": round(dt, 3), "contexts": contexts,
+            "out_bytes": int(np.mean([r["out_bytes"] for r in ok])) if ok else 0,
+            "timed_span": "first TIFF open -> last JPX written, uploaded (stub) and deleted; "
+                          "file read, H2D, encode, D2H, file write included"}
+
+
+def c5_single_gpu(enc, steps=2):
+    """C5 (configs[4]) at N=1: the full 40000x30000 Gray16 image, lossy 3 bpp,
+    7 levels, through the tile-split entry (jp2hip_encode_device_split) at
+    world 1, checked byte-equal to the single-image encode and, when the
+    committed fixture holds it, to the oracle's file (SHA-256 from
+    tests/golden/make_golden.py c5_full).  TIFF resident in HBM -> JPX bytes
+    in host memory, as the headline."""
+    import hashlib
+
+    import torch
+
+    import jp2hip
+    from jp2hip import split as js
+    band, lay, offs, rows = c5_band(0, 1)
+    d_src = torch.frombuffer(bytearray(band), dtype=torch.uint8).cuda()
+    del band
+    torch.cuda.synchronize()
+    rc = jp2hip.recipe(jp2hip.LOSSY, levels=C5["levels"])
+    sp = js.SingleGroup()
+    part, off, flen, st = enc.encode_device_split(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, sp.split(), rc)
+    single, _ = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
+    identical = single == part
+    sha = hashlib.sha256(single).hexdigest()
+    del single
+    oracle = None
+    try:
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+        if "c5_full" in g:
+            oracle = sha == g["c5_full"]["oracle_sha256"]
+    except (OSError, ValueError):
+        pass
+    times = []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        part, off, flen, st = enc.encode_device_split(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY,
+                                                      sp.split(), rc)
+        times.append(time.perf_counter() - t0)
+    npx = C5["w"] * C5["h"]
+    dt = min(times)
+    del d_src
+    torch.cuda.empty_cache()
+    return {"workload": "C5: 40000x30000 Gray16 -> JPX, lossy 9/7 3 bpp, 7 levels, 6 layers, 512^2 tiles, "
+                        "tile-split entry at world 1", "n_gpus": 1, "value": round(npx / 1e6 / dt, 3),
+            "unit": "MP/s", "seconds": round(dt, 4), "file_bytes": int(flen), "bpp": round(8 * flen / npx, 4),
+            "split_equals_single_encode": identical, "equals_oracle_sha256": oracle,
+            "codeblocks": int(st.codeblocks), "rate_iterations": int(st.rate_iterations),
+            "timed_span": "TIFF resident in HBM -> JPX bytes in host memory"}
 
 
 if __name__ == "__main__":

@@ -555,13 +555,29 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
     }
 }
 
+// The coder's byte ring: 64 bytes per lane.  Interleaved layout (default):
+// dword k of lane L's ring is LDS dword k * 64 + L, so the byte a lane stores
+// on every step lands in bank L whatever its position -- no bank conflicts
+// (the packed 68-byte-stride layout put the 64 lanes' data-dependent slots on
+// random banks: ~1 conflict cycle per LDS instruction).
+#ifndef JP2HIP_MQ_RING_IL
+#define JP2HIP_MQ_RING_IL 1
+#endif
+#if JP2HIP_MQ_RING_IL
+constexpr int kRingLaneStride = 4;
+__device__ __forceinline__ int ring_slot(int bp) { return ((bp & 60) << 6) | (bp & 3); }
+#else
+constexpr int kRingLaneStride = 68;
+__device__ __forceinline__ int ring_slot(int bp) { return bp & 63; }
+#endif
+
 __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
     uint32_t B = m.B;
     if (B != 0xFF && m.C >= 0x8000000u) {
         B++;
         m.C &= 0x7FFFFFFu;
     }
-    ring[m.bp & 63] = (uint8_t)B;  // bp = -1 -> slot 63, see mq_step
+    ring[ring_slot(m.bp)] = (uint8_t)B;  // bp = -1 -> slot 63, see mq_step
     m.bp++;
     const bool ff = B == 0xFF;
     m.B = ff ? (m.C >> 20) : (m.C >> 19);
@@ -636,7 +652,7 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
     // and never flushed before (ring_flush copies whole groups below bp).
     // Byte -1 (the MQ coder's initial pending byte, never output) lands in
     // slot 63, which byte 63 overwrites before that group is flushed
-    ring[m.bp & 63] = (uint8_t)Bc;
+    ring[ring_slot(m.bp)] = (uint8_t)Bc;
     uint32_t Cx = bo ? (C2 & ((1u << sh) - 1u)) : C1;
     int CTx = bo ? 27 - (int)sh : CT - n;
     int rem = n - s1;
@@ -656,9 +672,14 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
 // Copy the lane's completed 16-byte ring groups to the code-block output.
 __device__ __forceinline__ void ring_flush(const Mq &m, const uint8_t *ring, int &fl) {
     while (m.bp - fl >= 16) {
-        const uint32_t *g = (const uint32_t *)(ring + (fl & 63));
         uint4 v;
+#if JP2HIP_MQ_RING_IL
+        const uint32_t *g = (const uint32_t *)(ring + ring_slot(fl));
+        v.x = g[0]; v.y = g[64]; v.z = g[128]; v.w = g[192];
+#else
+        const uint32_t *g = (const uint32_t *)(ring + (fl & 63));
         v.x = g[0]; v.y = g[1]; v.z = g[2]; v.w = g[3];
+#endif
         if (fl + 16 <= m.cap) *(uint4 *)(m.out + fl) = v;
         fl += 16;
     }
@@ -683,7 +704,7 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 struct MqShared {
     uint32_t cxs[20 * 64];                 // 19 contexts + CX_PAD, lane-interleaved (modeller)
     uint32_t mqt[94];                      // state table
-    uint32_t rings[64 * 17];               // coder: 64-byte ring per lane at a 68-byte stride (banks)
+    uint32_t rings[64 * 17];               // coder: 64-byte ring per lane (ring_slot)
     // (the bucket bases are done with before the first chunk: one LDS slot,
     // 19.1 KB a workgroup, 8 per CU instead of 7)
     union {
@@ -817,7 +838,7 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
 __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
     const int lane = threadIdx.x & 63;
     const int b = sh.blk[lane];
-    uint8_t *ring = (uint8_t *)sh.rings + lane * 68;
+    uint8_t *ring = (uint8_t *)sh.rings + lane * kRingLaneStride;
     int fl = 0;  // bytes already copied from the ring
     Mq m;
     m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
@@ -855,7 +876,7 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
     const int nseg = sdone;
     m.A = sh.finA[lane];
     for (int i = fl; i < m.bp; i++)  // bytes still in the ring
-        if (i < m.cap) m.out[i] = ring[i & 63];
+        if (i < m.cap) m.out[i] = ring[ring_slot(i)];
     const int len = mq_flush(m);
     if (len > m.cap) atomicOr(a.err, 1);
     R[nseg - 1] = len;

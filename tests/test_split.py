@@ -392,12 +392,13 @@ def test_split_write_parts_to_one_file(encoder, tmp_path):
 
 
 @pytest.mark.gpu
-def test_split_c5_full_size(encoder):
+def test_split_c5_full_size(encoder, golden):
     """C5 at its configured size: 40000x30000 Gray16, lossy 3 bpp, 7 levels,
-    512^2 tiles (1.2 GP, 4 661 tiles, 350 701 code-blocks).  The tile-split
-    encode at world 1 and world 2 (ranks as threads on cuda:0) equals the
-    single-GPU encode, stays within rate, and decodes (opj_decompress on
-    three 1024^2 windows) at the expected PSNR."""
+    512^2 tiles (1.2 GP, 4 661 tiles, 350 701 code-blocks).  The single-GPU
+    file is the oracle's (SHA-256 committed by make_golden.py); the
+    tile-split encode at world 1 and world 2 (ranks as threads on cuda:0)
+    equals it, stays within rate, and decodes (opj_decompress on three
+    1024^2 windows) at the expected PSNR."""
     from concurrent.futures import ThreadPoolExecutor
     from devmem import DeviceBytes
     w, h, rps = 40000, 30000, 64
@@ -418,6 +419,10 @@ def test_split_c5_full_size(encoder):
     try:
         single, st = encoder.encode_device(d.ptr, d.nbytes, lay, jp2hip.LOSSY, rc)
         assert st.codeblocks == 350701
+        # the oracle's file for the same pixels (tests/golden/make_golden.py c5_full)
+        import hashlib
+        assert len(single) == golden["c5_full"]["oracle_bytes"]
+        assert hashlib.sha256(single).hexdigest() == golden["c5_full"]["oracle_sha256"]
         cs = im.codestream(single)
         assert len(cs) <= 3.0 * w * h / 8
         assert len(im.tile_parts(cs)) == 4661 * 8
