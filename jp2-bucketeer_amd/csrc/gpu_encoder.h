@@ -32,6 +32,7 @@ struct UnpackArgs {
     uint8_t *dst;
     const int *only;  // k_unlzw: decode only strips with only[s] != 0 (nullptr: all)
     int *err;
+    uint32_t *lnk;    // k_inflate: a link per output byte, strip s at lnk + s * stride
 };
 __host__ __device__ inline uint64_t strip_out_bytes(const UnpackArgs &a, int s) {
     if (a.unit_bytes) return a.unit_bytes;
@@ -213,7 +214,7 @@ class GpuEncoder {
     hipEvent_t ev[kNumEvents] = {};
     DevBuf coef, blocks, order, bp, sm, P, dref, dsig, t1out, rates, dists, npasses, lengths, weight,
         nhull, hpass, hkey, budget, nl, lrate, dstoff, packed, err, tcw, tch, strips, src, segcnt, segoff,
-        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, segkey, llbuf0, llbuf1, ordkey, segval, thr, items,
+        est, hist, kcut, pmin, mqspan, stage, soff, lzwseg, untiled, inflnk, segkey, llbuf0, llbuf1, ordkey, segval, thr, items,
         slotoff, stream_buf, counts, dspp, dbgbuf, t1fill, dbgsel;
     // PCRD selection (k_hull / k_select): slope-bin histogram, ticket + list
     // fills, candidate lists

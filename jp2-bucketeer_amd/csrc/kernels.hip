@@ -228,19 +228,27 @@ __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
 }
 
 // Deflate (RFC 1951) in a zlib wrapper (RFC 1950): TIFF compression 8
-// (Adobe Deflate) and 32946 (the older Deflate code), one wave per strip.
-// A Huffman stream has no positions known before decoding it, so a strip is
-// one serial chain; the wave runs it with wave-uniform control flow (every
-// lane executes the same decode, the state in scalar registers) and uses its
-// lanes where the work is parallel:
-//   - the compressed bytes reach an LDS ring 1 KiB per vector load (16 bytes
-//     a lane), one chunk loaded ahead, so the bit reader never waits on HBM;
-//   - the code tables (counts, symbols in code order, 2^FB-entry direct
-//     lookup) are built by the lanes: ranks within a code length by ballot,
-//     lookup entries filled a symbol per lane;
-//   - a match is copied by the lanes at once (one byte each; an overlapping
-//     match, dist < 64, as its period-dist pattern);
-//   - the 32 KiB window leaves for HBM 4 KiB at a time in 16-byte stores.
+// (Adobe Deflate) and 32946 (the older Deflate code), in two phases.
+//
+// k_inflate, one wave per strip: a Huffman stream has no positions known
+// before decoding it, so the symbol decode is one serial chain per strip.
+// The wave runs it with wave-uniform control flow (the state in scalar
+// registers) and keeps that chain short: it does not build the output.  Each
+// output byte p gets a 32-bit link instead -- kLinkByte | value for a
+// literal (or a stored-block byte), or the position of an earlier byte with
+// the same value for a match byte (an overlapping match, dist < length,
+// points before the match start: byte p0 + x -> p0 - dist + x mod dist) --
+// written by the lanes with plain stores (no window, no read-back, no
+// barrier).  Length and distance bases come from closed forms (scalar
+// arithmetic), so a literal costs one table lookup and a match two.  The
+// lanes are used where the work is parallel: the compressed bytes reach an LDS
+// ring 1 KiB per vector load, one chunk ahead; the code tables are built by
+// the lanes (ranks within a code length by ballot); a match's links and a
+// stored block's bytes are written a lane per byte.
+// k_inflate_links then resolves the links of every strip in parallel:
+// pointer doubling (link[p] = link[link[p]], in place -- a link read while
+// another thread rewrites it is still a valid link of the same value), then
+// each byte follows what is left of its chain and is written out.
 // kInfLanes is the wave width (the host build of tests/test_inflate_host.py
 // runs the same text with one lane).
 #ifndef JP2HIP_INF_LANES
@@ -249,16 +257,22 @@ __global__ void __launch_bounds__(64) k_unpackbits(UnpackArgs a) {
 constexpr int kInfLanes = JP2HIP_INF_LANES;
 constexpr uint32_t kInChunkWords = 4 * kInfLanes;       // words per ring refill (16 bytes a lane)
 constexpr uint32_t kInRingWords = 2 * (kInChunkWords > 16 ? kInChunkWords : 16);  // >= two chunks
-constexpr uint32_t kInfWin = 32768, kInfWM = kInfWin - 1;
 constexpr int kInfLB = 12, kInfDB = 9;                  // direct-lookup bits: literal/length, distance
+constexpr uint32_t kLinkByte = 0x80000000u;             // link of a byte whose value is known
+constexpr int kLinkDoublings = 5;                       // pointer-doubling rounds before the chase
 
-__constant__ uint16_t kInfLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                         31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kInfLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kInfDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
-                                          193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t kInfDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kInfClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// RFC 1951 3.2.5 in closed form: length code i = sym - 257 (0..28) and
+// distance code d (0..29) -> (base, extra bits)
+__device__ __forceinline__ uint32_t inf_len_extra(uint32_t i) { return i < 8u || i == 28u ? 0u : (i - 4u) >> 2; }
+__device__ __forceinline__ uint32_t inf_len_base(uint32_t i) {
+    return i == 28u ? 258u : (i < 8u ? 3u + i : ((4u + (i & 3u)) << inf_len_extra(i)) + 3u);
+}
+__device__ __forceinline__ uint32_t inf_dist_extra(uint32_t d) { return d < 4u ? 0u : (d >> 1) - 1u; }
+__device__ __forceinline__ uint32_t inf_dist_base(uint32_t d) {
+    return d < 4u ? d + 1u : ((2u + (d & 1u)) << inf_dist_extra(d)) + 1u;
+}
 
 __device__ __forceinline__ uint32_t inf_uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t inf_uni64(uint64_t v) {
@@ -267,12 +281,9 @@ __device__ __forceinline__ uint64_t inf_uni64(uint64_t v) {
 
 struct InfShared {
     uint32_t ring[kInRingWords];          // compressed stream words
-    uint8_t win[kInfWin];                 // sliding window = output staging
     uint16_t lfast[1 << kInfLB], dfast[1 << kInfDB];
     uint16_t lcnt[16], dcnt[16], lsym[288], dsym[32];
     uint8_t lens[320];
-    uint16_t lbase[29], dbase[30];
-    uint8_t lextra[29], dextra[30];
     uint32_t scr[64];                     // table-build scratch
 };
 
@@ -308,8 +319,8 @@ struct InfIn {
         pre = chunk(c + 1);
     }
     // at least 8 words (256 bits) ahead of k in the ring: called once per
-    // symbol / code length / stored byte (each reads < 64 bits), so refill()
-    // itself never tops up (one top-up site, not one per bit-reader call)
+    // symbol / code length (each reads < 64 bits), so refill() itself never
+    // tops up (one top-up site, not one per bit-reader call)
     __device__ __forceinline__ void ensure() {
         if (k + 8 >= loaded) {
             do top_up(); while (k + 8 >= loaded);  // (once per 1 KiB on the GPU)
@@ -454,54 +465,42 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
     __shared__ __attribute__((aligned(16))) InfShared S;
     const int s = blockIdx.x, lane = (int)threadIdx.x;
     if (s >= a.nstrips) return;
-    for (int i = lane; i < 30; i += kInfLanes) {  // per-match lookups from LDS, not the constant bank
-        if (i < 29) { S.lbase[i] = kInfLenBase[i]; S.lextra[i] = kInfLenExtra[i]; }
-        S.dbase[i] = kInfDistBase[i];
-        S.dextra[i] = kInfDistExtra[i];
-    }
     // the strip's geometry as wave-uniform (scalar) values: everything the
     // decode derives from them stays scalar, and its branches too
-    const uint8_t *in = a.src + inf_uni64(a.off[s]);
-    const uint64_t n = inf_uni64(a.cnt[s]);
+    const uint8_t *in0 = a.src + inf_uni64(a.off[s]);
+    const uint64_t n0 = inf_uni64(a.cnt[s]);
     const uint64_t cap64 = inf_uni64(strip_out_bytes(a, s));
-    uint8_t *out = a.dst + (uint64_t)s * a.stride;
-    if (cap64 >= (1ull << 32)) {  // a strip / tile of 4 GiB or more: not a TIFF the host parser accepts
+    uint32_t *L = a.lnk + (uint64_t)s * a.stride;  // this strip's links
+    if (cap64 >= (1ull << 31)) {  // a strip / tile of 2 GiB or more: not a TIFF the host parser accepts
         if (lane == 0) atomicOr(a.err, 2);
         return;
     }
     const uint32_t cap = (uint32_t)cap64;
-    uint32_t pos = 0, flushed = 0;
-    // window bytes [flushed, upto) to HBM: 16-byte stores from the lanes
-    // (upto a multiple of 16 except at the end of the strip)
-    auto flush = [&](uint32_t upto) {
-        const uint32_t whole = flushed + ((upto - flushed) & ~15u);
-        for (uint32_t o = flushed + 16u * (uint32_t)lane; o < whole; o += 16u * kInfLanes)
-            *(uint4 *)(out + o) = *(const uint4 *)&S.win[o & kInfWM];
-        for (uint32_t o = whole + (uint32_t)lane; o < upto; o += kInfLanes) out[o] = S.win[o & kInfWM];
-        flushed = upto;
-    };
-    const uint32_t h0 = inf_uni(n >= 1 ? in[0] : 0u), h1 = inf_uni(n >= 2 ? in[1] : 0u);
-    bool bad = n < 2 || (h0 & 15) != 8 || (h0 >> 4) > 7 || ((h0 << 8) | h1) % 31 || (h1 & 0x20);
+    uint32_t pos = 0;
+    const uint32_t h0 = inf_uni(n0 >= 1 ? in0[0] : 0u), h1 = inf_uni(n0 >= 2 ? in0[1] : 0u);
+    bool bad = n0 < 2 || (h0 & 15) != 8 || (h0 >> 4) > 7 || ((h0 << 8) | h1) % 31 || (h1 & 0x20);
+    // the reader restarts after a stored block: base = stream bytes before it
+    uint64_t base = 0;
     InfIn b;
-    b.init(in, n, S.ring, lane);
+    b.init(in0, n0, S.ring, lane);
     b.get(16);  // zlib CMF, FLG (checked above)
     bool last = false;
     while (!bad && !last) {
         b.ensure();
         last = b.get(1);
         const int type = (int)b.get(2);
-        if (type == 0) {  // stored: to the byte boundary, LEN, ~LEN, bytes
+        if (type == 0) {  // stored: to the byte boundary, LEN, ~LEN, then LEN bytes copied by the lanes
             b.align();
             uint32_t len = b.get(16);
             const uint32_t nlen = b.get(16);
             if (len != (~nlen & 0xFFFFu)) { bad = true; break; }
+            const uint64_t at = base + b.consumed() / 8;  // the block's first byte in the stream
+            if (at + len > n0) { bad = true; break; }     // truncated
             if (len > cap - pos) { len = cap - pos; last = true; }  // strip full: stop here
-            for (uint32_t i = 0; i < len; i++) {
-                b.ensure();
-                const uint32_t v = b.get(8);
-                if (lane == 0) S.win[pos & kInfWM] = (uint8_t)v;
-                if (++pos - flushed >= 4096) flush(flushed + 4096);
-            }
+            for (uint32_t i = (uint32_t)lane; i < len; i += kInfLanes) L[pos + i] = kLinkByte | in0[at + i];
+            pos += len;
+            base = at + len;  // (a partial block when the strip is full: nothing follows it)
+            b.init(in0 + base, n0 - base, S.ring, lane);
             continue;
         }
         if (type == 1) {  // fixed codes
@@ -556,49 +555,63 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
             if (sy < 256) {
                 if (sy < 0) { bad = true; break; }
                 if (pos >= cap) { last = true; break; }  // strip full: trailing data ignored
-                if (lane == 0) S.win[pos & kInfWM] = (uint8_t)sy;
-                if (++pos - flushed >= 4096) flush(flushed + 4096);
+                if (lane == 0) L[pos] = kLinkByte | (uint32_t)sy;
+                pos++;
                 continue;
             }
             if (sy == 256) break;
-            sy -= 257;
-            if (sy >= 29) { bad = true; break; }
-            uint32_t len = inf_uni(S.lbase[sy]) + b.get((int)inf_uni(S.lextra[sy]));
+            const uint32_t li = (uint32_t)sy - 257u;
+            if (li >= 29u) { bad = true; break; }
+            uint32_t len = inf_len_base(li) + b.get((int)inf_len_extra(li));
             const int d = inf_decode<kInfDB>(b, S.dfast, S.dcnt, S.dsym);
             if (d < 0 || d >= 30) { bad = true; break; }
-            const uint32_t dist = inf_uni(S.dbase[d]) + b.get((int)inf_uni(S.dextra[d]));
+            const uint32_t dist = inf_dist_base((uint32_t)d) + b.get((int)inf_dist_extra((uint32_t)d));
             if (dist > pos) { bad = true; break; }
             bool full = false;
             if (len > cap - pos) {  // the strip ends inside this match: keep what fits
                 len = cap - pos;
                 full = true;
             }
-            const uint32_t p0 = pos;
-            if (dist >= (uint32_t)kInfLanes) {
-                // rounds of kInfLanes bytes: a round reads only bytes before it
-                for (uint32_t o = 0; o < len; o += kInfLanes)
-                    if (o + (uint32_t)lane < len) {
-                        const uint32_t x = p0 + o + (uint32_t)lane;
-                        S.win[x & kInfWM] = S.win[(x - dist) & kInfWM];
-                    }
+            // each byte links to one before the match start (period dist when
+            // the match overlaps itself)
+            const uint32_t src = pos - dist;
+            if (dist >= len) {
+                for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x;
             } else {
-                // overlapping: byte pos + x repeats byte pos - dist + (x mod dist),
-                // all of them already final
-                for (uint32_t o = 0; o < len; o += kInfLanes)
-                    if (o + (uint32_t)lane < len) {
-                        const uint32_t x = o + (uint32_t)lane;
-                        S.win[(p0 + x) & kInfWM] = S.win[(p0 - dist + x % dist) & kInfWM];
-                    }
+                for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x % dist;
             }
-            __builtin_amdgcn_wave_barrier();
             pos += len;
-            if (pos - flushed >= 4096) flush(flushed + 4096);
             if (full) { last = true; break; }
         }
     }
-    bad = bad || b.consumed() > 8 * n;  // read past the end of the stream: truncated
-    if (!bad) flush(pos);
+    bad = bad || base * 8 + b.consumed() > 8 * n0;  // read past the end of the stream: truncated
     if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
+}
+
+// Resolves every decoded strip's links (k_inflate) into its bytes: grid
+// (chunks of kLinkChunk bytes, strips).  Rounds of pointer doubling first,
+// one launch each (round < kLinkDoublings), then the last launch chases what
+// is left of each chain and writes the bytes.  Links only point backwards
+// within their strip, so every chain ends at a byte of known value.
+constexpr int kLinkChunk = 4096;
+__global__ void __launch_bounds__(256) k_inflate_links(UnpackArgs a, int chase) {
+    const int s = blockIdx.y;
+    const uint32_t cap = (uint32_t)strip_out_bytes(a, s);
+    uint32_t *L = a.lnk + (uint64_t)s * a.stride;
+    uint8_t *out = a.dst + (uint64_t)s * a.stride;
+    const uint32_t p0 = blockIdx.x * (uint32_t)kLinkChunk;
+    for (uint32_t p = p0 + threadIdx.x; p < min(cap, p0 + (uint32_t)kLinkChunk); p += 256) {
+        uint32_t v = L[p];
+        if (!chase) {
+            if (!(v & kLinkByte)) {
+                const uint32_t u = L[v];
+                if (u != v) L[p] = u;
+            }
+            continue;
+        }
+        while (!(v & kLinkByte)) v = L[v];
+        out[p] = (uint8_t)v;
+    }
 }
 
 // Predictor 2: each sample adds the same component of the pixel to its left
@@ -1779,6 +1792,7 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
         ua.unit_bytes = tiled ? (uint64_t)unit_h * row_bytes : 0;
         ua.dst = (uint8_t *)stage.ptr;
         ua.only = nullptr;
+        ua.lnk = nullptr;
         ua.err = (int *)this->err.ptr;
         if (lay.compression == 5) {  // segment-parallel (lzw.hip)
             std::vector<uint64_t> slice;
@@ -1791,8 +1805,16 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
                 return false;
             }
         }
-        else if (lay.compression == 8 || lay.compression == 32946)
+        else if (lay.compression == 8 || lay.compression == 32946) {
+            // decode to links (a strip per wave), then resolve the links
+            // (every strip's bytes in parallel; k_inflate_links)
+            if (!ensure<uint32_t>(inflnk, stride * ns, err)) return false;
+            ua.lnk = (uint32_t *)inflnk.ptr;
             hipLaunchKernelGGL(k_inflate, dim3(ns), dim3(kInfLanes), 0, stream, ua);
+            const dim3 g((unsigned)((unit_h * row_bytes + kLinkChunk - 1) / kLinkChunk), (unsigned)ns);
+            for (int r = 0; r <= kLinkDoublings; r++)
+                hipLaunchKernelGGL(k_inflate_links, g, dim3(256), 0, stream, ua, r == kLinkDoublings ? 1 : 0);
+        }
         else hipLaunchKernelGGL(k_unpackbits, dim3(ns), dim3(64), 0, stream, ua);
         HIPCHECK(hipGetLastError());
         if (lay.predictor == 2) {  // per decoded row of a strip / of a tile

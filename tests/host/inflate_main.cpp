@@ -21,7 +21,7 @@
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 struct uint4 { uint32_t x, y, z, w; };
 static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
-static struct { int x; } blockIdx, threadIdx;
+static struct { int x, y; } blockIdx, threadIdx;
 static inline int atomicOr(int *p, int v) { int o = *p; *p |= v; return o; }
 static inline uint32_t atomicAdd(uint32_t *p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
 using std::min;
@@ -32,14 +32,25 @@ static int run(const std::vector<uint8_t> &z, int off, const std::vector<uint8_t
     std::vector<uint8_t> buf(z.size() + 16, 0xA5);
     std::memcpy(buf.data() + off, z.data(), z.size());
     std::vector<uint8_t> out(raw.size() + 256);
+    std::vector<uint32_t> lnk(raw.size() + 256, 0xDEADBEEFu);
     uint64_t o = off, c = z.size();
     int err = 0;
     UnpackArgs a{};
     a.src = buf.data(); a.off = &o; a.cnt = &c; a.nstrips = 1;
     a.unit_bytes = raw.size(); a.stride = raw.size() + 256; a.dst = out.data(); a.err = &err;
-    blockIdx.x = 0; threadIdx.x = 0;
+    a.lnk = lnk.data();
+    blockIdx.x = 0; blockIdx.y = 0; threadIdx.x = 0;
     k_inflate(a);
     if (err) return 1;
+    // k_inflate_links as the GPU runs it: doubling rounds, then the chase
+    const int chunks = (int)((raw.size() + kLinkChunk - 1) / kLinkChunk);
+    for (int r = 0; r <= kLinkDoublings; r++)
+        for (int bx = 0; bx < chunks; bx++)
+            for (int t = 0; t < 256; t++) {
+                blockIdx.x = bx; threadIdx.x = t;
+                k_inflate_links(a, r == kLinkDoublings ? 1 : 0);
+            }
+    blockIdx.x = 0; threadIdx.x = 0;
     return std::memcmp(out.data(), raw.data(), raw.size()) ? 2 : 0;
 }
 
@@ -74,6 +85,24 @@ int main() {
     const int rb = run(z, 0, raw);
     printf("reserved block -> %d\n", rb);
     fails += rb != 1;
+    // long runs: chains of matches of matches (the links' doubling + chase),
+    // and the strip ending inside a match / inside a stored block (a decoded
+    // stream longer than the strip is cut, as libtiff does)
+    std::vector<uint8_t> flat(700000, 0);
+    for (size_t i = 0; i < flat.size(); i++) flat[i] = (uint8_t)(i < 1000 ? i * 7 : (i < 400000 ? 3 : (i / 5000) & 1));
+    for (int lvl : {0, 1, 9}) {
+        uLongf fl = compressBound(flat.size());
+        std::vector<uint8_t> zf(fl);
+        compress2(zf.data(), &fl, flat.data(), flat.size(), lvl);
+        zf.resize(fl);
+        const int rf = run(zf, 2, flat);
+        printf("flat level %d -> %d\n", lvl, rf);
+        fails += rf != 0;
+        std::vector<uint8_t> cut(flat.begin(), flat.begin() + 654321);
+        const int rc = run(zf, 3, cut);
+        printf("flat level %d, strip shorter than the stream -> %d\n", lvl, rc);
+        fails += rc != 0;
+    }
     printf("%s\n", fails ? "FAIL" : "OK");
     return fails ? 1 : 0;
 }

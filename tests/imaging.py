@@ -481,3 +481,98 @@ def tiled_tiff_bytes(img: np.ndarray, tile=(32, 48), planar=False, big_endian=Fa
     extra = struct.pack(e + "H" * max(nc, 2), *([bits] * max(nc, 2)))
     extra += struct.pack(e + "I" * nt, *offs) + struct.pack(e + "I" * nt, *[len(t) for t in tiles])
     return hdr + ifd + extra + b"".join(tiles)
+
+
+# ---- a fixed-Huffman Deflate writer for crafted token streams (RFC 1951 3.2.6) ----
+_LEN_BASE = [3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131,
+             163, 195, 227, 258]
+_LEN_EXTRA = [0] * 8 + [1] * 4 + [2] * 4 + [3] * 4 + [4] * 4 + [5] * 4 + [0]
+_DIST_BASE = [1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049,
+              3073, 4097, 6145, 8193, 12289, 16385, 24577]
+_DIST_EXTRA = [0, 0, 0, 0] + [k for k in range(1, 14) for _ in (0, 1)]
+
+
+class _Bits:
+    def __init__(self):
+        self.buf, self.acc, self.n = bytearray(), 0, 0
+
+    def put(self, v, n):  # LSB first
+        self.acc |= v << self.n
+        self.n += n
+        while self.n >= 8:
+            self.buf.append(self.acc & 0xFF)
+            self.acc >>= 8
+            self.n -= 8
+
+    def put_code(self, code, n):  # Huffman codes go MSB first
+        self.put(int(format(code, f"0{n}b")[::-1], 2), n)
+
+    def done(self):
+        if self.n:
+            self.buf.append(self.acc & 0xFF)
+        return bytes(self.buf)
+
+
+def _fixed_litlen(bw, v):
+    if v < 144:
+        bw.put_code(0x30 + v, 8)
+    elif v < 256:
+        bw.put_code(0x190 + v - 144, 9)
+    elif v < 280:
+        bw.put_code(v - 256, 7)
+    else:
+        bw.put_code(0xC0 + v - 280, 8)
+
+
+def deflate_tokens(tokens) -> tuple[bytes, bytes]:
+    """zlib stream of one fixed-Huffman block coding `tokens` -- ints (a
+    literal byte) or (length, distance) matches -- exactly as given, and the
+    bytes it decodes to.  Lets a test pick every match distance and length
+    (zlib picks its own)."""
+    import zlib
+    out = bytearray()
+    bw = _Bits()
+    bw.put(1, 1)  # BFINAL
+    bw.put(1, 2)  # BTYPE 01: fixed codes
+    for t in tokens:
+        if isinstance(t, int):
+            _fixed_litlen(bw, t)
+            out.append(t)
+            continue
+        length, dist = t
+        assert 3 <= length <= 258 and 1 <= dist <= min(32768, len(out))
+        i = max(k for k in range(29) if _LEN_BASE[k] <= length) if length < 258 else 28
+        _fixed_litlen(bw, 257 + i)
+        if _LEN_EXTRA[i]:
+            bw.put(length - _LEN_BASE[i], _LEN_EXTRA[i])
+        j = max(k for k in range(30) if _DIST_BASE[k] <= dist)
+        bw.put_code(j, 5)
+        if _DIST_EXTRA[j]:
+            bw.put(dist - _DIST_BASE[j], _DIST_EXTRA[j])
+        for _ in range(length):
+            out.append(out[-dist])
+    _fixed_litlen(bw, 256)  # end of block
+    body = bw.done()
+    stream = b"\x78\x01" + body + struct.pack(">I", zlib.adler32(bytes(out)))
+    return stream, bytes(out)
+
+
+def crafted_match_tokens(seed=7):
+    """Every match distance 1..70 with lengths 3..258 (overlapping copies,
+    dist < length), then long distances up to 32768, between random
+    literals: the decoded data runs over many 4096-byte window flushes."""
+    rng = np.random.default_rng(seed)
+    toks, n = [], 0
+    for _ in range(300):
+        toks.append(int(rng.integers(0, 256)))
+        n += 1
+    lens = (3, 4, 5, 7, 10, 31, 63, 64, 65, 100, 127, 128, 129, 200, 257, 258)
+    for d in list(range(1, 71)) + [100, 255, 256, 1000, 4095, 4096, 4097, 20000, 32767, 32768]:
+        for L in lens:
+            for _ in range(int(rng.integers(0, 3))):
+                toks.append(int(rng.integers(0, 256)))
+                n += 1
+            if d <= n:
+                toks.append((L, d))
+                n += L
+    return toks

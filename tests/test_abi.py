@@ -287,3 +287,15 @@ def test_env_check_names_the_slow_settings(monkeypatch):
     assert "HSA_ENABLE_SDMA" in jp2hip._lib.env_check()
     monkeypatch.setenv("HSA_ENABLE_SDMA", "1")
     assert jp2hip._lib.env_check() == ""
+
+
+def test_crafted_deflate_writer_matches_zlib():
+    """The fixed-Huffman token writer behind the GPU inflate test decodes,
+    under zlib, to exactly the bytes it says (every distance 1..70, lengths
+    3..258, distances up to 32768)."""
+    import zlib
+    toks = im.crafted_match_tokens(7)
+    assert {t[1] for t in toks if isinstance(t, tuple)} >= set(range(1, 71)) | {32768}
+    assert {t[0] for t in toks if isinstance(t, tuple)} >= {3, 4, 5, 257, 258}
+    stream, raw = im.deflate_tokens(toks)
+    assert zlib.decompress(stream) == raw and len(raw) > 100_000

@@ -286,6 +286,30 @@ def test_corrupt_deflate_strip_fails_loudly(encoder, damage):
         encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
 
 
+def test_inflate_every_match_distance_and_length(encoder):
+    """the lane-strided match copies (dist >= 64 rounds and the
+    overlapping dist < 64 pattern) and the window flushes, on crafted
+    streams -- two strips, each one fixed-Huffman block coding every match
+    distance 1..70 at lengths 3..258 plus long distances up to 32768
+    (imaging.crafted_match_tokens) -- against the same pixels uncompressed
+    (the writer itself is pinned to zlib.decompress in test_abi)."""
+    w = 311
+    toks = [im.crafted_match_tokens(seed) for seed in (7, 8)]
+    rows = max(-(-len(im.deflate_tokens(t)[1]) // w) for t in toks)
+    strips, raws = [], []
+    for t in toks:
+        n = len(im.deflate_tokens(t)[1])
+        st, raw = im.deflate_tokens(t + [(11 * k) & 0xFF for k in range(rows * w - n)])
+        strips.append(st)
+        raws.append(raw)
+    img = np.frombuffer(b"".join(raws), np.uint8).reshape(2 * rows, w).copy()
+    it = iter(strips)
+    data = im.tiff_bytes(img, rows_per_strip=rows, strip_codec=lambda raw: next(it), compression=8)
+    got, _ = encoder.encode_tiff(data, jp2hip.LOSSLESS)
+    want, _ = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSLESS)
+    assert got == want
+
+
 @pytest.mark.parametrize("comp", ["tiff_lzw", "tiff_adobe_deflate", "packbits"])
 def test_compressed_strip_longer_than_needed_is_cut(encoder, comp):
     """A last strip that decodes to more rows than ImageLength leaves is cut

@@ -360,6 +360,48 @@ def test_split_compressed_and_tiled_masters(encoder, idx):
 
 
 @pytest.mark.gpu
+def test_split_truncated_band_fails_on_every_rank(encoder):
+    """one rank's band-only upload of a compressed master is cut
+    short (its last strip's bytes past the buffer): that rank fails on its
+    own, and every other rank fails too (the failure flag of the exchanges)
+    instead of writing a part of a file that cannot be whole."""
+    from devmem import DeviceBytes
+    img = im.synth_rgb8(1300, 700, seed=23)
+    tif = im.tiff_bytes(img, rows_per_strip=48, strip_codec=im.lzw_encode, compression=5)
+    rc = jp2hip.recipe(jp2hip.LOSSY, tile_w=256, tile_h=256)
+    lay, offs = jp2hip.tiff_layout(tif)
+    world = 3
+    g = js.ThreadGroup(world)
+    errs = [None] * world
+
+    def work(r):
+        enc = jp2hip.Encoder(0)
+        try:
+            r0, r1 = js.split_rows(lay.height, rc.tile_h, r, world, rc.flush_period)
+            buf, blay, keep = js.band_strips(tif, lay, offs, r0, r1)
+            if r == 1:
+                buf = buf[:len(buf) - 100]  # the band's last strip runs past the upload
+            d = DeviceBytes(buf or b"\0")
+            try:
+                enc.encode_device_split(d.ptr, d.nbytes, blay, jp2hip.LOSSY, g.member(r).split(), rc)
+            finally:
+                d.free()
+        except Exception as e:
+            errs[r] = e
+        finally:
+            enc.close()
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert all(isinstance(e, jp2hip.Jp2hipError) for e in errs), errs
+    assert "outside the source buffer" in str(errs[1])
+    assert all("another rank failed" in str(errs[r]) for r in (0, 2)), errs
+
+
+@pytest.mark.gpu
 def test_split_c5_shape_on_rate_and_identical(encoder):
     """C5's recipe (Gray16, 7 levels, 6 layers, lossy 3 bpp, 512^2 tiles) on a
     6000x4000 crop: 4 ranks == single GPU, within rate, decodes at a sane PSNR.

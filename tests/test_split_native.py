@@ -72,6 +72,16 @@ def test_more_ranks_than_tile_rows(tmp_path):
     assert np.array_equal(im.decode_pillow(b), img)
 
 
+def test_empty_ranks_with_a_compressed_master(tmp_path):
+    """world 4 on an LZW master of two tile rows -- two ranks
+    decode nothing and still join every exchange; the ragged last strip
+    (900 = 18 x 48 + 36 rows) ends the last band."""
+    img = im.synth_rgb8(900, 500, seed=17)
+    tif = im.tiff_bytes(img, rows_per_strip=48, strip_codec=im.lzw_encode, compression=5)
+    a, b, _ = _file_pair(tmp_path, tif, jp2hip.LOSSY, jp2hip.recipe(jp2hip.LOSSY, flush_period=0), [0, 0, 0])
+    assert a == b
+
+
 def test_one_rank_fails_every_rank_fails_no_file(tmp_path):
     """A corrupt strip in the last rank's band: the call fails with that
     rank's error, the others stop at their next exchange, no file is left."""
