@@ -879,7 +879,7 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
 
 
 def lossless_c4(device):
-    rows = 320
+    rows = 640  # >= 2 s of batch at ~10 GP/s
     value, dt, res = c4_batch(device, rows=rows)
     ok = [r for r in res if r["status"] == 0]
     bpp = 8 * float(np.mean([r["out_bytes"] for r in ok])) / (5000 * 7000) if ok else 0.0
@@ -893,7 +893,7 @@ def lossless_c4(device):
                               "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}}
 
 
-def c2_file_span(device, images=512, contexts=16):
+def c2_file_span(device, images=1024, contexts=16):
     """SURVEY.md 8(d)'s span for the headline workload: C2 (lossy 3 bpp) from
     TIFF files on disk to JPX files written, through the native per-GPU queue
     (reader threads: file -> pinned buffer + header parse; `contexts` encodes

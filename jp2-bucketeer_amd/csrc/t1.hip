@@ -555,13 +555,15 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
     }
 }
 
-// The coder's byte ring: 64 bytes per lane.  Interleaved layout (default):
-// dword k of lane L's ring is LDS dword k * 64 + L, so the byte a lane stores
-// on every step lands in bank L whatever its position -- no bank conflicts
-// (the packed 68-byte-stride layout put the 64 lanes' data-dependent slots on
-// random banks: ~1 conflict cycle per LDS instruction).
+// The coder's byte ring: 64 bytes per lane at a 68-byte stride (default), or
+// interleaved (JP2HIP_MQ_RING_IL=1): dword k of lane L's ring at LDS dword
+// k * 64 + L, so the byte a lane stores on every step lands in bank L
+// whatever its position -- no bank conflicts.  Measured (gpurun_out/r4a/
+// ab_ring): the interleaved ring's extra address arithmetic costs more than
+// the conflicts it removes (k_t1_mq alone 2894 -> 2905 us, C2 bench 24.9 ->
+// 24.3 GP/s), so the packed layout stays.
 #ifndef JP2HIP_MQ_RING_IL
-#define JP2HIP_MQ_RING_IL 1
+#define JP2HIP_MQ_RING_IL 0
 #endif
 #if JP2HIP_MQ_RING_IL
 constexpr int kRingLaneStride = 4;
@@ -900,6 +902,11 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
 __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
     __shared__ MqShared sh;
     const int tid = threadIdx.x, lane = tid & 63;
+#ifdef JP2HIP_MQ_PRIO
+    // issue priority over the other kernels' waves on the SIMD: the MQ
+    // chains are latency-bound and hold their LDS until they end
+    __builtin_amdgcn_s_setprio(JP2HIP_MQ_PRIO);
+#endif
     const uint64_t w0 = wall_clock64();
     if (tid == 0) atomicMax(&a.span[0], ~(unsigned long long)w0);
     for (int e = tid; e < 94; e += 128) {
