@@ -287,24 +287,23 @@ struct InfShared {
     uint32_t scr[64];                     // table-build scratch
 };
 
-// LSB-first bit reader over the strip's 16-byte-aligned words, fed from the
-// LDS ring.  Words past the stream read as zero (never loaded): decoding runs
-// on to the end of the strip's output or of the block, and a stream that was
-// read past its end (consumed() > 8 n) is reported corrupt at the end -- no
-// per-read bookkeeping on the hot path.
+// Bit reader over the strip's 16-byte-aligned words, fed from the LDS ring,
+// addressed by absolute bit position P (bit 0 = bit 0 of the aligned base
+// word; the stream starts at head_bits).  Words past the stream read as zero
+// (never loaded): decoding runs on to the end of the strip's output or of the
+// block, and a stream read past its end (P > end_bits) is reported corrupt at
+// the end -- no per-read bookkeeping on the hot path.
 struct InfIn {
     const uint32_t *w;                 // aligned base of the stream
     uint32_t nw;                       // words holding stream bytes
-    uint32_t k;                        // next word into buf
-    uint32_t loaded;                   // words written to the ring
-    uint32_t head_bits;                // bits before the stream in word 0
+    uint64_t loaded;                   // words written to the ring
+    uint64_t P;                        // next bit to read
+    uint64_t head_bits, end_bits;      // where the stream starts / ends (bits)
     uint4 pre;                         // this lane's 16 bytes of the chunk after them
-    uint64_t buf;
-    int cnt;
     uint32_t *ring;
     int lane;
-    __device__ __forceinline__ uint4 chunk(uint32_t c) const {  // this lane's part of chunk c
-        const uint32_t w0 = c * kInChunkWords + 4u * (uint32_t)lane;
+    __device__ __forceinline__ uint4 chunk(uint64_t c) const {  // this lane's part of chunk c
+        const uint64_t w0 = c * kInChunkWords + 4u * (uint32_t)lane;
         if (w0 + 4 <= nw) return *(const uint4 *)(w + w0);
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
         if (w0 + 0 < nw) v.x = w[w0 + 0];
@@ -313,23 +312,25 @@ struct InfIn {
         return v;
     }
     __device__ __forceinline__ void top_up() {  // the prefetched chunk into the ring, the next one in flight
-        const uint32_t c = loaded / kInChunkWords;
+        const uint64_t c = loaded / kInChunkWords;
         ((uint4 *)ring)[(c * kInfLanes + (uint32_t)lane) % (kInRingWords / 4)] = pre;
         loaded += kInChunkWords;
         pre = chunk(c + 1);
     }
-    // at least 8 words (256 bits) ahead of k in the ring: called once per
-    // symbol / code length (each reads < 64 bits), so refill() itself never
-    // tops up (one top-up site, not one per bit-reader call)
+    // the ring holds at least 8 words (256 bits) from P's word on: called once
+    // per window / symbol / code length (each reads < 64 bits from P)
     __device__ __forceinline__ void ensure() {
+        const uint64_t k = P >> 5;
         if (k + 8 >= loaded) {
+            if (k >= loaded) {  // a jump (past a stored block): restart the ring at P's chunk
+                loaded = (k / kInChunkWords) * kInChunkWords;
+                pre = chunk(loaded / kInChunkWords);
+            }
             do top_up(); while (k + 8 >= loaded);  // (once per 1 KiB on the GPU)
-            // the state is wave-uniform: say so after the lane-dependent
-            // loads, so the decode keeps running on the scalar unit
-            buf = inf_uni64(buf);
-            cnt = (int)inf_uni((uint32_t)cnt);
-            k = inf_uni(k);
-            loaded = inf_uni(loaded);
+            __builtin_amdgcn_wave_barrier();
+            // wave-uniform, after the lane-dependent loads: the decode keeps
+            // running on the scalar unit
+            loaded = inf_uni64(loaded);
         }
     }
     __device__ __forceinline__ void init(const uint8_t *in, uint64_t n, uint32_t *r, int ln) {
@@ -340,56 +341,59 @@ struct InfIn {
         lane = ln;
         loaded = 0;
         pre = chunk(0);
-        k = (uint32_t)(head >> 2);
+        head_bits = 8 * head;
+        end_bits = 8 * (head + n);
+        P = head_bits;
         ensure();
-        const uint32_t w0 = inf_uni(ring[head >> 2]);
-        buf = (uint64_t)w0 >> (8 * (head & 3));
-        cnt = 32 - 8 * (int)(head & 3);
-        k = (uint32_t)(head >> 2) + 1;
-        head_bits = (uint32_t)(8 * head);
     }
-    __device__ __forceinline__ uint64_t consumed() const { return (uint64_t)k * 32 - (uint64_t)cnt - head_bits; }
-    __device__ __forceinline__ void refill() {
-        if (cnt > 32) return;
-        buf |= (uint64_t)inf_uni(ring[k % kInRingWords]) << cnt;
-        cnt += 32;
-        k++;
+    // n <= 32 bits at bit position q (wave-uniform; the ring must hold them)
+    __device__ __forceinline__ uint32_t bits_at(uint64_t q, int n) const {
+        const uint64_t k = q >> 5;
+        const uint32_t lo = inf_uni(ring[k % kInRingWords]), hi = inf_uni(ring[(k + 1) % kInRingWords]);
+        const uint32_t v = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(q & 31));
+        return n >= 32 ? v : v & ((1u << n) - 1u);
     }
-    __device__ __forceinline__ uint32_t peek(int kb) { refill(); return (uint32_t)buf & ((1u << kb) - 1u); }
-    __device__ __forceinline__ void drop(int kb) {
-        buf >>= kb;
-        cnt -= kb;
-    }
-    __device__ __forceinline__ uint32_t get(int kb) {  // kb <= 16
-        const uint32_t v = peek(kb);
-        drop(kb);
+    __device__ __forceinline__ uint32_t get(int n) {  // n <= 32
+        const uint32_t v = bits_at(P, n);
+        P += (uint64_t)n;
         return v;
     }
-    __device__ __forceinline__ void align() { refill(); drop((int)((0u - (uint32_t)consumed()) & 7u)); }  // to the next byte
+    __device__ __forceinline__ uint64_t consumed() const { return P - head_bits; }
+    __device__ __forceinline__ void align() { P = (P + 7) & ~7ull; }  // to the next byte
 };
 
-// Canonical code of a length-walk (codes longer than the direct lookup)
-__device__ int inf_walk(InfIn &b, const uint16_t *cnt, const uint16_t *sym) {
+// Canonical code of a length-walk (codes longer than the direct lookup),
+// from bit position q; returns the symbol and sets *len (0: invalid)
+__device__ int inf_walk_at(const InfIn &b, uint64_t q, const uint16_t *cnt, const uint16_t *sym, int *len) {
     int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; len++) {
-        code |= (int)b.get(1);
-        const int count = (int)inf_uni(cnt[len]);
-        if (code - count < first) return (int)inf_uni(sym[index + (code - first)]);
+    const uint32_t v = b.bits_at(q, 16);
+    for (int l = 1; l <= 15; l++) {
+        code |= (int)((v >> (l - 1)) & 1u);
+        const int count = (int)inf_uni(cnt[l]);
+        if (code - count < first) {
+            *len = l;
+            return (int)inf_uni(sym[index + (code - first)]);
+        }
         index += count;
         first = (first + count) << 1;
         code <<= 1;
     }
+    *len = 0;
     return -1;
 }
 
+// One symbol from P with the 2^FB-entry direct lookup (code-length tables)
 template <int FB>
 __device__ __forceinline__ int inf_decode(InfIn &b, const uint16_t *fast, const uint16_t *cnt, const uint16_t *sym) {
-    const uint32_t e = inf_uni(fast[b.peek(FB)]);
+    const uint32_t e = inf_uni(fast[b.bits_at(b.P, FB)]);
     if (e) {
-        b.drop((int)(e >> 9));
+        b.P += e >> 9;
         return (int)(e & 511u);
     }
-    return inf_walk(b, cnt, sym);
+    int l;
+    const int s = inf_walk_at(b, b.P, cnt, sym, &l);
+    b.P += (uint64_t)l;
+    return s;
 }
 
 // Canonical Huffman table from n code lengths, built by the lanes: 16
@@ -461,6 +465,119 @@ __device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const ui
     return true;
 }
 
+// The symbols of one Huffman block, a window of kInfLanes bit offsets at a
+// time: lane l looks up the codes that would start at bit P + l (the
+// literal/length table and the distance table, one LDS read each for the
+// whole wave), then the walk follows the actual symbol boundaries through
+// those lookups by readlane -- offset o, o + code length, ... -- with no
+// memory access until the walk leaves the window.  A symbol's parts (code,
+// length extra bits, distance code, distance extra bits) may straddle two
+// windows: the walk is a state machine that resumes in the next window.
+// Literals collect in a register (lane i = the i-th of a run) and are
+// stored kInfLanes at a time; a match's links are stored by the lanes.
+// Returns false on a corrupt stream; *last = the strip is full.
+enum { kInfLit, kInfLenX, kInfDist, kInfDistX };
+__device__ bool inf_block(InfIn &b, InfShared &S, uint32_t *L, uint32_t cap, uint32_t &pos, bool &full, int lane) {
+    int state = kInfLit;
+    uint32_t li = 0, len = 0, dc = 0;
+    uint32_t lit = 0, nlit = 0, lit0 = pos;  // pending literal run: lane i holds value i
+    auto flush_lits = [&]() {
+        if ((uint32_t)lane < nlit) L[lit0 + (uint32_t)lane] = kLinkByte | lit;
+        nlit = 0;
+    };
+    for (;;) {
+        b.ensure();
+        // this lane's 32 bits from P + lane, and the two table entries there
+        const uint64_t q = b.P + (uint64_t)lane;
+        const uint32_t kw = (uint32_t)(q >> 5) % kInRingWords;
+        const uint32_t X = __builtin_amdgcn_alignbit(b.ring[(kw + 1) % kInRingWords], b.ring[kw], (uint32_t)(q & 31));
+        const uint32_t Le = S.lfast[X & ((1u << kInfLB) - 1u)], De = S.dfast[X & ((1u << kInfDB) - 1u)];
+        uint32_t o = 0;
+        while (o < (uint32_t)kInfLanes) {
+            if (state == kInfLit) {
+                uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)Le, (int)o), cl = e >> 9, sy = e & 511u;
+                if (!e) {  // a code longer than the direct lookup: walk it bit by bit
+                    int l;
+                    const int ws = inf_walk_at(b, b.P + o, S.lcnt, S.lsym, &l);
+                    if (ws < 0) return false;
+                    cl = (uint32_t)l;
+                    sy = (uint32_t)ws;
+                }
+                o += cl;
+                if (sy < 256u) {
+                    if (pos >= cap) {  // strip full: trailing data ignored
+                        flush_lits();
+                        b.P += o;
+                        full = true;
+                        return true;
+                    }
+                    if (nlit == 0) lit0 = pos;
+                    lit = (uint32_t)lane == nlit ? sy : lit;
+                    nlit++;
+                    pos++;
+                    if (nlit == (uint32_t)kInfLanes) flush_lits();
+                    continue;
+                }
+                flush_lits();
+                if (sy == 256u) {  // end of block
+                    b.P += o;
+                    return true;
+                }
+                li = sy - 257u;
+                if (li >= 29u) return false;
+                state = kInfLenX;
+            } else if (state == kInfLenX) {
+                const uint32_t nx = inf_len_extra(li);
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)o) & ((1u << nx) - 1u);
+                len = inf_len_base(li) + x;
+                o += nx;
+                state = kInfDist;
+            } else if (state == kInfDist) {
+                uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)De, (int)o), cl = e >> 9;
+                dc = e & 511u;
+                if (!e) {
+                    int l;
+                    const int ws = inf_walk_at(b, b.P + o, S.dcnt, S.dsym, &l);
+                    if (ws < 0) return false;
+                    cl = (uint32_t)l;
+                    dc = (uint32_t)ws;
+                }
+                if (dc >= 30u) return false;
+                o += cl;
+                state = kInfDistX;
+            } else {  // kInfDistX: the match
+                const uint32_t nx = inf_dist_extra(dc);
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)o) & ((1u << nx) - 1u);
+                const uint32_t dist = inf_dist_base(dc) + x;
+                o += nx;
+                state = kInfLit;
+                if (dist > pos) return false;
+                bool cut = false;
+                if (len > cap - pos) {  // the strip ends inside this match: keep what fits
+                    len = cap - pos;
+                    cut = true;
+                }
+                // each byte links to one before the match start (period dist
+                // when the match overlaps itself)
+                const uint32_t src = pos - dist;
+                if (dist >= len) {
+                    for (uint32_t x2 = (uint32_t)lane; x2 < len; x2 += kInfLanes) L[pos + x2] = src + x2;
+                } else {
+                    for (uint32_t x2 = (uint32_t)lane; x2 < len; x2 += kInfLanes) L[pos + x2] = src + x2 % dist;
+                }
+                pos += len;
+                if (cut) {
+                    b.P += o;
+                    full = true;
+                    return true;
+                }
+            }
+        }
+        b.P += o;
+        if (b.P > b.end_bits + 64) return false;  // far past the stream's end: truncated
+    }
+}
+
 __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
     __shared__ __attribute__((aligned(16))) InfShared S;
     const int s = blockIdx.x, lane = (int)threadIdx.x;
@@ -479,11 +596,9 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
     uint32_t pos = 0;
     const uint32_t h0 = inf_uni(n0 >= 1 ? in0[0] : 0u), h1 = inf_uni(n0 >= 2 ? in0[1] : 0u);
     bool bad = n0 < 2 || (h0 & 15) != 8 || (h0 >> 4) > 7 || ((h0 << 8) | h1) % 31 || (h1 & 0x20);
-    // the reader restarts after a stored block: base = stream bytes before it
-    uint64_t base = 0;
     InfIn b;
     b.init(in0, n0, S.ring, lane);
-    b.get(16);  // zlib CMF, FLG (checked above)
+    b.P += 16;  // zlib CMF, FLG (checked above)
     bool last = false;
     while (!bad && !last) {
         b.ensure();
@@ -494,13 +609,12 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
             uint32_t len = b.get(16);
             const uint32_t nlen = b.get(16);
             if (len != (~nlen & 0xFFFFu)) { bad = true; break; }
-            const uint64_t at = base + b.consumed() / 8;  // the block's first byte in the stream
+            const uint64_t at = b.consumed() / 8;  // the block's first byte in the stream
             if (at + len > n0) { bad = true; break; }     // truncated
             if (len > cap - pos) { len = cap - pos; last = true; }  // strip full: stop here
             for (uint32_t i = (uint32_t)lane; i < len; i += kInfLanes) L[pos + i] = kLinkByte | in0[at + i];
             pos += len;
-            base = at + len;  // (a partial block when the strip is full: nothing follows it)
-            b.init(in0 + base, n0 - base, S.ring, lane);
+            b.P += 8ull * len;
             continue;
         }
         if (type == 1) {  // fixed codes
@@ -549,42 +663,12 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
                 break;
             }
         } else { bad = true; break; }
-        for (;;) {  // literal / length-distance symbols up to end-of-block
-            b.ensure();
-            int sy = inf_decode<kInfLB>(b, S.lfast, S.lcnt, S.lsym);
-            if (sy < 256) {
-                if (sy < 0) { bad = true; break; }
-                if (pos >= cap) { last = true; break; }  // strip full: trailing data ignored
-                if (lane == 0) L[pos] = kLinkByte | (uint32_t)sy;
-                pos++;
-                continue;
-            }
-            if (sy == 256) break;
-            const uint32_t li = (uint32_t)sy - 257u;
-            if (li >= 29u) { bad = true; break; }
-            uint32_t len = inf_len_base(li) + b.get((int)inf_len_extra(li));
-            const int d = inf_decode<kInfDB>(b, S.dfast, S.dcnt, S.dsym);
-            if (d < 0 || d >= 30) { bad = true; break; }
-            const uint32_t dist = inf_dist_base((uint32_t)d) + b.get((int)inf_dist_extra((uint32_t)d));
-            if (dist > pos) { bad = true; break; }
-            bool full = false;
-            if (len > cap - pos) {  // the strip ends inside this match: keep what fits
-                len = cap - pos;
-                full = true;
-            }
-            // each byte links to one before the match start (period dist when
-            // the match overlaps itself)
-            const uint32_t src = pos - dist;
-            if (dist >= len) {
-                for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x;
-            } else {
-                for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x % dist;
-            }
-            pos += len;
-            if (full) { last = true; break; }
-        }
+        __builtin_amdgcn_wave_barrier();
+        bool full = false;
+        if (!inf_block(b, S, L, cap, pos, full, lane)) { bad = true; break; }
+        if (full) last = true;
     }
-    bad = bad || base * 8 + b.consumed() > 8 * n0;  // read past the end of the stream: truncated
+    bad = bad || b.P > b.end_bits;  // read past the end of the stream: truncated
     if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
 }
 

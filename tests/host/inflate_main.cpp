@@ -19,6 +19,10 @@
 #define JP2HIP_INF_LANES 1
 #define __builtin_amdgcn_readfirstlane(x) (x)
 #define __builtin_amdgcn_wave_barrier() ((void)0)
+#define __builtin_amdgcn_readlane(v, l) (v)  /* one lane: the only lane is 0 */
+static inline uint32_t __builtin_amdgcn_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+}
 struct uint4 { uint32_t x, y, z, w; };
 static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 static struct { int x, y; } blockIdx, threadIdx;
