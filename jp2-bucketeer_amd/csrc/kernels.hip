@@ -259,6 +259,9 @@ constexpr uint32_t kInChunkWords = 4 * kInfLanes;       // words per ring refill
 constexpr uint32_t kInRingWords = 2 * (kInChunkWords > 16 ? kInChunkWords : 16);  // >= two chunks
 constexpr int kInfLB = 12, kInfDB = 9;                  // direct-lookup bits: literal/length, distance
 constexpr uint32_t kLinkByte = 0x80000000u;             // link of a byte whose value is known
+// the literal/length direct lookup's entry for a longer code: bit 8 set like
+// every non-literal's, so "literal" is one bit test (entries: len << 9 | sym)
+constexpr uint32_t kInfNoFast = 0x100u;
 constexpr int kLinkDoublings = 5;                       // pointer-doubling rounds before the chase
 
 __constant__ uint8_t kInfClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -414,12 +417,13 @@ __device__ __forceinline__ uint32_t inf_ballot_below(bool p, int lane, uint32_t 
     return 0u;
 #endif
 }
-template <int FB>
+template <int FB, uint32_t EMPTY = 0u>
 __device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const uint8_t *len, int n, int lane,
                           uint32_t *scr) {
     uint32_t *cl = scr, *offs = scr + 16, *next = scr + 32, *seen = scr + 48;
     for (int i = lane; i < 64; i += kInfLanes) scr[i] = 0u;
-    for (int i = lane; i < (1 << FB) / 8; i += kInfLanes) ((uint4 *)fast)[i] = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t e2 = EMPTY * 0x10001u;
+    for (int i = lane; i < (1 << FB) / 8; i += kInfLanes) ((uint4 *)fast)[i] = make_uint4(e2, e2, e2, e2);
     __builtin_amdgcn_wave_barrier();
     for (int s = lane; s < n; s += kInfLanes)
         if (len[s]) atomicAdd(&cl[len[s]], 1u);
@@ -470,111 +474,140 @@ __device__ bool inf_build(uint16_t *cnt, uint16_t *sym, uint16_t *fast, const ui
 // literal/length table and the distance table, one LDS read each for the
 // whole wave), then the walk follows the actual symbol boundaries through
 // those lookups by readlane -- offset o, o + code length, ... -- with no
-// memory access until the walk leaves the window.  A symbol's parts (code,
-// length extra bits, distance code, distance extra bits) may straddle two
-// windows: the walk is a state machine that resumes in the next window.
-// Literals collect in a register (lane i = the i-th of a run) and are
-// stored kInfLanes at a time; a match's links are stored by the lanes.
-// Returns false on a corrupt stream; *last = the strip is full.
-enum { kInfLit, kInfLenX, kInfDist, kInfDistX };
+// memory access until the walk leaves the window.  Literals take a tight
+// loop; a match's parts (length extra bits, distance code, distance extra
+// bits) move to the next window whenever they start past this one.
+// A run of literals is stored by the lanes that hold them (each lane's own
+// table entry), at their ranks in the run; a match's links are stored by the
+// lanes.
+// Returns false on a corrupt stream; full = the strip is full.
+__device__ __attribute__((noinline)) int inf_walk_slow(const InfIn &b, uint64_t q, const uint16_t *cnt,
+                                                       const uint16_t *sym, int *len) {
+    return inf_walk_at(b, q, cnt, sym, len);
+}
 __device__ bool inf_block(InfIn &b, InfShared &S, uint32_t *L, uint32_t cap, uint32_t &pos, bool &full, int lane) {
-    int state = kInfLit;
-    uint32_t li = 0, len = 0, dc = 0;
-    uint32_t lit = 0, nlit = 0, lit0 = pos;  // pending literal run: lane i holds value i
-    auto flush_lits = [&]() {
-        if ((uint32_t)lane < nlit) L[lit0 + (uint32_t)lane] = kLinkByte | lit;
-        nlit = 0;
-    };
-    for (;;) {
+    uint32_t X = 0, Le = 0, De = 0, o = 0;
+    // the window at P: this lane's 32 bits from P + lane and the two table
+    // entries there
+    auto window = [&]() {
+        b.P += o;
+        o = 0;
         b.ensure();
-        // this lane's 32 bits from P + lane, and the two table entries there
         const uint64_t q = b.P + (uint64_t)lane;
         const uint32_t kw = (uint32_t)(q >> 5) % kInRingWords;
-        const uint32_t X = __builtin_amdgcn_alignbit(b.ring[(kw + 1) % kInRingWords], b.ring[kw], (uint32_t)(q & 31));
-        const uint32_t Le = S.lfast[X & ((1u << kInfLB) - 1u)], De = S.dfast[X & ((1u << kInfDB) - 1u)];
-        uint32_t o = 0;
-        while (o < (uint32_t)kInfLanes) {
-            if (state == kInfLit) {
-                uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)Le, (int)o), cl = e >> 9, sy = e & 511u;
-                if (!e) {  // a code longer than the direct lookup: walk it bit by bit
-                    int l;
-                    const int ws = inf_walk_at(b, b.P + o, S.lcnt, S.lsym, &l);
-                    if (ws < 0) return false;
-                    cl = (uint32_t)l;
-                    sy = (uint32_t)ws;
-                }
-                o += cl;
-                if (sy < 256u) {
-                    if (pos >= cap) {  // strip full: trailing data ignored
-                        flush_lits();
-                        b.P += o;
-                        full = true;
-                        return true;
-                    }
-                    if (nlit == 0) lit0 = pos;
-                    lit = (uint32_t)lane == nlit ? sy : lit;
-                    nlit++;
-                    pos++;
-                    if (nlit == (uint32_t)kInfLanes) flush_lits();
-                    continue;
-                }
-                flush_lits();
-                if (sy == 256u) {  // end of block
-                    b.P += o;
-                    return true;
-                }
-                li = sy - 257u;
-                if (li >= 29u) return false;
-                state = kInfLenX;
-            } else if (state == kInfLenX) {
-                const uint32_t nx = inf_len_extra(li);
-                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)o) & ((1u << nx) - 1u);
-                len = inf_len_base(li) + x;
-                o += nx;
-                state = kInfDist;
-            } else if (state == kInfDist) {
-                uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)De, (int)o), cl = e >> 9;
-                dc = e & 511u;
-                if (!e) {
-                    int l;
-                    const int ws = inf_walk_at(b, b.P + o, S.dcnt, S.dsym, &l);
-                    if (ws < 0) return false;
-                    cl = (uint32_t)l;
-                    dc = (uint32_t)ws;
-                }
-                if (dc >= 30u) return false;
-                o += cl;
-                state = kInfDistX;
-            } else {  // kInfDistX: the match
-                const uint32_t nx = inf_dist_extra(dc);
-                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, (int)o) & ((1u << nx) - 1u);
-                const uint32_t dist = inf_dist_base(dc) + x;
-                o += nx;
-                state = kInfLit;
-                if (dist > pos) return false;
-                bool cut = false;
-                if (len > cap - pos) {  // the strip ends inside this match: keep what fits
-                    len = cap - pos;
-                    cut = true;
-                }
-                // each byte links to one before the match start (period dist
-                // when the match overlaps itself)
-                const uint32_t src = pos - dist;
-                if (dist >= len) {
-                    for (uint32_t x2 = (uint32_t)lane; x2 < len; x2 += kInfLanes) L[pos + x2] = src + x2;
-                } else {
-                    for (uint32_t x2 = (uint32_t)lane; x2 < len; x2 += kInfLanes) L[pos + x2] = src + x2 % dist;
-                }
-                pos += len;
-                if (cut) {
-                    b.P += o;
+        X = __builtin_amdgcn_alignbit(b.ring[(kw + 1) % kInRingWords], b.ring[kw], (uint32_t)(q & 31));
+        Le = S.lfast[X & ((1u << kInfLB) - 1u)];
+        De = S.dfast[X & ((1u << kInfDB) - 1u)];
+    };
+    window();
+    for (;;) {
+        // the walk's state is wave-uniform; say so (the compiler's divergence
+        // analysis loses it through the stores of the lanes that hold literals)
+        pos = inf_uni(pos);
+        if (o >= (uint32_t)kInfLanes) {
+            window();
+            if (b.P > b.end_bits + 64) return false;  // far past the stream's end: truncated
+        }
+        // a run of literals inside this window: the walk only marks where
+        // each starts (bit o of `run`); the lane at that offset already holds
+        // the literal in its own table entry, and stores it at its rank in the
+        // run (at most kInfLanes literals: each code is at least one bit)
+        uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)Le, (int)o);
+        if (!(e & 0x100u) && cap - pos >= (uint32_t)kInfLanes) {
+            uint64_t run = 0;
+            do {
+                run |= 1ull << o;
+                o += e >> 9;
+                if (o >= (uint32_t)kInfLanes) break;
+                e = (uint32_t)__builtin_amdgcn_readlane((int)Le, (int)o);
+            } while (!(e & 0x100u));
+            run = inf_uni64(run);
+#if JP2HIP_INF_LANES > 1
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(run >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)run, 0u));
+#else
+            const uint32_t rank = 0u;
+#endif
+            if ((run >> lane) & 1ull) L[pos + rank] = kLinkByte | (Le & 255u);
+            pos += (uint32_t)__popcll(run);
+            if (o >= (uint32_t)kInfLanes) continue;
+        } else if (!(e & 0x100u)) {  // near the strip's end: one literal at a time
+            if (pos >= cap) {  // strip full: trailing data ignored
+                full = true;
+                b.P += o + (e >> 9);
+                return true;
+            }
+            L[pos] = kLinkByte | (e & 255u);  // every lane stores the same word
+            pos++;
+            o += e >> 9;
+            continue;
+        }
+        if (e == kInfNoFast) e = 0;  // (the walk below looks for 0)
+        uint32_t cl = e >> 9, sy = e & 511u;
+        if (!e) {  // a code longer than the direct lookup: walk it bit by bit
+            int l;
+            // (a call's results are per lane to the compiler: say they are uniform)
+            const int ws = (int)inf_uni((uint32_t)inf_walk_slow(b, b.P + o, S.lcnt, S.lsym, &l));
+            if (ws < 0) return false;
+            cl = inf_uni((uint32_t)l);
+            sy = (uint32_t)ws;
+            if (sy < 256u) {  // (rare) a long literal code
+                if (pos >= cap) {
                     full = true;
+                    b.P += o + cl;
                     return true;
                 }
+                L[pos] = kLinkByte | sy;  // every lane stores the same word
+                pos++;
+                o += cl;
+                continue;
             }
         }
-        b.P += o;
-        if (b.P > b.end_bits + 64) return false;  // far past the stream's end: truncated
+        o += cl;
+        if (sy == 256u) {  // end of block
+            b.P += o;
+            return true;
+        }
+        const uint32_t li = sy - 257u;
+        if (li >= 29u) return false;
+        if (o >= (uint32_t)kInfLanes) window();
+        const uint32_t nl = inf_len_extra(li);
+        uint32_t len = inf_len_base(li) + ((uint32_t)__builtin_amdgcn_readlane((int)X, (int)o) & ((1u << nl) - 1u));
+        o += nl;
+        if (o >= (uint32_t)kInfLanes) window();
+        uint32_t ed = (uint32_t)__builtin_amdgcn_readlane((int)De, (int)o), dc = ed & 511u, dl = ed >> 9;
+        if (!ed) {
+            int l;
+            const int ws = (int)inf_uni((uint32_t)inf_walk_slow(b, b.P + o, S.dcnt, S.dsym, &l));
+            if (ws < 0) return false;
+            dl = inf_uni((uint32_t)l);
+            dc = (uint32_t)ws;
+        }
+        if (dc >= 30u) return false;
+        o += dl;
+        if (o >= (uint32_t)kInfLanes) window();
+        const uint32_t nd = inf_dist_extra(dc);
+        const uint32_t dist = inf_dist_base(dc) + ((uint32_t)__builtin_amdgcn_readlane((int)X, (int)o) & ((1u << nd) - 1u));
+        o += nd;
+        if (dist > pos) return false;
+        bool cut = false;
+        if (len > cap - pos) {  // the strip ends inside this match: keep what fits
+            len = cap - pos;
+            cut = true;
+        }
+        // each byte links to one before the match start (period dist when
+        // the match overlaps itself)
+        const uint32_t src = pos - dist;
+        if (dist >= len) {
+            for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x;
+        } else {
+            for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x % dist;
+        }
+        pos += len;
+        if (cut) {
+            b.P += o;
+            full = true;
+            return true;
+        }
     }
 }
 
@@ -621,7 +654,7 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
             for (int i = lane; i < 318; i += kInfLanes)
                 S.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
             __builtin_amdgcn_wave_barrier();
-            inf_build<kInfLB>(S.lcnt, S.lsym, S.lfast, S.lens, 288, lane, S.scr);
+            inf_build<kInfLB, kInfNoFast>(S.lcnt, S.lsym, S.lfast, S.lens, 288, lane, S.scr);
             inf_build<kInfDB>(S.dcnt, S.dsym, S.dfast, S.lens + 288, 30, lane, S.scr);
         } else if (type == 2) {  // dynamic codes
             const int nlen = (int)b.get(5) + 257, ndist = (int)b.get(5) + 1, ncode = (int)b.get(4) + 4;
@@ -657,7 +690,7 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
             }
             __builtin_amdgcn_wave_barrier();
             if (bad || inf_uni(S.lens[256]) == 0) { bad = true; break; }
-            if (!inf_build<kInfLB>(S.lcnt, S.lsym, S.lfast, S.lens, nlen, lane, S.scr) ||
+            if (!inf_build<kInfLB, kInfNoFast>(S.lcnt, S.lsym, S.lfast, S.lens, nlen, lane, S.scr) ||
                 !inf_build<kInfDB>(S.dcnt, S.dsym, S.dfast, S.lens + nlen, ndist, lane, S.scr)) {
                 bad = true;
                 break;

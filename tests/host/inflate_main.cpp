@@ -20,6 +20,7 @@
 #define __builtin_amdgcn_readfirstlane(x) (x)
 #define __builtin_amdgcn_wave_barrier() ((void)0)
 #define __builtin_amdgcn_readlane(v, l) (v)  /* one lane: the only lane is 0 */
+#define __popcll(x) __builtin_popcountll(x)
 static inline uint32_t __builtin_amdgcn_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
 }
