@@ -599,8 +599,14 @@ __device__ bool inf_block(InfIn &b, InfShared &S, uint32_t *L, uint32_t cap, uin
         const uint32_t src = pos - dist;
         if (dist >= len) {
             for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x;
-        } else {
-            for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) L[pos + x] = src + x % dist;
+        } else {  // byte x repeats byte x mod dist before the match: one division per match
+            uint32_t r = (uint32_t)lane % dist;
+            const uint32_t step = (uint32_t)kInfLanes % dist;
+            for (uint32_t x = (uint32_t)lane; x < len; x += kInfLanes) {
+                L[pos + x] = src + r;
+                r += step;
+                r = r >= dist ? r - dist : r;
+            }
         }
         pos += len;
         if (cut) {
