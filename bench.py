@@ -335,6 +335,8 @@ def run(args):
         all_stats.append(st.as_dict())
         alone.append(st.as_dict())
 
+    host_delay = float(os.environ.get("JP2HIP_BENCH_HOST_DELAY_MS", "0")) / 1e3
+
     def timed(encode):
         """K steps over the contexts from a shared counter; (seconds, stats)."""
         stages, errors = [], []
@@ -350,6 +352,8 @@ def run(args):
                     if step >= total:
                         return
                     out, st = encode(encs[k])
+                    if host_delay:  # experiment only: a longer host turnaround per encode
+                        time.sleep(host_delay)
                     # the file stays in the library's pinned buffer (no copy
                     # into a Python bytes object); check it ends in EOC
                     ok = bytes(out.view()[-2:]) == b"\xff\xd9"

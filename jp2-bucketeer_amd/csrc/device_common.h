@@ -44,14 +44,20 @@ __device__ __forceinline__ int64_t dist_gain_small(uint32_t v, int p, bool lossl
     return (int64_t)(e1 * e1) - (int64_t)(e0 * e0);
 }
 
-__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        int lo = __shfl_xor((int)(uint32_t)v, o, 64);
-        int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), o, 64);
-        v += (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-    }
-    return v;
+// Whole-wave lane shifts by DPP (wave_shr:1 / wave_shl:1, GFX9 family): a
+// VALU move, not an LDS-crossbar ds_bpermute with its latency.  Lane 0
+// (shr) / lane 63 (shl) receive 0.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {  // lane i <- lane i-1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t x) {  // lane i <- lane i+1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint64_t wave_shr1(uint64_t x) {
+    return ((uint64_t)wave_shr1((uint32_t)(x >> 32)) << 32) | wave_shr1((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t wave_shl1(uint64_t x) {
+    return ((uint64_t)wave_shl1((uint32_t)(x >> 32)) << 32) | wave_shl1((uint32_t)x);
 }
 
 // inclusive prefix sum over the 64 lanes of a wave (DPP row shifts, then the
@@ -66,7 +72,43 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t n) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
     return (uint32_t)v;
 }
-// exclusive scan over a workgroup of NT threads (every thread calls it);
+// OR over the wave (every lane), by the same DPP steps
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t n) {
+    int v = (int)n;
+    v |= __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v |= __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_readlane(v, 63);
+}
+// the wave's total (every lane), by the DPP scan and lane 63
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t n) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(n), 63);
+}
+// 64-bit total: the same scan on both halves, the carries of the low half
+// added into the high one
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+    uint64_t x = (uint64_t)v;
+#define JP2HIP_SCAN64_STEP(ctl, rm)                                                                            \
+    {                                                                                                          \
+        const uint32_t lo_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, ctl, rm, 0xf, false);   \
+        const uint32_t hi_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), ctl, rm, 0xf, false); \
+        x += ((uint64_t)hi_ << 32) | lo_;                                                                      \
+    }
+    JP2HIP_SCAN64_STEP(0x111, 0xf)
+    JP2HIP_SCAN64_STEP(0x112, 0xf)
+    JP2HIP_SCAN64_STEP(0x114, 0xf)
+    JP2HIP_SCAN64_STEP(0x118, 0xf)
+    JP2HIP_SCAN64_STEP(0x142, 0xa)
+    JP2HIP_SCAN64_STEP(0x143, 0xc)
+#undef JP2HIP_SCAN64_STEP
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// exclusive scan of NT threads (every thread calls it);
 // wsum: NT/64 + 1 words of LDS; `tot` = the workgroup's sum
 template <int NT>
 __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t n, uint32_t *wsum, uint32_t &tot) {

@@ -545,7 +545,10 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
 // in the same order as lift_regs / oracle fwd97_1d (bit-exact): an update
 // whose neighbour lies outside the streamed rows is skipped, as lift_regs
 // leaves a window's edge stale, and never reaches a kept row.
-constexpr int kStreamBand = 64;
+#ifndef JP2HIP_STREAM_BAND
+#define JP2HIP_STREAM_BAND 64
+#endif
+constexpr int kStreamBand = JP2HIP_STREAM_BAND;
 template <bool REV, int NC, int CPT, int RB, bool ALIGNED>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     extern __shared__ int32_t lds[];

@@ -861,9 +861,9 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
         for (int y = 0; y < 64; y++)
             if (y < d.h) sm[y * 64] = (int32_t)col[y];
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-    // the wave-reduced maximum is uniform: keep P (and the plane loop) scalar
+    // the magnitude bits of the block = those of the OR of its magnitudes
+    // (a DPP reduction; uniform: P and the plane loop stay scalar)
+    vmax = wave_or_u32(vmax);
     const int P = __builtin_amdgcn_readfirstlane(vmax ? 32 - __clz(vmax) : 0);
     if (lane == 0) a.P[b] = (uint8_t)P;
     // column masks (lane c, bit y = row y): BT[p][c] = bit p of the
@@ -959,19 +959,17 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
         ST[(size_t)p * 64 + lane] = colS;
         // insignificant samples with a significant 8-neighbour (rows < h,
         // columns < w)
-        // (the shuffles run on every lane: a lane left out of a ds_bpermute
-        // reads as 0 to the lane that fetches from it)
-        const uint64_t up = (uint64_t)__shfl_up((long long)colS, 1, 64);
-        const uint64_t dn = (uint64_t)__shfl_down((long long)colS, 1, 64);
-        const uint64_t Lc = lane > 0 ? up : 0ull, Rc = lane < 63 ? dn : 0ull;
+        // (DPP whole-wave shifts on every lane: lanes 0 / 63 receive 0)
+        const uint64_t Lc = wave_shr1(colS), Rc = wave_shl1(colS);
         const uint64_t H = colS | Lc | Rc;
         uint32_t cN = wcol ? (uint32_t)__popcll((H | (H << 1) | (H >> 1)) & ~colS & hmask) : 0u;
         uint32_t cS = (uint32_t)__popcll(colS);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            cS += (uint32_t)__shfl_xor((int)cS, o, 64);
-            cN += (uint32_t)__shfl_xor((int)cN, o, 64);
-            nb1 += (uint32_t)__shfl_xor((int)nb1, o, 64);
+        // wave totals by DPP scans; cS and cN (<= 4096 each) share one scan
+        {
+            const uint32_t both = wave_sum_u32(cS | (cN << 16));
+            cS = both & 0xFFFFu;
+            cN = both >> 16;
+            nb1 = wave_sum_u32(nb1);
         }
         if (p <= 23) {
             const int64_t SV = wave_sum64(sv), SL = wave_sum64(sl);

@@ -86,16 +86,9 @@ __device__ __forceinline__ int order_bucket(uint32_t n) {
 constexpr uint64_t kStripeTop = 0x1111111111111111ull;  // rows with r % 4 == 0
 constexpr uint64_t kStripeBot = 0x8888888888888888ull;  // rows with r % 4 == 3
 
-__device__ __forceinline__ uint64_t col_left(uint64_t x, int lane) {  // column c-1's word
-    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, 1, 64);
-    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), 1, 64);
-    return lane == 0 ? 0ull : (((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ uint64_t col_right(uint64_t x, int lane) {  // column c+1's word
-    const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)x, 1, 64);
-    const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(x >> 32), 1, 64);
-    return lane == 63 ? 0ull : (((uint64_t)hi << 32) | lo);
-}
+// (DPP whole-wave shifts: lane 0 / 63 get 0, no ds_bpermute round trip)
+__device__ __forceinline__ uint64_t col_left(uint64_t x, int) { return wave_shr1(x); }   // column c-1's word
+__device__ __forceinline__ uint64_t col_right(uint64_t x, int) { return wave_shl1(x); }  // column c+1's word
 
 // The 8 neighbour masks of every row of the lane's column under (Vb, Va).
 struct Nbr8 {
@@ -565,12 +558,19 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
 #ifndef JP2HIP_MQ_RING_IL
 #define JP2HIP_MQ_RING_IL 0
 #endif
+// ring bytes per lane (packed layout): 64, or 32 (flushed 8 bytes at a time,
+// 2 KB less LDS per workgroup)
+#ifndef JP2HIP_MQ_RING_BYTES
+#define JP2HIP_MQ_RING_BYTES 64
+#endif
+constexpr int kRingLaneBytes = JP2HIP_MQ_RING_IL ? 64 : JP2HIP_MQ_RING_BYTES;
+constexpr int kRingFlush = kRingLaneBytes / 4;  // bytes per flush group
 #if JP2HIP_MQ_RING_IL
 constexpr int kRingLaneStride = 4;
 __device__ __forceinline__ int ring_slot(int bp) { return ((bp & 60) << 6) | (bp & 3); }
 #else
-constexpr int kRingLaneStride = 68;
-__device__ __forceinline__ int ring_slot(int bp) { return bp & 63; }
+constexpr int kRingLaneStride = kRingLaneBytes + 4;  // odd dword stride: lanes on different banks
+__device__ __forceinline__ int ring_slot(int bp) { return bp & (kRingLaneBytes - 1); }
 #endif
 
 __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
@@ -579,7 +579,7 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
         B++;
         m.C &= 0x7FFFFFFu;
     }
-    ring[ring_slot(m.bp)] = (uint8_t)B;  // bp = -1 -> slot 63, see mq_step
+    ring[ring_slot(m.bp)] = (uint8_t)B;  // bp = -1 -> the ring's last slot, see mq_code
     m.bp++;
     const bool ff = B == 0xFF;
     m.B = ff ? (m.C >> 20) : (m.C >> 19);
@@ -653,7 +653,8 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
     // byte-out the slot is the next byte's, written again when it is emitted
     // and never flushed before (ring_flush copies whole groups below bp).
     // Byte -1 (the MQ coder's initial pending byte, never output) lands in
-    // slot 63, which byte 63 overwrites before that group is flushed
+    // the ring's last slot, which the byte of that slot overwrites before
+    // its group is flushed
     ring[ring_slot(m.bp)] = (uint8_t)Bc;
     uint32_t Cx = bo ? (C2 & ((1u << sh) - 1u)) : C1;
     int CTx = bo ? 27 - (int)sh : CT - n;
@@ -673,17 +674,25 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
 
 // Copy the lane's completed 16-byte ring groups to the code-block output.
 __device__ __forceinline__ void ring_flush(const Mq &m, const uint8_t *ring, int &fl) {
-    while (m.bp - fl >= 16) {
-        uint4 v;
+    while (m.bp - fl >= kRingFlush) {
 #if JP2HIP_MQ_RING_IL
+        uint4 v;
         const uint32_t *g = (const uint32_t *)(ring + ring_slot(fl));
         v.x = g[0]; v.y = g[64]; v.z = g[128]; v.w = g[192];
-#else
-        const uint32_t *g = (const uint32_t *)(ring + (fl & 63));
-        v.x = g[0]; v.y = g[1]; v.z = g[2]; v.w = g[3];
-#endif
         if (fl + 16 <= m.cap) *(uint4 *)(m.out + fl) = v;
-        fl += 16;
+#else
+        const uint32_t *g = (const uint32_t *)(ring + ring_slot(fl));
+        if (kRingFlush == 16) {
+            uint4 v;
+            v.x = g[0]; v.y = g[1]; v.z = g[2]; v.w = g[3];
+            if (fl + 16 <= m.cap) *(uint4 *)(m.out + fl) = v;
+        } else {
+            uint2 v;
+            v.x = g[0]; v.y = g[1];
+            if (fl + 8 <= m.cap) *(uint2 *)(m.out + fl) = v;
+        }
+#endif
+        fl += kRingFlush;
     }
 }
 
@@ -706,7 +715,7 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 struct MqShared {
     uint32_t cxs[20 * 64];                 // 19 contexts + CX_PAD, lane-interleaved (modeller)
     uint32_t mqt[94];                      // state table
-    uint32_t rings[64 * 17];               // coder: 64-byte ring per lane (ring_slot)
+    uint32_t rings[64 * (kRingLaneStride / 4) + (JP2HIP_MQ_RING_IL ? 64 * 16 : 0)];  // coder: byte ring per lane
     // (the bucket bases are done with before the first chunk: one LDS slot,
     // 19.1 KB a workgroup, 8 per CU instead of 7)
     union {
@@ -871,7 +880,12 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
 #pragma unroll
         for (int j = 0; j < kMqChunk; j++) cw[j] = in[j * 64];
 #pragma unroll
-        for (int j = 0; j < kMqChunk; j++) mq_code(m, cw[j], ring);
+        for (int j = 0; j < kMqChunk; j++) {
+            mq_code(m, cw[j], ring);
+            // a 32-byte ring is emptied twice a chunk: 8 decisions add at most
+            // 15 bytes (<= 15 shifts each), so <= 22 are pending
+            if (kRingLaneBytes < 64 && j == kMqChunk / 2 - 1) ring_flush(m, ring, fl);
+        }
         ring_flush(m, ring, fl);
     }
     if (b < 0) return;
@@ -899,7 +913,11 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
 // The launch's execution span is recorded in 100 MHz wall-clock ticks
 // (span[0] = ~earliest wave start, span[1] = latest lane end; vector atomics
 // on words k_quant zeroed).
+#ifdef JP2HIP_MQ_WAVES_PER_EU
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(JP2HIP_MQ_WAVES_PER_EU))) k_t1_mq(T1MqArgs a) {
+#else
 __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
+#endif
     __shared__ MqShared sh;
     const int tid = threadIdx.x, lane = tid & 63;
 #ifdef JP2HIP_MQ_PRIO
