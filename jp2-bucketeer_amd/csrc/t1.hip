@@ -56,7 +56,7 @@ constexpr int kCmWaves = 2;  // items per workgroup
 // wide), largest first; inside a bucket the order is whatever the atomics
 // give.  k_t1_cm3's last plane of a block files it (bslots[bucket][i]);
 // k_t1_mq maps its lanes through the bucket fills' prefix.
-constexpr unsigned long long kAccMask = (1ull << 40) - 1ull;
+[[maybe_unused]] constexpr unsigned long long kAccMask = (1ull << 40) - 1ull;
 __device__ __forceinline__ int order_bucket(uint32_t n) {
     const uint32_t v = n + 1u;
     const int e = 31 - __clz(v);                                      // 0..31
@@ -197,6 +197,8 @@ __device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, u
 // to the plan's item bound).
 // --------------------------------------------------------------------------
 constexpr int kRingBytes = 2048;
+constexpr int kRingGuard = 4;     // dwords past the ring: a lane's <= 4 dwords never wrap
+constexpr int kRingWords = kRingBytes / 4 + kRingGuard;
 constexpr int kCm3Blocks = 4096;  // workgroups (2 waves each) at most
 
 __device__ __forceinline__ uint32_t spread4(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
@@ -209,13 +211,17 @@ __device__ __forceinline__ uint32_t nibw(uint32_t w, int sh) { return __builtin_
 // Ring writer state (wave-uniform): `pos` = next byte of the plane's slot,
 // `fl` = bytes already stored to HBM (a multiple of 16).
 struct Ring {
-    uint32_t *r;  // this wave's ring (kRingBytes)
+    uint32_t *r;  // this wave's ring (kRingWords)
     uint8_t *out;
     int pos, fl;
 };
 
-// Place this lane's n bytes (o0, o1, o2 little-endian) at pos + its prefix;
-// returns the wave's total.
+// Place this lane's n bytes (o0, o1, o2 little-endian; NW = the dwords they
+// can span at any alignment: 2 for <= 4 bytes, 3 for <= 8, 4 for <= 12) at
+// pos + its prefix; returns the wave's total.  The lane's dwords are OR-ed
+// at one base address with constant offsets: dwords past the ring's end land
+// in its guard, which ring_drain folds back to the ring's start.
+template <int NW>
 __device__ __forceinline__ int ring_put(Ring &g, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t n, int lane) {
     // inclusive scan over the wave: DPP row shifts 1, 2, 4, 8, then lane 15
     // into 16..31 / 47 into 48..63 and lane 31 into 32..63
@@ -228,36 +234,48 @@ __device__ __forceinline__ int ring_put(Ring &g, uint32_t o0, uint32_t o1, uint3
     v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
     const int total = __builtin_amdgcn_readlane(v, 63);
     const uint32_t at = (uint32_t)g.pos + (uint32_t)v - n;
-    const uint32_t s = (at & 3u) * 8u;
-    const uint64_t w01 = (((uint64_t)o1 << 32) | o0) << s;
-    const uint32_t w2 = (uint32_t)(((((uint64_t)o2 << 32) | o1) << s) >> 32);
-    const uint32_t w3 = (uint32_t)(((uint64_t)o2 << s) >> 32);
-    const uint32_t d = at >> 2;
-    constexpr uint32_t M = kRingBytes / 4 - 1;
+    // the bytes shifted up by t = at & 3: dword k = bytes of (o_k : o_{k-1})
+    // funnel-shifted, one v_perm each (selector byte j = 4 + j - t)
+    const uint32_t t = at & 3u;
+    const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, t, 0u);  // t in every byte
+    uint32_t *q = g.r + ((at >> 2) & (uint32_t)(kRingBytes / 4 - 1));
     if (n) {
-        atomicOr(&g.r[d & M], (uint32_t)w01);
-        atomicOr(&g.r[(d + 1) & M], (uint32_t)(w01 >> 32));
-        atomicOr(&g.r[(d + 2) & M], w2);
-        atomicOr(&g.r[(d + 3) & M], w3);
+        atomicOr(q, o0 << (8u * t));
+        atomicOr(q + 1, __builtin_amdgcn_perm(o1, o0, sel));
+        if (NW >= 3) atomicOr(q + 2, __builtin_amdgcn_perm(o2, o1, sel));
+        if (NW >= 4) atomicOr(q + 3, __builtin_amdgcn_perm(0u, o2, sel));
     }
     return total;
 }
 
-// Store ring bytes [fl, upto) (upto a multiple of 16) and zero them.
+// Store ring bytes [fl, upto) (upto a multiple of 16) and zero them; the
+// guard's dwords (bytes that ran past the ring's end) are first OR-ed into
+// the ring's first dwords.  (Safe: pending bytes stay below 1792 < the ring,
+// so the ring's first dwords of the previous lap were stored and zeroed
+// before any lane reached its end again.)
 __device__ __forceinline__ void ring_drain(Ring &g, int upto, int lane) {
+    if (lane < kRingGuard) {
+        const uint32_t gv = g.r[kRingBytes / 4 + lane];
+        if (gv) {
+            g.r[lane] |= gv;
+            g.r[kRingBytes / 4 + lane] = 0u;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
     for (int o = g.fl + 16 * lane; o < upto; o += 1024) {
         uint4 *src = (uint4 *)((uint8_t *)g.r + (o & (kRingBytes - 1)));
         const uint4 v = *src;
         *src = make_uint4(0u, 0u, 0u, 0u);
         *(uint4 *)(g.out + o) = v;
     }
-    g.fl = upto;
+    g.fl = __builtin_amdgcn_readfirstlane(upto);
 }
 
 // After a stripe: whole KiBs leave the ring (a stripe adds <= 768 bytes, so
 // at most 1792 are pending).
 __device__ __forceinline__ void ring_step(Ring &g, int lane) {
-    if (g.pos - g.fl >= 1024) ring_drain(g, g.fl + 1024, lane);
+    // (wave-uniform: a scalar branch)
+    if (__builtin_amdgcn_readfirstlane(g.pos - g.fl) >= 1024) ring_drain(g, g.fl + 1024, lane);
 }
 
 // Pass end: neutral decisions to the next 16-byte boundary, every byte out.
@@ -287,26 +305,270 @@ __device__ __forceinline__ void zc_sg_bytes(const Half &m, int sh, uint32_t &zc,
          spread4s(nibw(m.c2, sh), 3);
 }
 
+// One bit-plane p (depth k = P-1-p) of block b: the three passes' decision
+// bytes through the wave's ring into the plane's stream slot, the pass counts
+// and the SPP distortion decrease stored; returns the plane's decisions.
+// B, S0 = S[p], S1 = S[p+1], S2 = S[p+2] and SG are the lane's column masks
+// (0 past the block width, S1 / S2 0 above the top plane).
+__device__ __forceinline__ uint32_t cm_plane(const T1CmArgs &a, Ring &g, const uint2 *lut, int lane, int b, int k,
+                                             int p, int P, int w, int h, int band, const uint64_t *CT, uint64_t B,
+                                             uint64_t S0, uint64_t S1, uint64_t S2, uint64_t SG, uint64_t LSG,
+                                             uint64_t RSG) {
+    const bool lossless = a.lossless != 0;
+    const bool vl = lane < w;
+    const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;
+    const int nstripes = (h + 3) >> 2;
+    g.out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
+    g.pos = 0;
+    g.fl = 0;
+    int n_spp = 0, n_mrp = 0;
+    const bool spp = p < P - 1;
+    const uint64_t LS1 = col_left(S1, lane), RS1 = col_right(S1, lane);
+    uint64_t N = 0, memS = 0;
+    if (spp) {
+        // ---- significance propagation: least fixed point of the causal rule ----
+        for (;;) {
+            const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
+            const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
+            const uint64_t cand = ~S1 & VR & (nb.UL | nb.U | nb.UR | nb.L | nb.R | nb.DL | nb.D | nb.DR);
+            const uint64_t Nn = cand & B;
+            if (!__any(Nn != N)) {
+                memS = cand;
+                break;
+            }
+            N = Nn;
+        }
+        {
+            const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
+            const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
+            const Ctx4 z = zc_masks(band, nb);
+            const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
+            for (int hf = 0; hf * 8 < nstripes; hf++) {
+                const Half m = half_of(hf, memS, B, z, sc, SG ^ sc.xr, 0);
+                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                    const int sh = s4 * 4;
+                    const uint32_t mem = nibw(m.mem, sh);
+                    if (!__any(mem)) continue;
+                    uint32_t zc, sg;
+                    zc_sg_bytes(m, sh, zc, sg);
+                    const uint32_t K = mem | ((mem & nibw(m.bb, sh)) << 4);
+                    const uint2 sel = lut[K];
+                    const uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
+                    g.pos += ring_put<3>(g, o0, o1, 0u, (uint32_t)__popc(K), lane);
+                    ring_step(g, lane);
+                }
+            }
+        }
+        n_spp = g.pos;
+        ring_pass_end(g, lane);
+        const int mrp0 = g.pos;
+        // ---- magnitude refinement: neighbours in the post-SPP state ----
+        {
+            const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
+            const uint64_t anyn = (Pst << 1) | (Pst >> 1) | LP | RP | (LP << 1) | (RP << 1) | (LP >> 1) | (RP >> 1);
+            const uint64_t memM = S1 & VR, fr = S1 & ~S2, fa = fr & anyn;
+            for (int hf = 0; hf * 8 < nstripes; hf++) {
+                const int hs = hf * 32;
+                const uint32_t wm = (uint32_t)(memM >> hs), wb = (uint32_t)(B >> hs), wf = (uint32_t)(fr >> hs),
+                               wa = (uint32_t)(fa >> hs);
+                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                    const int sh = s4 * 4;
+                    const uint32_t mem = nibw(wm, sh);
+                    if (!__any(mem)) continue;
+                    // ctx 14 (first refinement), 15 (... with a significant
+                    // neighbour), 16 (later refinements): bytes 0x1C, 0x1E, 0x20
+                    const uint32_t f = spread4(nibw(wf, sh));
+                    const uint32_t mr = spread4(nibw(wb, sh)) | (f * 0x1Cu) | (spread4(nibw(wa, sh)) << 1) |
+                                        ((0x01010101u ^ f) << 5);
+                    const uint32_t o0 = __builtin_amdgcn_perm(0u, mr, lut[mem].x);
+                    g.pos += ring_put<2>(g, o0, 0u, 0u, (uint32_t)__popc(mem), lane);
+                    ring_step(g, lane);
+                }
+            }
+        }
+        n_mrp = g.pos - mrp0;
+        ring_pass_end(g, lane);
+    }
+    const int cup0 = g.pos;
+    // ---- cleanup: visited neighbours in S[p], the others post-SPP ----
+    {
+        const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
+        const uint64_t LS0 = col_left(S0, lane), RS0 = col_right(S0, lane);
+        const Nbr8 nb = nbr8(S0, Pst, LS0, RS0, LP, RP);
+        const Ctx4 z = zc_masks(band, nb);
+        const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
+        const uint64_t memC = ~S1 & ~memS & VR;
+        // run-length mode blocked by a significant neighbour: left column
+        // (visited) in S[p], right column post-SPP, the row above a stripe
+        // in S[p], the row below it post-SPP
+        const uint64_t side = LS0 | RP, above = S0 | LS0 | RS0, below = Pst | LP | RP;
+        const uint64_t blk = side | ((above << 1) & kStripeTop) | ((below >> 1) & kStripeBot);
+        for (int hf = 0; hf * 8 < nstripes; hf++) {
+            const Half m = half_of(hf, memC, B, z, sc, SG ^ sc.xr, blk);
+            for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                const int sh = s4 * 4;
+                const uint32_t mem = nibw(m.mem, sh);
+                if (!__any(mem)) continue;
+                uint32_t zc, sg;
+                zc_sg_bytes(m, sh, zc, sg);
+                const uint32_t bb = nibw(m.bb, sh);
+                // four members, none with a significant neighbour (mem ==
+                // 0xF implies the stripe's four rows lie inside the block)
+                const bool rl = mem == 0xFu && nibw(m.x, sh) == 0u;
+                const uint32_t r = __builtin_ctz(bb | 16u);
+                const uint32_t mr = rl ? (0xEu << r) & 0xFu : mem;  // samples coded normally
+                const uint32_t K = mr | ((mr & bb) << 4);
+                const uint2 sel = lut[K];
+                uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
+                uint32_t o2 = 0u;
+                uint32_t n = (uint32_t)__popc(K);
+                if (rl) {  // run-length prefix: RL 0 alone, or RL 1, two UNI bits, row r's sign
+                    if (bb == 0u) {
+                        o0 = (uint32_t)(CX_RL << 1);
+                        n = 1;
+                    } else {
+                        o2 = o1;
+                        o1 = o0;
+                        o0 = (uint32_t)((CX_RL << 1) | 1) | ((uint32_t)((CX_UNI << 1) | (r >> 1)) << 8) |
+                             ((uint32_t)((CX_UNI << 1) | (r & 1u)) << 16) | (((sg >> (8 * r)) & 0xFFu) << 24);
+                        n += 4;
+                    }
+                }
+                g.pos += ring_put<4>(g, o0, o1, o2, n, lane);
+                ring_step(g, lane);
+            }
+        }
+    }
+    const int n_cup = g.pos - cup0;
+    ring_pass_end(g, lane);
+    // SPP distortion decrease: the newly significant samples N have top bit
+    // p, each gains 2^p (12 v + 6d - 9 2^p) (d = 1 lossy, 0 lossless; 4 at
+    // lossless p = 0), and sum_N v = 2^p |N| + sum_{q<p} 2^q |N & B[q]|
+    // from the column masks of the lower planes (dist_gain, exact)
+    int64_t nN = 0, sv = 0;
+    if (spp && __any(N != 0ull)) {
+        nN = __popcll(N);
+        sv = nN << p;
+        // (N is 0 on lanes past the block width: no lane test, so the
+        // unrolled loads issue together)
+#pragma unroll 4
+        for (int q = 0; q < p; q++) sv += (int64_t)__popcll(N & CT[(size_t)q * 64 + lane]) << q;
+    }
+    nN = wave_sum64(nN);
+    sv = wave_sum64(sv);
+    const int64_t dspp = (lossless && p == 0) ? 4 * nN
+                                              : ((12 * sv + (6 * (lossless ? 0 : 1) - 9 * ((int64_t)1 << p)) * nN) << p);
+    if (lane == 0) {
+        uint4 cnt;
+        cnt.x = (uint32_t)n_spp;
+        cnt.y = (uint32_t)n_mrp;
+        cnt.z = (uint32_t)n_cup;
+        cnt.w = 0;
+        a.counts[(size_t)b * 32 + k] = cnt;
+        a.dspp[(size_t)b * 32 + k] = dspp;
+    }
+    return (uint32_t)(n_spp + n_mrp + n_cup);
+}
+
+// Compaction selectors of the stripe step: entry K = members (bits 0-3) |
+// members with a 1 bit (bits 4-7); output byte order q = 0..3: zc byte q
+// (selector q), then its sign byte (selector 4 + q); unused bytes select 0x00
+// (0x0C).  (Byte n of the 64-bit pair set by shifts: no private array.)
+__device__ __forceinline__ uint2 cm_selectors(int K) {
+    uint64_t sel = 0x0C0C0C0C0C0C0C0Cull;
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int bit = (q & 1) ? 4 + (q >> 1) : (q >> 1);  // zc q/2, then its sign
+        if ((K >> bit) & 1) {
+            sel = (sel & ~(0xFFull << (8 * n))) | ((uint64_t)((q & 1) ? 4 + (q >> 1) : (q >> 1)) << (8 * n));
+            n++;
+        }
+    }
+    return make_uint2((uint32_t)sel, (uint32_t)(sel >> 32));
+}
+
+#ifndef JP2HIP_CM_ITEMS
+// k_t1_cm3, one wave per code-block: the block's coded planes top-down, in
+// order, so a plane's S[p+1] and S[p+2] are the masks the wave already holds
+// and the next plane's two masks load while this one is coded (one dependent
+// descriptor chain per block instead of per plane); the block's decision
+// total is known at its end, where it is filed in its MQ lane-order bucket.
+// Blocks are taken from the depth-0 work list (every block with a coded
+// plane) in a grid-stride loop.
+#ifdef JP2HIP_CM_WAVES_PER_EU
+__global__ void __launch_bounds__(64 * kCmWaves) __attribute__((amdgpu_waves_per_eu(JP2HIP_CM_WAVES_PER_EU))) k_t1_cm3(T1CmArgs a) {
+#else
+__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
+#endif
+    __shared__ uint2 lut[256];
+    __shared__ uint32_t rings[kCmWaves][kRingWords];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int K = threadIdx.x; K < 256; K += 64 * kCmWaves) lut[K] = cm_selectors(K);
+    for (int i = threadIdx.x; i < kCmWaves * kRingWords; i += 64 * kCmWaves) (&rings[0][0])[i] = 0u;
+    __syncthreads();
+    const int nblk = a.kmax > 0 ? (int)a.dfill[0] : 0;
+    Ring g;
+    g.r = rings[wv];
+    for (int bi = blockIdx.x * kCmWaves + wv; bi < nblk; bi += gridDim.x * kCmWaves) {
+        const int b = a.dlist[bi];
+        const BlockDesc d = a.blocks[b];
+        const int P = a.P[b];
+        const int c = (int)(a.acc[b] >> 40);  // coded planes (emit_t1_items)
+        const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
+        const bool vl = lane < w;
+        const uint64_t *CT = a.bp + d.bp_off;
+        const uint64_t SGl = CT[(size_t)2 * Mb * 64 + lane];
+        uint64_t Bl = CT[(size_t)(P - 1) * 64 + lane];
+        uint64_t S0l = CT[(size_t)(Mb + P - 1) * 64 + lane];
+        const uint64_t SG = vl ? SGl : 0ull;
+        const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
+        uint64_t S1 = 0, S2 = 0;
+        uint32_t tot = 0;
+        const uint32_t cap = plane_stream_cap(w, h);
+        uint8_t *out = a.stream + a.slot_off[b];
+        for (int k = 0; k < c; k++) {
+            const int p = P - 1 - k;
+            const uint64_t B = vl ? Bl : 0ull, S0 = vl ? S0l : 0ull;
+            if (k + 1 < c) {  // the next plane's masks, in flight during this one
+                Bl = CT[(size_t)(p - 1) * 64 + lane];
+                S0l = CT[(size_t)(Mb + p - 1) * 64 + lane];
+            }
+            g.out = out + (size_t)k * cap;
+            g.pos = 0;
+            g.fl = 0;
+            tot += cm_plane(a, g, lut, lane, b, k, p, P, w, h, band, CT, B, S0, S1, S2, SG, LSG, RSG);
+#ifdef JP2HIP_BURN_VALU  // resource experiments only: N dependent VALU per plane
+            {
+                uint32_t x = (uint32_t)B ^ (uint32_t)lane;
+                for (int i = 0; i < JP2HIP_BURN_VALU; i++) x = (x ^ (uint32_t)i) + (x << 3);
+                if (x == 0x9E3779B9u) a.counts[(size_t)b * 32 + k].w = x;
+            }
+#endif
+#ifdef JP2HIP_BURN_SLEEP  // ... or a wave that idles N x 64 cycles per plane
+            __builtin_amdgcn_s_sleep(JP2HIP_BURN_SLEEP);
+#endif
+            S2 = S1;
+            S1 = S0;
+        }
+        if (lane == 0 && c > 0) {
+            a.acc[b] = tot;  // decisions (k_hull's tier-1 totals); no planes left
+            const int bk = order_bucket(tot);
+            a.bslots[(size_t)bk * a.nb + atomicAdd(&a.bfill[bk], 1u)] = b;
+        }
+    }
+}
+#else
+// k_t1_cm3 over (block, plane) items (A/B builds: -DJP2HIP_CM_ITEMS)
 __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
     __shared__ uint2 lut[256];
-    __shared__ uint32_t rings[kCmWaves][kRingBytes / 4];
+    __shared__ uint32_t rings[kCmWaves][kRingWords];
     __shared__ uint32_t dbase[65];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // compaction selectors: entry K = members (bits 0-3) | members with a 1
-    // bit (bits 4-7); output byte order q = 0..3: zc byte q (selector q), then
-    // its sign byte (selector 4 + q); unused bytes select 0x00 (0x0C)
-    for (int K = threadIdx.x; K < 256; K += 64 * kCmWaves) {
-        uint32_t sel[8] = {12, 12, 12, 12, 12, 12, 12, 12};
-        int n = 0;
-        for (int q = 0; q < 4; q++) {
-            if ((K >> q) & 1) sel[n++] = (uint32_t)q;
-            if ((K >> (4 + q)) & 1) sel[n++] = 4u + (uint32_t)q;
-        }
-        lut[K] = make_uint2(sel[0] | sel[1] << 8 | sel[2] << 16 | sel[3] << 24,
-                            sel[4] | sel[5] << 8 | sel[6] << 16 | sel[7] << 24);
-    }
-    for (int i = threadIdx.x; i < kCmWaves * kRingBytes / 4; i += 64 * kCmWaves) (&rings[0][0])[i] = 0u;
+    for (int K = threadIdx.x; K < 256; K += 64 * kCmWaves) lut[K] = cm_selectors(K);
+    for (int i = threadIdx.x; i < kCmWaves * kRingWords; i += 64 * kCmWaves) (&rings[0][0])[i] = 0u;
     // item = (depth k, entry) of the per-depth lists (emit_t1_items): the
     // depth bases are an exclusive scan of the list fills
     if (threadIdx.x < 64) {
@@ -327,177 +589,25 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         const BlockDesc d = a.blocks[b];
         const int P = a.P[b];
         const int p = P - 1 - k;
-        const bool lossless = a.lossless != 0;
         const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
         const bool vl = lane < w;
-        const uint64_t VR = vl ? (h >= 64 ? ~0ull : ((1ull << h) - 1ull)) : 0ull;
         const uint64_t *CT = a.bp + d.bp_off;
-        // the five mask loads issue together (no load under a branch; rows
-        // past S[Mb-1] read the sign row and are dropped by the selects)
         const uint64_t Bl = CT[(size_t)p * 64 + lane];
         const uint64_t S0l = CT[(size_t)(Mb + p) * 64 + lane];
         const uint64_t S1l = CT[(size_t)min(Mb + p + 1, 2 * Mb) * 64 + lane];
         const uint64_t S2l = CT[(size_t)min(Mb + p + 2, 2 * Mb) * 64 + lane];
         const uint64_t SGl = CT[(size_t)2 * Mb * 64 + lane];
-        const uint64_t B = vl ? Bl : 0ull;
-        const uint64_t S0 = vl ? S0l : 0ull;
-        const uint64_t S1 = (vl && p + 1 < P) ? S1l : 0ull;
-        const uint64_t S2 = (vl && p + 2 < P) ? S2l : 0ull;
         const uint64_t SG = vl ? SGl : 0ull;
-        const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
-        const int nstripes = (h + 3) >> 2;
         g.out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
         g.pos = 0;
         g.fl = 0;
-        int n_spp = 0, n_mrp = 0;
-        const bool spp = p < P - 1;
-        const uint64_t LS1 = col_left(S1, lane), RS1 = col_right(S1, lane);
-        uint64_t N = 0, memS = 0;
-        if (spp) {
-            // ---- significance propagation: least fixed point of the causal rule ----
-            for (;;) {
-                const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
-                const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
-                const uint64_t cand = ~S1 & VR & (nb.UL | nb.U | nb.UR | nb.L | nb.R | nb.DL | nb.D | nb.DR);
-                const uint64_t Nn = cand & B;
-                if (!__any(Nn != N)) {
-                    memS = cand;
-                    break;
-                }
-                N = Nn;
-            }
-            {
-                const uint64_t Vb = S1 | N, LVb = col_left(Vb, lane), RVb = col_right(Vb, lane);
-                const Nbr8 nb = nbr8(Vb, S1, LVb, RVb, LS1, RS1);
-                const Ctx4 z = zc_masks(band, nb);
-                const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
-                for (int hf = 0; hf * 8 < nstripes; hf++) {
-                    const Half m = half_of(hf, memS, B, z, sc, SG ^ sc.xr, 0);
-                    for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
-                        const int sh = s4 * 4;
-                        const uint32_t mem = nibw(m.mem, sh);
-                        if (!__any(mem)) continue;
-                        uint32_t zc, sg;
-                        zc_sg_bytes(m, sh, zc, sg);
-                        const uint32_t K = mem | ((mem & nibw(m.bb, sh)) << 4);
-                        const uint2 sel = lut[K];
-                        const uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
-                        g.pos += ring_put(g, o0, o1, 0u, (uint32_t)__popc(K), lane);
-                        ring_step(g, lane);
-                    }
-                }
-            }
-            n_spp = g.pos;
-            ring_pass_end(g, lane);
-            const int mrp0 = g.pos;
-            // ---- magnitude refinement: neighbours in the post-SPP state ----
-            {
-                const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
-                const uint64_t anyn = (Pst << 1) | (Pst >> 1) | LP | RP | (LP << 1) | (RP << 1) | (LP >> 1) | (RP >> 1);
-                const uint64_t memM = S1 & VR, fr = S1 & ~S2, fa = fr & anyn;
-                for (int hf = 0; hf * 8 < nstripes; hf++) {
-                    const int hs = hf * 32;
-                    const uint32_t wm = (uint32_t)(memM >> hs), wb = (uint32_t)(B >> hs), wf = (uint32_t)(fr >> hs),
-                                   wa = (uint32_t)(fa >> hs);
-                    for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
-                        const int sh = s4 * 4;
-                        const uint32_t mem = nibw(wm, sh);
-                        if (!__any(mem)) continue;
-                        // ctx 14 (first refinement), 15 (... with a significant
-                        // neighbour), 16 (later refinements): bytes 0x1C, 0x1E, 0x20
-                        const uint32_t f = spread4(nibw(wf, sh));
-                        const uint32_t mr = spread4(nibw(wb, sh)) | (f * 0x1Cu) | (spread4(nibw(wa, sh)) << 1) |
-                                            ((0x01010101u ^ f) << 5);
-                        const uint32_t o0 = __builtin_amdgcn_perm(0u, mr, lut[mem].x);
-                        g.pos += ring_put(g, o0, 0u, 0u, (uint32_t)__popc(mem), lane);
-                        ring_step(g, lane);
-                    }
-                }
-            }
-            n_mrp = g.pos - mrp0;
-            ring_pass_end(g, lane);
-        }
-        const int cup0 = g.pos;
-        // ---- cleanup: visited neighbours in S[p], the others post-SPP ----
-        {
-            const uint64_t Pst = S1 | N, LP = col_left(Pst, lane), RP = col_right(Pst, lane);
-            const uint64_t LS0 = col_left(S0, lane), RS0 = col_right(S0, lane);
-            const Nbr8 nb = nbr8(S0, Pst, LS0, RS0, LP, RP);
-            const Ctx4 z = zc_masks(band, nb);
-            const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
-            const uint64_t memC = ~S1 & ~memS & VR;
-            // run-length mode blocked by a significant neighbour: left column
-            // (visited) in S[p], right column post-SPP, the row above a stripe
-            // in S[p], the row below it post-SPP
-            const uint64_t side = LS0 | RP, above = S0 | LS0 | RS0, below = Pst | LP | RP;
-            const uint64_t blk = side | ((above << 1) & kStripeTop) | ((below >> 1) & kStripeBot);
-            for (int hf = 0; hf * 8 < nstripes; hf++) {
-                const Half m = half_of(hf, memC, B, z, sc, SG ^ sc.xr, blk);
-                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
-                    const int sh = s4 * 4;
-                    const uint32_t mem = nibw(m.mem, sh);
-                    if (!__any(mem)) continue;
-                    uint32_t zc, sg;
-                    zc_sg_bytes(m, sh, zc, sg);
-                    const uint32_t bb = nibw(m.bb, sh);
-                    // four members, none with a significant neighbour (mem ==
-                    // 0xF implies the stripe's four rows lie inside the block)
-                    const bool rl = mem == 0xFu && nibw(m.x, sh) == 0u;
-                    const uint32_t r = __builtin_ctz(bb | 16u);
-                    const uint32_t mr = rl ? (0xEu << r) & 0xFu : mem;  // samples coded normally
-                    const uint32_t K = mr | ((mr & bb) << 4);
-                    const uint2 sel = lut[K];
-                    uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
-                    uint32_t o2 = 0u;
-                    uint32_t n = (uint32_t)__popc(K);
-                    if (rl) {  // run-length prefix: RL 0 alone, or RL 1, two UNI bits, row r's sign
-                        if (bb == 0u) {
-                            o0 = (uint32_t)(CX_RL << 1);
-                            n = 1;
-                        } else {
-                            o2 = o1;
-                            o1 = o0;
-                            o0 = (uint32_t)((CX_RL << 1) | 1) | ((uint32_t)((CX_UNI << 1) | (r >> 1)) << 8) |
-                                 ((uint32_t)((CX_UNI << 1) | (r & 1u)) << 16) | (((sg >> (8 * r)) & 0xFFu) << 24);
-                            n += 4;
-                        }
-                    }
-                    g.pos += ring_put(g, o0, o1, o2, n, lane);
-                    ring_step(g, lane);
-                }
-            }
-        }
-        const int n_cup = g.pos - cup0;
-        ring_pass_end(g, lane);
-        // SPP distortion decrease: the newly significant samples N have top bit
-        // p, each gains 2^p (12 v + 6d - 9 2^p) (d = 1 lossy, 0 lossless; 4 at
-        // lossless p = 0), and sum_N v = 2^p |N| + sum_{q<p} 2^q |N & B[q]|
-        // from the column masks of the lower planes (dist_gain, exact)
-        int64_t nN = 0, sv = 0;
-        if (spp && __any(N != 0ull)) {
-            nN = __popcll(N);
-            sv = nN << p;
-            // (N is 0 on lanes past the block width: no lane test, so the
-            // unrolled loads issue together)
-#pragma unroll 4
-            for (int q = 0; q < p; q++) sv += (int64_t)__popcll(N & CT[(size_t)q * 64 + lane]) << q;
-        }
-        nN = wave_sum64(nN);
-        sv = wave_sum64(sv);
-        const int64_t dspp = (lossless && p == 0) ? 4 * nN
-                                                  : ((12 * sv + (6 * (lossless ? 0 : 1) - 9 * ((int64_t)1 << p)) * nN) << p);
+        const uint32_t nd = cm_plane(a, g, lut, lane, b, k, p, P, w, h, band, CT, vl ? Bl : 0ull, vl ? S0l : 0ull,
+                                     (vl && p + 1 < P) ? S1l : 0ull, (vl && p + 2 < P) ? S2l : 0ull, SG,
+                                     col_left(SG, lane), col_right(SG, lane));
         if (lane == 0) {
-            uint4 cnt;
-            cnt.x = (uint32_t)n_spp;
-            cnt.y = (uint32_t)n_mrp;
-            cnt.z = (uint32_t)n_cup;
-            cnt.w = 0;
-            a.counts[(size_t)b * 32 + k] = cnt;
-            a.dspp[(size_t)b * 32 + k] = dspp;
             // one atomic per plane: planes left (bits 40+) down by one,
             // decisions up; the block's last plane knows its total and files
             // the block in its MQ lane-order bucket
-            const uint32_t nd = (uint32_t)(n_spp + n_mrp + n_cup);
             const unsigned long long old = atomicAdd(&a.acc[b], (unsigned long long)nd - (1ull << 40));
             if ((old >> 40) == 1ull) {
                 const uint32_t tot = (uint32_t)(old & kAccMask) + nd;
@@ -507,6 +617,7 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         }
     }
 }
+#endif
 
 // --------------------------------------------------------------------------
 // MQ coder
@@ -913,11 +1024,7 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
 // The launch's execution span is recorded in 100 MHz wall-clock ticks
 // (span[0] = ~earliest wave start, span[1] = latest lane end; vector atomics
 // on words k_quant zeroed).
-#ifdef JP2HIP_MQ_WAVES_PER_EU
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(JP2HIP_MQ_WAVES_PER_EU))) k_t1_mq(T1MqArgs a) {
-#else
 __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
-#endif
     __shared__ MqShared sh;
     const int tid = threadIdx.x, lane = tid & 63;
 #ifdef JP2HIP_MQ_PRIO
@@ -967,7 +1074,11 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (!a.max_items) return;
+#ifndef JP2HIP_CM_ITEMS
+    const dim3 g((a.nb + kCmWaves - 1) / kCmWaves);  // a wave per block at most
+#else
     const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
+#endif
     hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {

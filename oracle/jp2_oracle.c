@@ -1000,7 +1000,8 @@ static int predict_cut(const int64_t *hist, int64_t target) {
         acc += hist[k];
         if (acc >= goal) break;
     }
-    return k - kSkipMargin;
+    const char *m = getenv("ORACLE_SKIP_MARGIN");  /* experiments only (margin sweeps) */
+    return k - (m ? atoi(m) : kSkipMargin);
 }
 
 /* T1-code every block with its predicted plane range (skip mode) */
@@ -1035,6 +1036,7 @@ static int predict_and_code(encoder *E, int64_t target) {
             b->npasses = np;
             total += b->len;
         }
+        if (getenv("ORACLE_SKIP_DEBUG")) fprintf(stderr, "skip pass %d: coded %lld bytes, %lld decisions so far\n", pass, (long long)total, (long long)g_decisions);
         if (pass == 0 && !(skipped && total < target)) break;
     }
     for (int i = 0; i < E->nall; i++) { free(E->all[i]->sm); E->all[i]->sm = NULL; }
