@@ -814,52 +814,52 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     BlockDesc d = a.blocks[b];
     int lane = threadIdx.x & 63;
     bool act = lane < d.w;
+    // the block's first row (wave-uniform: each row load is a scalar base +
+    // the lane's column offset, no per-row address registers)
     const int32_t *src = (const int32_t *)a.coef + (size_t)d.tc * a.plane_w * a.plane_h +
-                         (size_t)d.y0 * a.plane_w + d.x0 + (act ? lane : 0);
+                         (size_t)d.y0 * a.plane_w + d.x0;
+    const int cl = act ? lane : 0;
     int32_t *sm = a.sm + d.sm_off + lane;
     // the sign-magnitude copy is read only by the 64-bit distortion path of
     // planes above 23 (below) and by the debug dumps
     const bool keep_sm = a.keep_sm || d.Mb > 24;
     uint32_t vmax = 0;
     uint32_t lim = (1u << d.Mb) - 1u;
-    // the lane's column stays in registers (sign | magnitude; 0 outside the
-    // block) for the bit-plane and distortion passes: the coefficients are
-    // read from HBM once.  Rows past the block end are a wave-uniform exit;
-    // lanes past its width read column 0 and keep 0.
-    // The row loads of each half block (32 rows) are issued before any is
-    // used (rows past the block end re-read its last row and are zeroed
-    // below): a load under a per-row branch was waited for before the next
-    // one issued.
+    // the lane's column stays in registers (sign | magnitude) for the
+    // bit-plane and distortion passes: the coefficients are read from HBM
+    // once.  All 64 row loads are in flight at once; rows past the block end
+    // re-read its last row and lanes past its width read column 0 -- values
+    // of the block, so its maximum is unchanged -- and are cleared from the
+    // bit-plane masks (`valid`), not row by row.
     uint32_t col[64];
     const int hm1 = d.h - 1;
-    // all 64 row loads in flight at once (the column lives in 64 registers
-    // either way)
 #pragma unroll
-    for (int y = 0; y < 64; y++) col[y] = (uint32_t)src[(size_t)min(y, hm1) * a.plane_w];
+    for (int y = 0; y < 64; y++) col[y] = (uint32_t)src[(size_t)min(y, hm1) * a.plane_w + cl];
+    // magnitudes in col[], the signs straight into the sign column (the sign
+    // bit as stored: a -0.0 quantises to 0, and a zero's sign is never coded)
+    uint32_t sg_lo = 0, sg_hi = 0;
 #pragma unroll
-    for (int y0 = 0; y0 < 64; y0 += 32) {
-#pragma unroll
-        for (int y = y0; y < y0 + 32; y++) {
-            const int32_t raw = (int32_t)col[y];
-            uint32_t v, s;
-            if constexpr (REV) {
-                s = raw < 0;
-                v = (uint32_t)(raw < 0 ? -raw : raw);
-            } else {
-                const float cf = __int_as_float(raw);
-                s = cf < 0.0f;
-                v = (uint32_t)floorf(fabsf(cf) * d.inv_delta);
-            }
-            const bool in = act && y < d.h;
-            v = in ? min(v, lim) : 0u;
-            col[y] = in ? (s << 31) | v : 0u;
-            vmax = max(vmax, v);
+    for (int y = 0; y < 64; y++) {
+        const uint32_t raw = col[y];
+        uint32_t v;
+        if constexpr (REV) {
+            v = (uint32_t)abs((int32_t)raw);
+        } else {
+            v = (uint32_t)floorf(__uint_as_float(raw & 0x7FFFFFFFu) * d.inv_delta);
         }
+        if (y < 32) sg_lo |= (raw >> 31) << y;
+        else sg_hi |= (raw >> 31) << (y - 32);
+        v = min(v, lim);
+        col[y] = v;
+        vmax = max(vmax, v);
     }
+    const uint64_t hmask = d.h >= 64 ? ~0ull : ((1ull << d.h) - 1ull);
+    const uint64_t valid = act ? hmask : 0ull;  // rows < h of columns < w
+    const uint64_t sgcol = (((uint64_t)sg_hi << 32) | sg_lo) & valid;
     if (keep_sm) {
 #pragma unroll
         for (int y = 0; y < 64; y++)
-            if (y < d.h) sm[y * 64] = (int32_t)col[y];
+            if (y < d.h) sm[y * 64] = act ? (int32_t)(col[y] | (uint32_t)((sgcol >> y) & 1u) << 31) : 0;
     }
     // the magnitude bits of the block = those of the OR of its magnitudes
     // (a DPP reduction; uniform: P and the plane loop stay scalar)
@@ -872,18 +872,7 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     uint64_t *BT = a.bp + d.bp_off;
     uint64_t *ST = BT + (size_t)d.Mb * 64;
     uint64_t *SGT = BT + (size_t)2 * d.Mb * 64;
-    {
-        uint32_t t_lo = 0, t_hi = 0;
-#pragma unroll
-        for (int y = 0; y < 32; y++) {
-            t_lo |= (col[y] >> 31) << y;
-            t_hi |= (col[y + 32] >> 31) << y;
-        }
-        SGT[lane] = ((uint64_t)t_hi << 32) | t_lo;
-    }
-    // magnitudes only from here on
-#pragma unroll
-    for (int y = 0; y < 64; y++) col[y] &= 0x7FFFFFFFu;
+    SGT[lane] = sgcol;
     // every plane's column mask, kept in LDS for the distortion sums below.
     // Four planes at a time: a row's 4 bits are spread to the 4 bytes of a
     // word by one multiply (nib * 0x204081 & 0x01010101), so G[g] collects
@@ -908,14 +897,13 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
             const uint32_t sel = (uint32_t)k | ((uint32_t)(k + 4) << 8) | 0x0C0C0000u;
             const uint32_t lo = __builtin_amdgcn_perm(G[1], G[0], sel) | (__builtin_amdgcn_perm(G[3], G[2], sel) << 16);
             const uint32_t hi = __builtin_amdgcn_perm(G[5], G[4], sel) | (__builtin_amdgcn_perm(G[7], G[6], sel) << 16);
-            const uint64_t m = ((uint64_t)hi << 32) | lo;
+            const uint64_t m = (((uint64_t)hi << 32) | lo) & valid;
             planes[p * 64 + lane] = m;
             BT[(size_t)p * 64 + lane] = m;
         }
     }
     constexpr bool lossless = REV;
     constexpr int dd = lossless ? 0 : 1;  // reconstruction offset, half-units
-    const uint64_t hmask = d.h >= 64 ? ~0ull : ((1ull << d.h) - 1ull);
     const bool wcol = lane < d.w;
     uint64_t colS = 0;       // S[p+1] of this column
     uint32_t cnt_above = 0;  // |S[p+1]| over the block
@@ -2005,7 +1993,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<uint8_t>(pmin, nb, err)) return false;
     if (!ensure<unsigned long long>(hist, kSlopeBins, err)) return false;
     if (!ensure<int>(kcut, 1, err)) return false;
-    if (!ensure<uint8_t>(t1out, plan.out_bytes, err)) return false;
+    if (!ensure<uint8_t>(t1out, plan.out_bytes + 64, err)) return false;  // + k_t2_copy's dword over-read
     if (!ensure<int32_t>(rates, (size_t)nb * kMaxPasses, err)) return false;
     if (!ensure<int64_t>(dists, (size_t)nb * kMaxPasses, err)) return false;
     if (!ensure<uint8_t>(npasses, nb, err)) return false;

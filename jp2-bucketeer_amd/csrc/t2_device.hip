@@ -932,29 +932,44 @@ __global__ void __launch_bounds__(64) k_t2_tp_emit(T2Args a) {
 // code-block bytes into the packet bodies: one wave per block, its layer
 // pieces in turn; bytes move in 16-byte vector loads/stores where source and
 // destination are both aligned, else one byte per lane
+// A wave per block: lanes 0..L-1 read the layers' segment bounds and body
+// offsets at once, then each layer's bytes go over as dwords aligned to the
+// destination, each built from two source dwords by one v_alignbyte (the
+// source reads up to 3 bytes past a segment: t1out carries 64 bytes of slack).
 __global__ void __launch_bounds__(256) k_t2_copy(T2Args a, int nblocks, const uint8_t *t1out) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (b >= nblocks) return;
     const int L = a.L;
-    const uint8_t *nb = a.nl + (size_t)b * L;
-    const int32_t *lr = a.lrate + (size_t)b * L;
-    const uint8_t *src0 = t1out + a.blocks[b].out_off;
-    for (int l = 0; l < L; l++) {
-        if (nb[l] <= (l ? nb[l - 1] : 0)) continue;
-        const int r0 = l ? lr[l - 1] : 0, n = lr[l] - r0;
-        const uint8_t *s = src0 + r0;
-        uint8_t *d = a.out + a.blkdst[(size_t)b * L + l];
-        const int head = (int)((16 - ((uintptr_t)d & 15)) & 15);
-        if ((((uintptr_t)s ^ (uintptr_t)d) & 15) == 0 && n >= head + 16) {
-            if (lane < head) d[lane] = s[lane];
-            const int nv = (n - head) >> 4;
-            const uint4 *sv = (const uint4 *)(s + head);
-            uint4 *dv = (uint4 *)(d + head);
-            for (int i = lane; i < nv; i += 64) dv[i] = sv[i];
-            for (int i = head + (nv << 4) + lane; i < n; i += 64) d[i] = s[i];
-        } else {
-            for (int i = lane; i < n; i += 64) d[i] = s[i];
+    int r1 = 0, r0 = 0, np = 0, pp = 0;
+    uint64_t dst = 0;
+    if (lane < L) {
+        r1 = a.lrate[(size_t)b * L + lane];
+        np = a.nl[(size_t)b * L + lane];
+        if (lane) {
+            r0 = a.lrate[(size_t)b * L + lane - 1];
+            pp = a.nl[(size_t)b * L + lane - 1];
         }
+        dst = a.blkdst[(size_t)b * L + lane];
+    }
+    const uint64_t live = __ballot(lane < L && np > pp);  // layers with bytes of this block
+    const uint8_t *src0 = t1out + a.blocks[b].out_off;
+    for (uint64_t m = live; m; m &= m - 1) {
+        const int l = __builtin_ctzll(m);
+        const int s0 = __builtin_amdgcn_readlane(r0, l);
+        const int n = __builtin_amdgcn_readlane(r1, l) - s0;
+        const uint8_t *s = src0 + s0;
+        uint8_t *d = a.out + (((uint64_t)__builtin_amdgcn_readlane((uint32_t)(dst >> 32), l) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((uint32_t)dst, l));
+        const int head = min(n, (int)((0u - (uint32_t)(uintptr_t)d) & 3u));
+        if (lane < head) d[lane] = s[lane];
+        const uint8_t *s4 = s + head;
+        uint32_t *d4 = (uint32_t *)(d + head);
+        const int nw = (n - head) >> 2;
+        const uint32_t sh = (uint32_t)(uintptr_t)s4 & 3u;
+        const uint32_t *sa = (const uint32_t *)(s4 - sh);
+        for (int i = lane; i < nw; i += 64) d4[i] = __builtin_amdgcn_alignbyte(sa[i + 1], sa[i], sh);
+        const int t0 = head + 4 * nw;
+        if (lane < n - t0) d[t0 + lane] = s[t0 + lane];
     }
 }
 
