@@ -196,7 +196,7 @@ __device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, u
 // Items are taken in a grid-stride loop (the grid is sized to the chip, not
 // to the plan's item bound).
 // --------------------------------------------------------------------------
-constexpr int kRingBytes = 2048;
+constexpr int kRingBytes = 4096;  // a stripe pair adds <= 1536 bytes; drains every KiB
 constexpr int kRingGuard = 4;     // dwords past the ring: a lane's <= 4 dwords never wrap
 constexpr int kRingWords = kRingBytes / 4 + kRingGuard;
 constexpr int kCm3Blocks = 4096;  // workgroups (2 waves each) at most
@@ -216,28 +216,16 @@ struct Ring {
     int pos, fl;
 };
 
-// Place this lane's n bytes (o0, o1, o2 little-endian; NW = the dwords they
-// can span at any alignment: 2 for <= 4 bytes, 3 for <= 8, 4 for <= 12) at
-// pos + its prefix; returns the wave's total.  The lane's dwords are OR-ed
-// at one base address with constant offsets: dwords past the ring's end land
-// in its guard, which ring_drain folds back to the ring's start.
+// OR this lane's n bytes (o0, o1, o2 little-endian; NW = the dwords they can
+// span at any alignment: 2 for <= 4 bytes, 3 for <= 8, 4 for <= 12) into the
+// ring at byte `at`: one base address, constant offsets (dwords past the
+// ring's end land in its guard, which ring_drain folds back to its start),
+// each dword a funnel shift of (o_k : o_k-1) by one v_perm.
 template <int NW>
-__device__ __forceinline__ int ring_put(Ring &g, uint32_t o0, uint32_t o1, uint32_t o2, uint32_t n, int lane) {
-    // inclusive scan over the wave: DPP row shifts 1, 2, 4, 8, then lane 15
-    // into 16..31 / 47 into 48..63 and lane 31 into 32..63
-    int v = (int)n;
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
-    const int total = __builtin_amdgcn_readlane(v, 63);
-    const uint32_t at = (uint32_t)g.pos + (uint32_t)v - n;
-    // the bytes shifted up by t = at & 3: dword k = bytes of (o_k : o_{k-1})
-    // funnel-shifted, one v_perm each (selector byte j = 4 + j - t)
+__device__ __forceinline__ void ring_or(const Ring &g, uint32_t at, uint32_t o0, uint32_t o1, uint32_t o2,
+                                        uint32_t n) {
     const uint32_t t = at & 3u;
-    const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, t, 0u);  // t in every byte
+    const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, t, 0u);  // byte j: 4 + j - t
     uint32_t *q = g.r + ((at >> 2) & (uint32_t)(kRingBytes / 4 - 1));
     if (n) {
         atomicOr(q, o0 << (8u * t));
@@ -245,14 +233,37 @@ __device__ __forceinline__ int ring_put(Ring &g, uint32_t o0, uint32_t o1, uint3
         if (NW >= 3) atomicOr(q + 2, __builtin_amdgcn_perm(o2, o1, sel));
         if (NW >= 4) atomicOr(q + 3, __builtin_amdgcn_perm(0u, o2, sel));
     }
-    return total;
+}
+
+// Two consecutive stripes' bytes (A then B, each in column order) at pos:
+// ONE wave scan of both counts packed in a dword (<= 768 each), so a stripe
+// pair costs one DPP scan; advances pos.
+template <int NW>
+__device__ __forceinline__ void ring_put2(Ring &g, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t na, uint32_t b0,
+                                          uint32_t b1, uint32_t b2, uint32_t nb) {
+    // inclusive scan over the wave: DPP row shifts 1, 2, 4, 8, then lane 15
+    // into 16..31 / 47 into 48..63 and lane 31 into 32..63
+    const uint32_t n = na | (nb << 16);
+    int v = (int)n;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(v, 63);
+    const uint32_t ex = (uint32_t)v - n;  // exclusive prefixes, packed
+    const uint32_t ta = tot & 0xFFFFu;
+    ring_or<NW>(g, (uint32_t)g.pos + (ex & 0xFFFFu), a0, a1, a2, na);
+    ring_or<NW>(g, (uint32_t)g.pos + ta + (ex >> 16), b0, b1, b2, nb);
+    g.pos += (int)(ta + (tot >> 16));
 }
 
 // Store ring bytes [fl, upto) (upto a multiple of 16) and zero them; the
 // guard's dwords (bytes that ran past the ring's end) are first OR-ed into
-// the ring's first dwords.  (Safe: pending bytes stay below 1792 < the ring,
-// so the ring's first dwords of the previous lap were stored and zeroed
-// before any lane reached its end again.)
+// the ring's first dwords.  (Safe: pending bytes stay below 2560, well inside
+// the ring, so the ring's first dwords of the previous lap were stored and
+// zeroed before any lane reached its end again.)
 __device__ __forceinline__ void ring_drain(Ring &g, int upto, int lane) {
     if (lane < kRingGuard) {
         const uint32_t gv = g.r[kRingBytes / 4 + lane];
@@ -271,8 +282,8 @@ __device__ __forceinline__ void ring_drain(Ring &g, int upto, int lane) {
     g.fl = __builtin_amdgcn_readfirstlane(upto);
 }
 
-// After a stripe: whole KiBs leave the ring (a stripe adds <= 768 bytes, so
-// at most 1792 are pending).
+// After a stripe pair: whole KiBs leave the ring (a pair adds <= 1536 bytes,
+// so at most 2560 of the ring's 4096 are pending).
 __device__ __forceinline__ void ring_step(Ring &g, int lane) {
     // (wave-uniform: a scalar branch)
     if (__builtin_amdgcn_readfirstlane(g.pos - g.fl) >= 1024) ring_drain(g, g.fl + 1024, lane);
@@ -298,11 +309,80 @@ __device__ __forceinline__ Half half_of(int hf, uint64_t mem, uint64_t bb, const
                 (uint32_t)(sc.b2 >> sh), (uint32_t)(xs >> sh), (uint32_t)(x >> sh)};
 }
 // the four rows' zero-coding bytes and sign bytes of a stripe
+// (bit k of each byte: a 24-bit multiply by 0x204081 << k for k <= 2, whose
+// constant still fits 24 bits -- no shift of the nibble -- else spread4s)
+__device__ __forceinline__ uint32_t spread_or(uint32_t w, int sh, int k, uint32_t acc) {
+    const uint32_t nib = nibw(w, sh);
+    if (k <= 2) return (__umul24(nib, 0x00204081u << k) & (0x01010101u << k)) | acc;
+    return spread4s(nib, k) | acc;  // (nib << k) * 0x204081: no 32-bit multiply
+}
 __device__ __forceinline__ void zc_sg_bytes(const Half &m, int sh, uint32_t &zc, uint32_t &sg) {
-    zc = spread4s(nibw(m.bb, sh), 0) | spread4s(nibw(m.z0, sh), 1) | spread4s(nibw(m.z1, sh), 2) |
-         spread4s(nibw(m.z2, sh), 3) | spread4s(nibw(m.z3, sh), 4);
-    sg = 0x10101010u | spread4s(nibw(m.xs, sh), 0) | spread4s(nibw(m.c0, sh), 1) | spread4s(nibw(m.c1, sh), 2) |
-         spread4s(nibw(m.c2, sh), 3);
+    zc = spread_or(m.bb, sh, 0, 0u);
+    zc = spread_or(m.z0, sh, 1, zc);
+    zc = spread_or(m.z1, sh, 2, zc);
+    zc = spread_or(m.z2, sh, 3, zc);
+    zc = spread_or(m.z3, sh, 4, zc);
+    sg = spread_or(m.xs, sh, 0, 0x10101010u);
+    sg = spread_or(m.c0, sh, 1, sg);
+    sg = spread_or(m.c1, sh, 2, sg);
+    sg = spread_or(m.c2, sh, 3, sg);
+}
+
+// One stripe's decision bytes of each pass (sh = its nibble in the half):
+// members in scan order, each its zero-coding byte then (CUP/SPP, when its
+// bit is 1) its sign byte; n bytes.
+__device__ __forceinline__ void spp_stripe(const Half &m, int sh, const uint2 *lut, uint32_t &o0, uint32_t &o1,
+                                           uint32_t &n) {
+    const uint32_t mem = nibw(m.mem, sh);
+    uint32_t zc, sg;
+    zc_sg_bytes(m, sh, zc, sg);
+    const uint32_t K = mem | ((mem & nibw(m.bb, sh)) << 4);
+    const uint2 sel = lut[K];
+    o0 = __builtin_amdgcn_perm(sg, zc, sel.x);
+    o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
+    n = (uint32_t)__popc(K);
+}
+// ctx 14 (first refinement), 15 (... with a significant neighbour), 16
+// (later refinements): bytes 0x1C, 0x1E, 0x20 -- 0x20 - 4 f per byte (f =
+// first refinement, 0 / 1), no borrow across bytes; the neighbour flag (a
+// subset of f) in bit 1, the refinement bit in bit 0
+__device__ __forceinline__ void mrp_stripe(uint32_t wm, uint32_t wb, uint32_t wf, uint32_t wa, int sh,
+                                           const uint2 *lut, uint32_t &o0, uint32_t &n) {
+    const uint32_t mem = nibw(wm, sh);
+    const uint32_t f = spread4(nibw(wf, sh));
+    const uint32_t mr = (0x20202020u - (f << 2)) | spread_or(wa, sh, 1, spread4(nibw(wb, sh)));
+    o0 = __builtin_amdgcn_perm(0u, mr, lut[mem].x);
+    n = (uint32_t)__popc(mem);
+}
+__device__ __forceinline__ void cup_stripe(const Half &m, int sh, const uint2 *lut, uint32_t &o0, uint32_t &o1,
+                                           uint32_t &o2, uint32_t &n) {
+    const uint32_t mem = nibw(m.mem, sh);
+    uint32_t zc, sg;
+    zc_sg_bytes(m, sh, zc, sg);
+    const uint32_t bb = nibw(m.bb, sh);
+    // four members, none with a significant neighbour (mem == 0xF implies
+    // the stripe's four rows lie inside the block)
+    const bool rl = mem == 0xFu && nibw(m.x, sh) == 0u;
+    const uint32_t r = __builtin_ctz(bb | 16u);
+    const uint32_t mr = rl ? (0xEu << r) & 0xFu : mem;  // samples coded normally
+    const uint32_t K = mr | ((mr & bb) << 4);
+    const uint2 sel = lut[K];
+    o0 = __builtin_amdgcn_perm(sg, zc, sel.x);
+    o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
+    o2 = 0u;
+    n = (uint32_t)__popc(K);
+    if (rl) {  // run-length prefix: RL 0 alone, or RL 1, two UNI bits, row r's sign
+        if (bb == 0u) {
+            o0 = (uint32_t)(CX_RL << 1);
+            n = 1;
+        } else {
+            o2 = o1;
+            o1 = o0;
+            o0 = (uint32_t)((CX_RL << 1) | 1) | ((uint32_t)((CX_UNI << 1) | (r >> 1)) << 8) |
+                 ((uint32_t)((CX_UNI << 1) | (r & 1u)) << 16) | (((sg >> (8 * r)) & 0xFFu) << 24);
+            n += 4;
+        }
+    }
 }
 
 // One bit-plane p (depth k = P-1-p) of block b: the three passes' decision
@@ -345,16 +425,15 @@ __device__ __forceinline__ uint32_t cm_plane(const T1CmArgs &a, Ring &g, const u
             const Sc4 sc = sc_masks(nb.L, LSG, nb.R, RSG, nb.U, SG << 1, nb.D, SG >> 1);
             for (int hf = 0; hf * 8 < nstripes; hf++) {
                 const Half m = half_of(hf, memS, B, z, sc, SG ^ sc.xr, 0);
-                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                // stripe pairs (A, B = A + 1; B past the block: no members)
+                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4 += 2) {
                     const int sh = s4 * 4;
-                    const uint32_t mem = nibw(m.mem, sh);
-                    if (!__any(mem)) continue;
-                    uint32_t zc, sg;
-                    zc_sg_bytes(m, sh, zc, sg);
-                    const uint32_t K = mem | ((mem & nibw(m.bb, sh)) << 4);
-                    const uint2 sel = lut[K];
-                    const uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
-                    g.pos += ring_put<3>(g, o0, o1, 0u, (uint32_t)__popc(K), lane);
+                    const bool hb = hf * 8 + s4 + 1 < nstripes;
+                    if (!__any(nibw(m.mem, sh) | (hb ? nibw(m.mem, sh + 4) : 0u))) continue;
+                    uint32_t a0, a1, ca, b0 = 0, b1 = 0, cb = 0;
+                    spp_stripe(m, sh, lut, a0, a1, ca);
+                    if (hb) spp_stripe(m, sh + 4, lut, b0, b1, cb);
+                    ring_put2<3>(g, a0, a1, 0u, ca, b0, b1, 0u, cb);
                     ring_step(g, lane);
                 }
             }
@@ -371,17 +450,14 @@ __device__ __forceinline__ uint32_t cm_plane(const T1CmArgs &a, Ring &g, const u
                 const int hs = hf * 32;
                 const uint32_t wm = (uint32_t)(memM >> hs), wb = (uint32_t)(B >> hs), wf = (uint32_t)(fr >> hs),
                                wa = (uint32_t)(fa >> hs);
-                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+                for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4 += 2) {
                     const int sh = s4 * 4;
-                    const uint32_t mem = nibw(wm, sh);
-                    if (!__any(mem)) continue;
-                    // ctx 14 (first refinement), 15 (... with a significant
-                    // neighbour), 16 (later refinements): bytes 0x1C, 0x1E, 0x20
-                    const uint32_t f = spread4(nibw(wf, sh));
-                    const uint32_t mr = spread4(nibw(wb, sh)) | (f * 0x1Cu) | (spread4(nibw(wa, sh)) << 1) |
-                                        ((0x01010101u ^ f) << 5);
-                    const uint32_t o0 = __builtin_amdgcn_perm(0u, mr, lut[mem].x);
-                    g.pos += ring_put<2>(g, o0, 0u, 0u, (uint32_t)__popc(mem), lane);
+                    const bool hb = hf * 8 + s4 + 1 < nstripes;
+                    if (!__any(nibw(wm, sh) | (hb ? nibw(wm, sh + 4) : 0u))) continue;
+                    uint32_t a0, ca, b0 = 0, cb = 0;
+                    mrp_stripe(wm, wb, wf, wa, sh, lut, a0, ca);
+                    if (hb) mrp_stripe(wm, wb, wf, wa, sh + 4, lut, b0, cb);
+                    ring_put2<2>(g, a0, 0u, 0u, ca, b0, 0u, 0u, cb);
                     ring_step(g, lane);
                 }
             }
@@ -405,36 +481,14 @@ __device__ __forceinline__ uint32_t cm_plane(const T1CmArgs &a, Ring &g, const u
         const uint64_t blk = side | ((above << 1) & kStripeTop) | ((below >> 1) & kStripeBot);
         for (int hf = 0; hf * 8 < nstripes; hf++) {
             const Half m = half_of(hf, memC, B, z, sc, SG ^ sc.xr, blk);
-            for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4++) {
+            for (int s4 = 0; s4 < 8 && hf * 8 + s4 < nstripes; s4 += 2) {
                 const int sh = s4 * 4;
-                const uint32_t mem = nibw(m.mem, sh);
-                if (!__any(mem)) continue;
-                uint32_t zc, sg;
-                zc_sg_bytes(m, sh, zc, sg);
-                const uint32_t bb = nibw(m.bb, sh);
-                // four members, none with a significant neighbour (mem ==
-                // 0xF implies the stripe's four rows lie inside the block)
-                const bool rl = mem == 0xFu && nibw(m.x, sh) == 0u;
-                const uint32_t r = __builtin_ctz(bb | 16u);
-                const uint32_t mr = rl ? (0xEu << r) & 0xFu : mem;  // samples coded normally
-                const uint32_t K = mr | ((mr & bb) << 4);
-                const uint2 sel = lut[K];
-                uint32_t o0 = __builtin_amdgcn_perm(sg, zc, sel.x), o1 = __builtin_amdgcn_perm(sg, zc, sel.y);
-                uint32_t o2 = 0u;
-                uint32_t n = (uint32_t)__popc(K);
-                if (rl) {  // run-length prefix: RL 0 alone, or RL 1, two UNI bits, row r's sign
-                    if (bb == 0u) {
-                        o0 = (uint32_t)(CX_RL << 1);
-                        n = 1;
-                    } else {
-                        o2 = o1;
-                        o1 = o0;
-                        o0 = (uint32_t)((CX_RL << 1) | 1) | ((uint32_t)((CX_UNI << 1) | (r >> 1)) << 8) |
-                             ((uint32_t)((CX_UNI << 1) | (r & 1u)) << 16) | (((sg >> (8 * r)) & 0xFFu) << 24);
-                        n += 4;
-                    }
-                }
-                g.pos += ring_put<4>(g, o0, o1, o2, n, lane);
+                const bool hb = hf * 8 + s4 + 1 < nstripes;
+                if (!__any(nibw(m.mem, sh) | (hb ? nibw(m.mem, sh + 4) : 0u))) continue;
+                uint32_t a0, a1, a2, ca, b0 = 0, b1 = 0, b2 = 0, cb = 0;
+                cup_stripe(m, sh, lut, a0, a1, a2, ca);
+                if (hb) cup_stripe(m, sh + 4, lut, b0, b1, b2, cb);
+                ring_put2<4>(g, a0, a1, a2, ca, b0, b1, b2, cb);
                 ring_step(g, lane);
             }
         }
