@@ -25,14 +25,8 @@ import time
 
 import numpy as np
 
-# device -> pinned host copies on the DMA engines: without it the runtime
-# copies with blit kernels, which under load wait for CUs like any kernel
-# (the code-stream D2H took 1.3 ms per image in the bench's kernel trace,
-# 0.13 ms alone): +5-6 % C2 (tests/tools/sdma_ab.sh, profiles/r03/ab/sdma.txt).
-# Read when the HSA runtime starts, so it is set before anything can start
-# it; the deployment sets it the same way.  (Under
-# rocprofv3 the runtime starts before Python does: traces show blit copies.)
-os.environ.setdefault("HSA_ENABLE_SDMA", "1")
+# (HSA_ENABLE_SDMA is not set: the runtime copies device -> pinned host with
+# its blit kernel whatever it says -- profiles/r04/sdma_probe.txt)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jp2-bucketeer_amd"))

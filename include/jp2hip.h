@@ -149,10 +149,9 @@ int jp2hip_device_ordinals(int32_t *ordinals, int32_t max);
 
 /* "" when the process environment suits the contexts alive in it, else
  * what to change: GPU_MAX_HW_QUEUES below the live context count (contexts
- * sharing a hardware queue run their kernels one after another) or
- * HSA_ENABLE_SDMA not 1 (the code-stream download becomes a blit kernel
- * that waits for CUs under load).  Both must be set before the library
- * loads; a converter logs this once after creating its contexts. */
+ * sharing a hardware queue run their kernels one after another).  It must
+ * be set before the library loads; a converter logs this once after
+ * creating its contexts. */
 const char *jp2hip_env_check(void);
 
 /* Fill the Bucketeer recipe for JP2HIP_LOSSY / JP2HIP_LOSSLESS. */

@@ -1134,10 +1134,6 @@ const char *jp2hip_env_check(void) {
         msg += "GPU_MAX_HW_QUEUES=" + std::to_string(queues) + " is below the " + std::to_string(live) +
                " contexts of this process (contexts sharing a hardware queue run their kernels one after "
                "another; set it to contexts per GPU + 4 before the library loads); ";
-    const char *sd = std::getenv("HSA_ENABLE_SDMA");
-    if (!sd || std::strcmp(sd, "1") != 0)
-        msg += "HSA_ENABLE_SDMA is not 1 (the code-stream download then runs as a blit kernel that "
-               "waits for CUs under load); ";
     if (!msg.empty()) msg.resize(msg.size() - 2);
     return msg.c_str();
 }

@@ -159,7 +159,7 @@ def device_ordinals() -> list[int]:
 
 def env_check() -> str:
     """"" or what the process environment should change for the contexts
-    alive in it (jp2hip_env_check: GPU_MAX_HW_QUEUES, HSA_ENABLE_SDMA)."""
+    alive in it (jp2hip_env_check: GPU_MAX_HW_QUEUES)."""
     return lib().jp2hip_env_check().decode()
 
 

@@ -130,8 +130,6 @@ class BatchQueue:
         # one HW queue per context (+4 for the runtime); only takes effect if
         # nothing in this process has initialised HIP yet
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, (contexts or 12) + 4))))
-        # code-stream copies on the DMA engines, not blit kernels
-        os.environ.setdefault("HSA_ENABLE_SDMA", "1")
         L = _bind()
         cfg = BatchConfig(device, contexts, reader_threads, uploader_threads, host_threads,
                           1 if delete_after_upload else 0, 1 if write_output else 0, 0)

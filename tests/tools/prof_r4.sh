@@ -13,3 +13,5 @@ o=gpurun_out/${1:-prof4}
 mkdir -p $o
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $o/kt -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-extras > $o/bench_rocprof.json 2> $o/bench_rocprof.err || exit 1
 python tests/tools/mq_agreement.py $o/bench_rocprof.json $o/kt > $o/mq_agreement.txt 2>&1 || exit 1
+python tests/tools/stream_gaps.py $o/kt/run_kernel_trace.csv > $o/stream_gaps.txt 2>&1 || exit 1
+python tests/tools/kstats.py $o/kt/run_kernel_stats.csv > $o/kstats.txt 2>&1 || true
