@@ -370,8 +370,8 @@ __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, Row
     }
 }
 
-template <bool REV, bool INGEST, int RB>
-__global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
+template <bool REV, bool INGEST, int RB, int NT = kDwtThreads>
+__global__ void __launch_bounds__(NT) k_dwt_band(DwtBandArgs a) {
     extern __shared__ int32_t lds[];
     constexpr int NR = RB + 2 * kDwtHalo;
     const int tc = blockIdx.y;
@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
     const int tid = threadIdx.x;
     const int ld = lds_row_stride(W);
     // ---- vertical: one column per thread, in registers ----
-    for (int x = tid; x < W; x += kDwtThreads) {
+    for (int x = tid; x < W; x += NT) {
         int32_t v[NR];
         // every row load issues before any is used: rows outside the band
         // read a clamped (valid) row and are zeroed after (a load under a
@@ -422,8 +422,8 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_band(DwtBandArgs a) {
         lrow = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : hrow;
         return true;
     };
-    if (W > 1 && (W & 15) == 0) hlift_seg<REV, RB, true>(lds, W, ld, rows);
-    else hlift_seg<REV, RB, false>(lds, W, ld, rows);
+    if (W > 1 && (W & 15) == 0) hlift_seg<REV, RB, true, NT>(lds, W, ld, rows);
+    else hlift_seg<REV, RB, false, NT>(lds, W, ld, rows);
 }
 
 // Level 1 with ingest, every component of a tile at once: a workgroup owns
@@ -838,19 +838,32 @@ __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
     }
 }
 
-template <bool REV, bool INGEST, int RB>
+template <bool REV, bool INGEST, int RB, int NT>
 static void launch_band(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
     static bool wide = false;  // opt in to > 64 KiB dynamic LDS once per instance
     if (lds > (size_t)kDwtLdsWords * 4 && !wide) {
-        (void)hipFuncSetAttribute((const void *)k_dwt_band<REV, INGEST, RB>,
+        (void)hipFuncSetAttribute((const void *)k_dwt_band<REV, INGEST, RB, NT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kDwtLdsWordsWide * 4);
         wide = true;
     }
-    hipLaunchKernelGGL((k_dwt_band<REV, INGEST, RB>), g, dim3(kDwtThreads), lds, st, a);
+    hipLaunchKernelGGL((k_dwt_band<REV, INGEST, RB, NT>), g, dim3(NT), lds, st, a);
 }
+#ifndef JP2HIP_BAND_RB
+#define JP2HIP_BAND_RB 16
+#endif
+#ifndef JP2HIP_BAND_NARROW
+#define JP2HIP_BAND_NARROW 128  // levels at most this wide: workgroups of this many threads
+#endif
+constexpr int kBandRb = JP2HIP_BAND_RB;
+// (a level of <= 128 columns in 128-thread workgroups: with 256 threads half
+// of them had no column)
 template <bool REV, bool INGEST>
-static void launch_band_rb(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
-    launch_band<REV, INGEST, 8>(g, lds, st, a);
+static void launch_band_rb(int maxW, dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
+    if (!INGEST && JP2HIP_BAND_NARROW < kDwtThreads && maxW <= JP2HIP_BAND_NARROW)
+        launch_band<REV, INGEST, kBandRb, (JP2HIP_BAND_NARROW < kDwtThreads ? JP2HIP_BAND_NARROW : kDwtThreads)>(
+            g, lds, st, a);
+    else
+        launch_band<REV, INGEST, kBandRb, kDwtThreads>(g, lds, st, a);
 }
 
 template <bool REV, int NC>
@@ -936,7 +949,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             else hipLaunchKernelGGL(k_dwt_tail<false>, dim3(p.ntc), dim3(kTailThreads), 0, st, t);
             return hipGetLastError() == hipSuccess;
         }
-        const int R = 8;  // kept rows per workgroup (more workgroups in flight; 16 / 32 measured slower)
+        const int R = kBandRb;  // kept rows per workgroup (16: 8 took 2 x 40 us for levels 2-3, 16 70 us, profiles/r04/ab_dwt_band.txt)
         a.level = lv;
         a.R = R;
         a.src = scratch[(lv - 1) & 1];
@@ -965,11 +978,11 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             if (p.reversible) launch_l1<true>(p.nc, g1, lds1, st, a);
             else launch_l1<false>(p.nc, g1, lds1, st, a);
         } else if (lv == 1) {
-            if (p.reversible) launch_band_rb<true, true>(g, lds, st, a);
-            else launch_band_rb<false, true>(g, lds, st, a);
+            if (p.reversible) launch_band_rb<true, true>(maxW, g, lds, st, a);
+            else launch_band_rb<false, true>(maxW, g, lds, st, a);
         } else {
-            if (p.reversible) launch_band_rb<true, false>(g, lds, st, a);
-            else launch_band_rb<false, false>(g, lds, st, a);
+            if (p.reversible) launch_band_rb<true, false>(maxW, g, lds, st, a);
+            else launch_band_rb<false, false>(maxW, g, lds, st, a);
         }
         if (hipGetLastError() != hipSuccess) return false;
     }

@@ -15,6 +15,9 @@
 // written in the same order as the oracle so the lossy path is bit-exact.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <thread>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -1837,10 +1840,22 @@ bool GpuEncoder::h2d(void *dst, const void *src, size_t bytes, std::string &err)
 // Host waits for this context's stream by sleeping on an event rather than
 // spinning: with many images in flight the spinning callers would take the
 // cores the tier-2 threads need.
+#ifndef JP2HIP_WAIT_POLL_US
+#define JP2HIP_WAIT_POLL_US 0  // A/B builds: poll the event every N us instead of sleeping on it
+#endif
 bool GpuEncoder::host_wait(std::string &err) {
     waits++;
     HIPCHECK(hipEventRecord(sync_ev, stream));
+#if JP2HIP_WAIT_POLL_US > 0
+    for (;;) {
+        const hipError_t q = hipEventQuery(sync_ev);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIPCHECK(q);
+        std::this_thread::sleep_for(std::chrono::microseconds(JP2HIP_WAIT_POLL_US));
+    }
+#else
     HIPCHECK(hipEventSynchronize(sync_ev));
+#endif
     return true;
 }
 

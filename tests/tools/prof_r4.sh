@@ -8,7 +8,7 @@
 # rocprofv3's average over the same launches.
 set -o pipefail
 export TMPDIR=/tmp
-export GPU_MAX_HW_QUEUES=20 HSA_ENABLE_SDMA=1 JP2HIP_KEEP_HW_QUEUES=1
+export GPU_MAX_HW_QUEUES=20 JP2HIP_KEEP_HW_QUEUES=1
 o=gpurun_out/${1:-prof4}
 mkdir -p $o
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $o/kt -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-extras > $o/bench_rocprof.json 2> $o/bench_rocprof.err || exit 1
