@@ -549,6 +549,9 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
 #define JP2HIP_STREAM_BAND 64
 #endif
 constexpr int kStreamBand = JP2HIP_STREAM_BAND;
+#ifndef JP2HIP_L1S_R
+#define JP2HIP_L1S_R 4  // rows per horizontal batch (4 or 8)
+#endif
 template <bool REV, int NC, int CPT, int RB, bool ALIGNED>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     extern __shared__ int32_t lds[];
@@ -968,7 +971,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
         if (lv == 1 && lds1 <= (size_t)kDwtLdsWordsWide * 4 && maxW <= 4 * kDwtThreads) {
             // streaming vertical pass (k_dwt_l1s), bands of kStreamBand rows,
             // horizontal batches of 4 rows
-            a.R = 4;
+            a.R = JP2HIP_L1S_R;
             const size_t lds_s = ((size_t)p.nc * a.R * lds_row_stride(maxW) + kPadL + kPadR) * 4;
             dim3 g1((maxH + kStreamBand - 1) / kStreamBand, p.ntc / p.nc);
             if (p.reversible) launch_l1s<true>(p.nc, cpt, g1, lds_s, st, a);
