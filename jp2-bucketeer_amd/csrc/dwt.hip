@@ -549,6 +549,9 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
 #define JP2HIP_STREAM_BAND 64
 #endif
 constexpr int kStreamBand = JP2HIP_STREAM_BAND;
+#ifndef JP2HIP_L1S_INTERIOR
+#define JP2HIP_L1S_INTERIOR 0  // A/B: the select-free interior lifting path
+#endif
 #ifndef JP2HIP_L1S_R
 #define JP2HIP_L1S_R 4  // rows per horizontal batch (4 or 8)
 #endif
@@ -665,7 +668,30 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         if (m < e) place(1, NWIN - 1);
         if (m + 1 < e) fetch(0);
         if (m + 2 < e) fetch(1);
-        if (H > 1) {
+        // interior iterations (every step's rows and neighbours inside the
+        // streamed rows and the signal, none at row 0): fixed neighbour slots,
+        // no per-value selects -- the same expressions in the same order
+        if (JP2HIP_L1S_INTERIOR && H > 1 && m - NS - 1 >= s && m < e) {
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                const int ti = NWIN - 2 - k;
+#pragma unroll
+                for (int j = 0; j < CPT; j++)
+#pragma unroll
+                    for (int c = 0; c < NC; c++) {
+                        const int32_t lv = w[j][c][ti - 1], rv = w[j][c][ti + 1];
+                        if (REV) {
+                            if (k == 0) w[j][c][ti] -= (lv + rv) >> 1;
+                            else w[j][c][ti] += (lv + rv + 2) >> 2;
+                        } else {
+                            const float cf = k == 0 ? A97 : (k == 1 ? B97 : (k == 2 ? G97 : D97));
+                            float tt = __int_as_float(lv) + __int_as_float(rv);
+                            tt = cf * tt;
+                            w[j][c][ti] = __float_as_int(__int_as_float(w[j][c][ti]) + tt);
+                        }
+                    }
+            }
+        } else if (H > 1) {
 #pragma unroll
             for (int k = 0; k < NS; k++) {
                 const int tr = m - 1 - k, ti = NWIN - 2 - k;  // target row, its window slot

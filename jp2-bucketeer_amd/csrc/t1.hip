@@ -499,19 +499,20 @@ __device__ __forceinline__ uint32_t cm_plane(const T1CmArgs &a, Ring &g, const u
     // p, each gains 2^p (12 v + 6d - 9 2^p) (d = 1 lossy, 0 lossless; 4 at
     // lossless p = 0), and sum_N v = 2^p |N| + sum_{q<p} 2^q |N & B[q]|
     // from the column masks of the lower planes (dist_gain, exact)
-    int64_t nN = 0, sv = 0;
+    // (a plane whose SPP makes nothing significant skips the sums: 0)
+    int64_t dspp = 0;
     if (spp && __any(N != 0ull)) {
-        nN = __popcll(N);
-        sv = nN << p;
+        const uint32_t nl = (uint32_t)__popcll(N);
+        int64_t sv = (int64_t)nl << p;
         // (N is 0 on lanes past the block width: no lane test, so the
         // unrolled loads issue together)
 #pragma unroll 4
         for (int q = 0; q < p; q++) sv += (int64_t)__popcll(N & CT[(size_t)q * 64 + lane]) << q;
+        const int64_t nN = (int64_t)wave_sum_u32(nl);  // <= 4096
+        sv = wave_sum64(sv);
+        dspp = (lossless && p == 0) ? 4 * nN
+                                    : ((12 * sv + (6 * (lossless ? 0 : 1) - 9 * ((int64_t)1 << p)) * nN) << p);
     }
-    nN = wave_sum64(nN);
-    sv = wave_sum64(sv);
-    const int64_t dspp = (lossless && p == 0) ? 4 * nN
-                                              : ((12 * sv + (6 * (lossless ? 0 : 1) - 9 * ((int64_t)1 << p)) * nN) << p);
     if (lane == 0) {
         uint4 cnt;
         cnt.x = (uint32_t)n_spp;
