@@ -1030,8 +1030,13 @@ static int predict_and_code(encoder *E, int64_t target) {
             skipped |= b->pmin > 0;
             int cap = b->w * b->h * 8 + 256;
             if (!b->data) b->data = (uint8_t *)malloc((size_t)cap);
+            const int64_t dec0 = g_decisions;
             int np = oracle_t1_encode_planes(b->sm, b->w, b->h, b->band, lossless, b->pmin, b->data, cap,
                                              &b->len, b->rates, b->dd, &b->P);
+            if (getenv("ORACLE_BLOCK_DECISIONS")) {  /* experiments: decisions per block */
+                FILE *f = fopen(getenv("ORACLE_BLOCK_DECISIONS"), "a");
+                if (f) { fprintf(f, "%lld %d\n", (long long)(g_decisions - dec0), np); fclose(f); }
+            }
             if (np < 0) return -1;
             b->npasses = np;
             total += b->len;
