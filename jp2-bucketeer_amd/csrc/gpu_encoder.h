@@ -47,7 +47,11 @@ size_t lzw_scratch_bytes(int nstrips, uint64_t segs);
 bool launch_lzw(const UnpackArgs &u, uint64_t segs, void *scratch, hipStream_t st);
 
 // tier-1 kernels (t1.hip)
-constexpr int kOrderBuckets = 256;  // MQ lane-order buckets (decision count, 12.5 % wide)
+#ifndef JP2HIP_ORDER_SUB
+#define JP2HIP_ORDER_SUB 16  // MQ lane-order buckets per octave of decision count
+#endif
+constexpr int kOrderSub = JP2HIP_ORDER_SUB;
+constexpr int kOrderBuckets = 32 * kOrderSub;  // MQ lane-order buckets (decision count, 6.25 % wide)
 // Work lists of k_t1_cm3, filled once the coded planes are known
 // (emit_t1_items: k_plane_pmin, or k_t1_items without slope prediction):
 // list k holds the blocks with more than k coded planes (item = plane k from

@@ -52,16 +52,17 @@ constexpr int kCmWaves = 2;  // items per workgroup
 
 // MQ lane order: blocks by decreasing decision count, so the lanes of an MQ
 // wave carry similar work.  The order only groups blocks (it changes no
-// output): bucket = 8 * floor(log2(n + 1)) + the next 3 bits of n + 1 (12.5 %
-// wide), largest first; inside a bucket the order is whatever the atomics
-// give.  k_t1_cm3's last plane of a block files it (bslots[bucket][i]);
+// output): bucket = 16 * floor(log2(n + 1)) + the next 4 bits of n + 1 (6.25 %
+// wide; 8 / 3 bits before round 4: lanes idle 4.2 -> 2.6 % of the wave-steps,
+// simulated on the oracle's per-block counts of C2), largest first; inside a
+// bucket the order is whatever the atomics give.  k_t1_cm3's last plane of a block files it (bslots[bucket][i]);
 // k_t1_mq maps its lanes through the bucket fills' prefix.
-[[maybe_unused]] constexpr unsigned long long kAccMask = (1ull << 40) - 1ull;
 __device__ __forceinline__ int order_bucket(uint32_t n) {
     const uint32_t v = n + 1u;
     const int e = 31 - __clz(v);                                      // 0..31
-    const int f = e >= 3 ? (int)((v >> (e - 3)) & 7u) : (int)((v << (3 - e)) & 7u);
-    return kOrderBuckets - 1 - min(kOrderBuckets - 1, 8 * e + f);   // descending
+    constexpr int kLog = kOrderSub == 16 ? 4 : 3;                     // bits of the sub-bucket
+    const int f = e >= kLog ? (int)((v >> (e - kLog)) & (kOrderSub - 1u)) : (int)((v << (kLog - e)) & (kOrderSub - 1u));
+    return kOrderBuckets - 1 - min(kOrderBuckets - 1, kOrderSub * e + f);  // descending
 }
 
 
@@ -543,7 +544,6 @@ __device__ __forceinline__ uint2 cm_selectors(int K) {
     return make_uint2((uint32_t)sel, (uint32_t)(sel >> 32));
 }
 
-#ifndef JP2HIP_CM_ITEMS
 // k_t1_cm3, one wave per code-block: the block's coded planes top-down, in
 // order, so a plane's S[p+1] and S[p+2] are the masks the wave already holds
 // and the next plane's two masks load while this one is coded (one dependent
@@ -614,65 +614,6 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         }
     }
 }
-#else
-// k_t1_cm3 over (block, plane) items (A/B builds: -DJP2HIP_CM_ITEMS)
-__global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
-    __shared__ uint2 lut[256];
-    __shared__ uint32_t rings[kCmWaves][kRingWords];
-    __shared__ uint32_t dbase[65];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int K = threadIdx.x; K < 256; K += 64 * kCmWaves) lut[K] = cm_selectors(K);
-    for (int i = threadIdx.x; i < kCmWaves * kRingWords; i += 64 * kCmWaves) (&rings[0][0])[i] = 0u;
-    // item = (depth k, entry) of the per-depth lists (emit_t1_items): the
-    // depth bases are an exclusive scan of the list fills
-    if (threadIdx.x < 64) {
-        const uint32_t v = threadIdx.x < (unsigned)a.kmax ? a.dfill[threadIdx.x] : 0u;
-        const uint32_t inc = wave_incl_scan(v);
-        dbase[threadIdx.x + 1] = inc;
-        if (threadIdx.x == 0) dbase[0] = 0;
-    }
-    __syncthreads();
-    const int nitems = (int)dbase[a.kmax];
-    Ring g;
-    g.r = rings[wv];
-    for (int gi = blockIdx.x * kCmWaves + wv; gi < nitems; gi += gridDim.x * kCmWaves) {
-        int k = 0;  // the depth holding item gi (wave-uniform)
-        for (int step = 32; step > 0; step >>= 1)
-            if (k + step < a.kmax && dbase[k + step] <= (uint32_t)gi) k += step;
-        const int b = a.dlist[(size_t)k * a.nb + (gi - (int)dbase[k])];
-        const BlockDesc d = a.blocks[b];
-        const int P = a.P[b];
-        const int p = P - 1 - k;
-        const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
-        const bool vl = lane < w;
-        const uint64_t *CT = a.bp + d.bp_off;
-        const uint64_t Bl = CT[(size_t)p * 64 + lane];
-        const uint64_t S0l = CT[(size_t)(Mb + p) * 64 + lane];
-        const uint64_t S1l = CT[(size_t)min(Mb + p + 1, 2 * Mb) * 64 + lane];
-        const uint64_t S2l = CT[(size_t)min(Mb + p + 2, 2 * Mb) * 64 + lane];
-        const uint64_t SGl = CT[(size_t)2 * Mb * 64 + lane];
-        const uint64_t SG = vl ? SGl : 0ull;
-        g.out = a.stream + a.slot_off[b] + (size_t)k * plane_stream_cap(w, h);
-        g.pos = 0;
-        g.fl = 0;
-        const uint32_t nd = cm_plane(a, g, lut, lane, b, k, p, P, w, h, band, CT, vl ? Bl : 0ull, vl ? S0l : 0ull,
-                                     (vl && p + 1 < P) ? S1l : 0ull, (vl && p + 2 < P) ? S2l : 0ull, SG,
-                                     col_left(SG, lane), col_right(SG, lane));
-        if (lane == 0) {
-            // one atomic per plane: planes left (bits 40+) down by one,
-            // decisions up; the block's last plane knows its total and files
-            // the block in its MQ lane-order bucket
-            const unsigned long long old = atomicAdd(&a.acc[b], (unsigned long long)nd - (1ull << 40));
-            if ((old >> 40) == 1ull) {
-                const uint32_t tot = (uint32_t)(old & kAccMask) + nd;
-                const int bk = order_bucket(tot);
-                a.bslots[(size_t)bk * a.nb + atomicAdd(&a.bfill[bk], 1u)] = b;
-            }
-        }
-    }
-}
-#endif
 
 // --------------------------------------------------------------------------
 // MQ coder
@@ -1095,14 +1036,14 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
         sh.mqt[e] = (uint32_t)c_qe[i] | ((uint32_t)(2 * c_nmps[i] + mps) << 16) |
                     ((uint32_t)(2 * c_nlps[i] + (mps ^ sw)) << 23) | ((uint32_t)mps << 31);
     }
-    if (tid < 64) {  // exclusive scan of the bucket fills, 4 per lane
-        uint32_t v[4], t = 0;
+    if (tid < 64) {  // exclusive scan of the bucket fills, kOrderBuckets / 64 per lane
+        uint32_t v[kOrderBuckets / 64], t = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) t += (v[i] = a.bfill[4 * lane + i]);
+        for (int i = 0; i < kOrderBuckets / 64; i++) t += (v[i] = a.bfill[kOrderBuckets / 64 * lane + i]);
         uint32_t o = wave_incl_scan(t) - t;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            sh.bbase[4 * lane + i] = o;
+        for (int i = 0; i < kOrderBuckets / 64; i++) {
+            sh.bbase[kOrderBuckets / 64 * lane + i] = o;
             o += v[i];
         }
         if (lane == 63) sh.bbase[kOrderBuckets] = o;
@@ -1115,7 +1056,7 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
         int b = -1;
         if (gi < (int)sh.bbase[kOrderBuckets]) {
             int bk = 0;
-            for (int step = 128; step > 0; step >>= 1)
+            for (int step = kOrderBuckets / 2; step > 0; step >>= 1)
                 if (sh.bbase[bk + step] <= (uint32_t)gi) bk += step;
             b = a.bslots[(size_t)bk * a.nblocks + (gi - (int)sh.bbase[bk])];
         }
@@ -1129,11 +1070,7 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
 
 void launch_t1_cm(const T1CmArgs &a, hipStream_t st) {
     if (!a.max_items) return;
-#ifndef JP2HIP_CM_ITEMS
     const dim3 g((a.nb + kCmWaves - 1) / kCmWaves);  // a wave per block at most
-#else
-    const dim3 g((a.max_items + kCmWaves - 1) / kCmWaves);
-#endif
     hipLaunchKernelGGL(k_t1_cm3, dim3(std::min<int>((int)g.x, kCm3Blocks)), dim3(64 * kCmWaves), 0, st, a);
 }
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st) {
