@@ -544,6 +544,38 @@ __device__ __forceinline__ uint2 cm_selectors(int K) {
     return make_uint2((uint32_t)sel, (uint32_t)(sel >> 32));
 }
 
+// A block's descriptor fields k_t1_cm3 uses (wave-uniform), and its first
+// masks (the sign column, B and S of the top plane).
+struct CmBlk {
+    int b, P, c, w, h, Mb, band;
+    uint64_t bp_off, slot;
+};
+__device__ __forceinline__ CmBlk cm_blk_load(const T1CmArgs &a, int b) {
+    const BlockDesc d = a.blocks[b];
+    CmBlk k;
+    k.b = b;
+    k.P = a.P[b];
+    k.c = (int)(a.acc[b] >> 40);  // coded planes (emit_t1_items)
+    k.w = d.w;
+    k.h = d.h;
+    k.Mb = d.Mb;
+    k.band = d.band;
+    k.bp_off = d.bp_off;
+    k.slot = a.slot_off[b];
+    return k;
+}
+struct CmMasks {
+    uint64_t SG, B, S0;
+};
+__device__ __forceinline__ CmMasks cm_masks_load(const T1CmArgs &a, const CmBlk &k, int lane) {
+    const uint64_t *CT = a.bp + k.bp_off;
+    CmMasks m;
+    m.SG = CT[(size_t)2 * k.Mb * 64 + lane];
+    m.B = CT[(size_t)(k.P - 1) * 64 + lane];
+    m.S0 = CT[(size_t)(k.Mb + k.P - 1) * 64 + lane];
+    return m;
+}
+
 // k_t1_cm3, one wave per code-block: the block's coded planes top-down, in
 // order, so a plane's S[p+1] and S[p+2] are the masks the wave already holds
 // and the next plane's two masks load while this one is coded (one dependent
@@ -566,29 +598,41 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
     const int nblk = a.kmax > 0 ? (int)a.dfill[0] : 0;
     Ring g;
     g.r = rings[wv];
-    for (int bi = blockIdx.x * kCmWaves + wv; bi < nblk; bi += gridDim.x * kCmWaves) {
-        const int b = a.dlist[bi];
-        const BlockDesc d = a.blocks[b];
-        const int P = a.P[b];
-        const int c = (int)(a.acc[b] >> 40);  // coded planes (emit_t1_items)
-        const int w = d.w, h = d.h, Mb = d.Mb, band = d.band;
+    const int stride = gridDim.x * kCmWaves;
+    int bi = blockIdx.x * kCmWaves + wv;
+    if (bi >= nblk) return;  // (no barrier follows)
+    // Blocks are pipelined one ahead: during block i the wave loads block
+    // i+1's descriptor (while block i's first plane is coded) and then its
+    // first masks (at block i's end), and the work-list index of block i+2,
+    // so a block starts with nothing to wait for -- the four dependent loads
+    // (work list -> descriptor -> masks) of a block no longer sit between
+    // two blocks.
+    CmBlk cur = cm_blk_load(a, a.dlist[bi]);
+    CmMasks mk = cm_masks_load(a, cur, lane);
+    int idx_next = bi + stride < nblk ? a.dlist[bi + stride] : -1;
+    for (;;) {
+        const int b = cur.b, P = cur.P, c = cur.c, w = cur.w, h = cur.h, Mb = cur.Mb, band = cur.band;
         const bool vl = lane < w;
-        const uint64_t *CT = a.bp + d.bp_off;
-        const uint64_t SGl = CT[(size_t)2 * Mb * 64 + lane];
-        uint64_t Bl = CT[(size_t)(P - 1) * 64 + lane];
-        uint64_t S0l = CT[(size_t)(Mb + P - 1) * 64 + lane];
-        const uint64_t SG = vl ? SGl : 0ull;
+        const uint64_t *CT = a.bp + cur.bp_off;
+        uint64_t Bl = mk.B, S0l = mk.S0;
+        const uint64_t SG = vl ? mk.SG : 0ull;
         const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
         uint64_t S1 = 0, S2 = 0;
         uint32_t tot = 0;
         const uint32_t cap = plane_stream_cap(w, h);
-        uint8_t *out = a.stream + a.slot_off[b];
+        uint8_t *out = a.stream + cur.slot;
+        CmBlk nxt;
+        int idx_after = -1;
         for (int k = 0; k < c; k++) {
             const int p = P - 1 - k;
             const uint64_t B = vl ? Bl : 0ull, S0 = vl ? S0l : 0ull;
             if (k + 1 < c) {  // the next plane's masks, in flight during this one
                 Bl = CT[(size_t)(p - 1) * 64 + lane];
                 S0l = CT[(size_t)(Mb + p - 1) * 64 + lane];
+            }
+            if (k == 0 && idx_next >= 0) {  // the next block's descriptor, and the index after it
+                nxt = cm_blk_load(a, idx_next);
+                if (bi + 2 * stride < nblk) idx_after = a.dlist[bi + 2 * stride];
             }
             g.out = out + (size_t)k * cap;
             g.pos = 0;
@@ -607,11 +651,17 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
             S2 = S1;
             S1 = S0;
         }
-        if (lane == 0 && c > 0) {
+        const bool more = idx_next >= 0;
+        if (more) mk = cm_masks_load(a, nxt, lane);  // the next block's first masks
+        if (lane == 0) {
             a.acc[b] = tot;  // decisions (k_hull's tier-1 totals); no planes left
             const int bk = order_bucket(tot);
             a.bslots[(size_t)bk * a.nb + atomicAdd(&a.bfill[bk], 1u)] = b;
         }
+        if (!more) break;
+        bi += stride;
+        cur = nxt;
+        idx_next = idx_after;
     }
 }
 
