@@ -1,12 +1,13 @@
 // t1.hip -- EBCOT tier-1 (ISO/IEC 15444-1 Annex D) and the MQ coder (Annex C)
 // for gfx950, split in two kernels so the serial part is as short as possible:
 //
-//   k_t1_cm3 context modelling, one wave per (code-block, bit-plane),
-//            lane = column.  Significance lives in 64-bit column masks (bit
-//            r = row r), so the neighbourhood and context rules run
-//            bit-sliced for the whole column at once.  The
-//            state at the start of plane p is known from the bit-planes
-//            (S[p+1] = OR of planes above p), so planes are independent:
+//   k_t1_cm3 context modelling, one wave per code-block (its coded planes
+//            top-down), lane = column.  Significance lives in 64-bit column
+//            masks (bit r = row r), so the neighbourhood and context rules
+//            run bit-sliced for the whole column at once.  The state at the
+//            start of plane p is known from the bit-planes (S[p+1] = OR of
+//            planes above p), so a plane needs no state from the passes
+//            coded before it:
 //              - SPP membership is the least fixed point of the causal
 //                neighbourhood rule (iterated on the whole masks);
 //              - MRP neighbours all see the post-SPP state S[p+1] | N;
@@ -48,14 +49,15 @@ __host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
     return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
 }
 
-constexpr int kCmWaves = 2;  // items per workgroup
+constexpr int kCmWaves = 2;  // code-blocks (waves) per workgroup
 
 // MQ lane order: blocks by decreasing decision count, so the lanes of an MQ
 // wave carry similar work.  The order only groups blocks (it changes no
 // output): bucket = 16 * floor(log2(n + 1)) + the next 4 bits of n + 1 (6.25 %
 // wide; 8 / 3 bits before round 4: lanes idle 4.2 -> 2.6 % of the wave-steps,
 // simulated on the oracle's per-block counts of C2), largest first; inside a
-// bucket the order is whatever the atomics give.  k_t1_cm3's last plane of a block files it (bslots[bucket][i]);
+// bucket the order is whatever the atomics give.  k_t1_cm3 files a block at
+// its end (bslots[bucket][i]);
 // k_t1_mq maps its lanes through the bucket fills' prefix.
 __device__ __forceinline__ int order_bucket(uint32_t n) {
     const uint32_t v = n + 1u;
@@ -67,8 +69,8 @@ __device__ __forceinline__ int order_bucket(uint32_t n) {
 
 
 // --------------------------------------------------------------------------
-// Context modelling on column masks.  One wavefront per (code-block,
-// bit-plane) item, in the transposed layout: lane
+// Context modelling on column masks.  One wavefront per code-block, one
+// bit-plane at a time, in the transposed layout: lane
 // c holds column c of every mask as a 64-bit word (bit r = row r; k_quant
 // writes them), so a vertical neighbour is a bit shift inside the lane and a
 // horizontal one is the next lane.  The neighbourhood and context rules then
@@ -189,13 +191,15 @@ __device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, u
 // spread to byte lanes by one multiply (nibble * 0x204081 & 0x01010101).  The
 // member samples' bytes are compacted in scan order by two v_perm_b32 whose
 // selectors come from a 256-entry table indexed by (members | members with a
-// 1 bit << 4) -- no per-sample branch.  The wave's lanes place their <= 12
-// bytes at an exclusive prefix of the counts (DPP wave scan) in a 2 KB LDS
-// ring per wave, OR-ing whole dwords (the ring is zero where nothing has
-// been written, and a lane's bytes are zero-padded, so neighbours' partial
-// dwords merge); every full KiB leaves the ring in one 16-byte store per lane.
-// Items are taken in a grid-stride loop (the grid is sized to the chip, not
-// to the plan's item bound).
+// 1 bit << 4) -- no per-sample branch.  Two stripes at a time, the wave's
+// lanes place their <= 12 bytes per stripe at an exclusive prefix of the
+// counts (one DPP wave scan of both stripes' counts packed in a dword) in a
+// 4 KB LDS ring per wave, OR-ing whole dwords (the ring is zero where nothing
+// has been written, and a lane's bytes are zero-padded, so neighbours'
+// partial dwords merge); every full KiB leaves the ring in one 16-byte store
+// per lane.
+// Blocks are taken in a grid-stride loop (the grid is sized to the chip, not
+// to the plan's block count).
 // --------------------------------------------------------------------------
 constexpr int kRingBytes = 4096;  // a stripe pair adds <= 1536 bytes; drains every KiB
 constexpr int kRingGuard = 4;     // dwords past the ring: a lane's <= 4 dwords never wrap
