@@ -890,7 +890,7 @@ static void tile_samples(const encoder *E, const void *pix, int tx0, int ty0, in
     for (int y = 0; y < th; y++) {
         for (int x = 0; x < tw; x++) {
             size_t pi = ((size_t)(ty0 + y) * E->w + (tx0 + x)) * nc;
-            int32_t s[4];
+            int32_t s[4] = {0, 0, 0, 0};
             for (int c = 0; c < nc; c++)
                 s[c] = (B == 8 ? (int32_t)((const uint8_t *)pix)[pi + c]
                                : (int32_t)((const uint16_t *)pix)[pi + c]) - off;
