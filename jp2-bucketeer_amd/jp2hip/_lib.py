@@ -240,6 +240,13 @@ class Output:
     def tobytes(self) -> bytes:
         return bytes(self.view())
 
+    def tail(self, k: int) -> bytes:
+        """The last k bytes, read in place (no array type, no view)."""
+        if self._buf is None:
+            raise ValueError("released output")
+        k = min(k, self._n)
+        return ctypes.string_at(ctypes.addressof(self._buf.ptr.contents) + self._n - k, k)
+
     def close(self):
         self._buf = None
 

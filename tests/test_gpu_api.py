@@ -19,3 +19,21 @@ def test_env_check_names_too_few_queues(monkeypatch):
     finally:
         for e in encs:
             e.close()
+
+
+def test_output_tail_reads_in_place():
+    """Output.tail(k) (the bench's EOC check) equals the view's last bytes."""
+    import imaging as im
+    from devmem import DeviceBytes
+    tif = im.tiff_bytes(im.synth_rgb8(200, 300, seed=4))
+    lay, _ = jp2hip.tiff_layout(tif)
+    d = DeviceBytes(tif)
+    e = jp2hip.Encoder(0)
+    try:
+        out, _ = e.encode_device(d.ptr, d.nbytes, lay, jp2hip.LOSSY, jp2hip.recipe(jp2hip.LOSSY), copy=False)
+        assert out.tail(2) == b"\xff\xd9"
+        assert out.tail(10) == bytes(out.view()[-10:])
+        out.close()
+    finally:
+        e.close()
+        d.free()
