@@ -709,38 +709,25 @@ __device__ __forceinline__ void mq_byteout(Mq &m) {
     }
 }
 
-// The coder's byte ring: 64 bytes per lane at a 68-byte stride (default), or
-// interleaved (JP2HIP_MQ_RING_IL=1): dword k of lane L's ring at LDS dword
-// k * 64 + L, so the byte a lane stores on every step lands in bank L
-// whatever its position -- no bank conflicts.  Measured (gpurun_out/r4a/
-// ab_ring): the interleaved ring's extra address arithmetic costs more than
-// the conflicts it removes (k_t1_mq alone 2894 -> 2905 us, C2 bench 24.9 ->
-// 24.3 GP/s), so the packed layout stays.
-#ifndef JP2HIP_MQ_RING_IL
-#define JP2HIP_MQ_RING_IL 0
-#endif
-// ring bytes per lane (packed layout): 64, or 32 (flushed 8 bytes at a time,
-// 2 KB less LDS per workgroup)
-#ifndef JP2HIP_MQ_RING_BYTES
-#define JP2HIP_MQ_RING_BYTES 64
-#endif
-constexpr int kRingLaneBytes = JP2HIP_MQ_RING_IL ? 64 : JP2HIP_MQ_RING_BYTES;
-constexpr int kRingFlush = kRingLaneBytes / 4;  // bytes per flush group
-#if JP2HIP_MQ_RING_IL
-constexpr int kRingLaneStride = 4;
-__device__ __forceinline__ int ring_slot(int bp) { return ((bp & 60) << 6) | (bp & 3); }
-#else
-constexpr int kRingLaneStride = kRingLaneBytes + 4;  // odd dword stride: lanes on different banks
-__device__ __forceinline__ int ring_slot(int bp) { return bp & (kRingLaneBytes - 1); }
-#endif
+// The coder's byte ring: 64 bytes per lane, lane L's at LDS byte 64 L, byte
+// position bp (offset by 4 L, which spreads the lanes over the banks) at
+// slot bp & 63 -- one bit-field insert per address.  (Measured before:
+// rings at a 68-byte stride, and interleaved by lane -- dword k of lane L at
+// dword 64 k + L, no conflicts but more address arithmetic: k_t1_mq alone
+// 2894 -> 2905 us, C2 bench 24.9 -> 24.3 GP/s, gpurun_out/r4a/ab_ring.)
+__device__ __forceinline__ uint32_t ring_at(int bp, uint32_t lb) {  // lb = 64 L
+    uint32_t r;  // (bp & 63) | lb as one bit-field insert (the compiler adds after an AND)
+    asm("v_bfi_b32 %0, 63, %1, %2" : "=v"(r) : "v"(bp), "v"(lb));
+    return r;
+}
 
-__device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
+__device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring, uint32_t lb) {
     uint32_t B = m.B;
     if (B != 0xFF && m.C >= 0x8000000u) {
         B++;
         m.C &= 0x7FFFFFFu;
     }
-    ring[ring_slot(m.bp)] = (uint8_t)B;  // bp = -1 -> the ring's last slot, see mq_code
+    ring[ring_at(m.bp, lb)] = (uint8_t)B;  // bp = -1 -> the ring's last slot, see mq_code
     m.bp++;
     const bool ff = B == 0xFF;
     m.B = ff ? (m.C >> 20) : (m.C >> 19);
@@ -754,16 +741,20 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
 //   wave 0 (modeller) walks the blocks' decision streams with the context
 //     states and the interval register A: per decision it knows whether C
 //     gains Qe and how many bits the renormalisation shifts -- the code
-//     register's whole input -- and leaves (add | shifts << 16) in an LDS slot;
+//     register's whole input -- and leaves (add << 16 | shifts) in an LDS slot;
 //   wave 1 (coder) runs C, CT and the byte-outs over those words.
 // Chunks of 16 decisions per lane, double-buffered, one workgroup barrier per
 // chunk: the modeller writes chunk i + 1 while the coder codes chunk i, so a
 // decision costs the longer of the two chains, not their sum.
 //
 // Context state = the 32-bit word of its (table index i, MPS symbol) pair,
-// entry e = 2 i + MPS of a 94-entry table: Qe | e(NMPS) << 16 | e(NLPS) << 23
-// with the MPS symbol in bit 31, where e(NLPS) already carries the MPS flip of
-// a SWITCH state -- the next state is one table read, no bit fix-up.
+// entry e = 2 i + MPS: Qe << 16 | 8 e | MPS.  Entry e's 8 bytes in the LDS
+// table are the words of its NMPS and NLPS entries (the NLPS one with a
+// SWITCH state's MPS flip applied), so the state word is also the address of
+// both candidate next states: they are read (one 8-byte LDS read) as soon as
+// the state is known, while the decision's arithmetic runs, and a select
+// picks one.  The interval register A is kept scaled by 2^16 (the Qe field
+// needs no shift, and the renormalisation count is its leading zeros).
 //
 // The CODEMPS/CODELPS procedures fold into one select -- the interval keeps
 // A - Qe exactly when "MPS" xor "conditional exchange" -- and the context
@@ -775,31 +766,34 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring) {
 constexpr int kMqChunk = 16;
 constexpr uint32_t kPadWord = 0x01010101u * kPadDecision;
 
+// the state word of entry e (Qe << 16 | 8 e | MPS)
+__device__ __forceinline__ uint32_t mq_word(int e) { return ((uint32_t)c_qe[e >> 1] << 16) | ((uint32_t)e << 3) | (uint32_t)(e & 1); }
+
 // modeller: one decision; returns the context's next state, *code = the
-// coder's input word
-__device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, const uint32_t *tab, const uint32_t d,
+// coder's input word (C's addend << 16 | renormalisation shifts).  A = the
+// interval register << 16.
+__device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, const uint8_t *tab, const uint32_t d,
                                              uint32_t &code) {
-    const uint32_t qe = t & 0xFFFFu;
-    const bool isM = d == (t >> 31);
-    // next state: the NMPS / NLPS entry (MPS flip included), read early
-    const uint32_t tw = tab[__builtin_amdgcn_ubfe(t, isM ? 16u : 23u, 7u)];
+    const uint2 nx = *(const uint2 *)(tab + (t & 0x3F8u));  // NMPS / NLPS words, read first
+    const uint32_t qe = t & 0xFFFF0000u;  // Qe << 16
+    const bool isM = d == (t & 1u);
     const uint32_t A1 = A - qe;
     const bool keep = isM != (A1 < qe);
-    const uint32_t An = keep ? A1 : qe;  // never 0: Qe >= 1, and A1 = A >= 0x8000 for Qe = 0
-    const bool ren = !isM || A1 < 0x8000u;
-    const uint32_t n = (uint32_t)__builtin_clz(An) - 16u;  // renormalisation shifts
+    const uint32_t An = keep ? A1 : qe;  // never 0: Qe >= 1, and A1 = A >= 2^31 for Qe = 0
+    const bool ren = !isM || A1 < 0x80000000u;
+    const uint32_t n = (uint32_t)__builtin_clz(An);  // renormalisation shifts
     A = An << n;
-    code = (keep ? qe : 0u) | (n << 16);
-    return ren ? tw : t;
+    code = (keep ? qe : 0u) | n;
+    return ren ? (isM ? nx.x : nx.y) : t;
 }
 
 // coder: C += add, then n shifts with their byte-outs.  The (at most one,
 // common) byte-out is applied by select and its byte written to the lane's
 // 64-byte LDS ring on every step -- so the only branch is the rare second
 // byte-out of one renormalisation.
-__device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *ring) {
-    const uint32_t add = code & 0xFFFFu;
-    const int n = (int)(code >> 16);
+__device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *ring, uint32_t lb) {
+    const uint32_t add = code >> 16;
+    const int n = (int)(code & 0xFFFFu);
     const uint32_t C0 = m.C + add;
     const int CT = m.CT;
     const bool bo = n >= CT;  // a byte-out inside this renormalisation
@@ -816,7 +810,7 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
     // Byte -1 (the MQ coder's initial pending byte, never output) lands in
     // the ring's last slot, which the byte of that slot overwrites before
     // its group is flushed
-    ring[ring_slot(m.bp)] = (uint8_t)Bc;
+    ring[ring_at(m.bp, lb)] = (uint8_t)Bc;
     uint32_t Cx = bo ? (C2 & ((1u << sh) - 1u)) : C1;
     int CTx = bo ? 27 - (int)sh : CT - n;
     int rem = n - s1;
@@ -825,7 +819,7 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
     if (bo && rem >= CTx) {  // rare: a second byte-out in this renormalisation
         m.C = Cx << CTx;
         rem -= CTx;
-        ring_byteout(m, ring);
+        ring_byteout(m, ring, lb);
         Cx = m.C;
         CTx = m.CT;
     }
@@ -833,27 +827,18 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
     m.CT = CTx - rem;
 }
 
-// Copy the lane's completed 16-byte ring groups to the code-block output.
-__device__ __forceinline__ void ring_flush(const Mq &m, const uint8_t *ring, int &fl) {
-    while (m.bp - fl >= kRingFlush) {
-#if JP2HIP_MQ_RING_IL
+// Copy the lane's completed 16-byte groups to the code-block output (byte
+// positions run `off` = 4 L ahead of the output's, so a group's dwords may
+// wrap round the lane's ring).
+__device__ __forceinline__ void ring_flush(const Mq &m, const uint8_t *ring, uint32_t lb, int off, int &fl) {
+    while (m.bp - fl >= 16) {
         uint4 v;
-        const uint32_t *g = (const uint32_t *)(ring + ring_slot(fl));
-        v.x = g[0]; v.y = g[64]; v.z = g[128]; v.w = g[192];
-        if (fl + 16 <= m.cap) *(uint4 *)(m.out + fl) = v;
-#else
-        const uint32_t *g = (const uint32_t *)(ring + ring_slot(fl));
-        if (kRingFlush == 16) {
-            uint4 v;
-            v.x = g[0]; v.y = g[1]; v.z = g[2]; v.w = g[3];
-            if (fl + 16 <= m.cap) *(uint4 *)(m.out + fl) = v;
-        } else {
-            uint2 v;
-            v.x = g[0]; v.y = g[1];
-            if (fl + 8 <= m.cap) *(uint2 *)(m.out + fl) = v;
-        }
-#endif
-        fl += kRingFlush;
+        v.x = *(const uint32_t *)(ring + ring_at(fl, lb));
+        v.y = *(const uint32_t *)(ring + ring_at(fl + 4, lb));
+        v.z = *(const uint32_t *)(ring + ring_at(fl + 8, lb));
+        v.w = *(const uint32_t *)(ring + ring_at(fl + 12, lb));
+        if (fl - off + 16 <= m.cap) *(uint4 *)(m.out + (fl - off)) = v;
+        fl += 16;
     }
 }
 
@@ -874,9 +859,9 @@ __device__ __forceinline__ int mq_flush(Mq &m) {
 
 // LDS of one k_t1_mq workgroup
 struct MqShared {
+    uint2 mqt[94];                         // per entry: its NMPS and NLPS state words
     uint32_t cxs[20 * 64];                 // 19 contexts + CX_PAD, lane-interleaved (modeller)
-    uint32_t mqt[94];                      // state table
-    uint32_t rings[64 * (kRingLaneStride / 4) + (JP2HIP_MQ_RING_IL ? 64 * 16 : 0)];  // coder: byte ring per lane
+    uint32_t rings[64 * 16];               // coder: a 64-byte byte ring per lane
     // (the bucket bases are done with before the first chunk: one LDS slot,
     // 19.1 KB a workgroup, 8 per CU instead of 7)
     union {
@@ -901,14 +886,15 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
     const int lane = threadIdx.x & 63;
     const int b = sh.blk[lane];
     uint32_t *cx = sh.cxs + lane;
-    const uint32_t *mqt = sh.mqt;
+    const uint8_t *mqt = (const uint8_t *)sh.mqt;
+    const uint32_t w0 = mq_word(0);
 #pragma unroll
-    for (int q = 0; q < 19; q++) cx[q * 64] = mqt[0];  // entry 2 i + MPS; all start with MPS 0
+    for (int q = 0; q < 19; q++) cx[q * 64] = w0;  // entry 2 i + MPS; all start with MPS 0
     cx[CX_PAD * 64] = 0u;  // Qe 0, MPS 0: the padding decisions' no-op state
-    cx[0] = mqt[2 * 4];
-    cx[CX_RL * 64] = mqt[2 * 3];
-    cx[CX_UNI * 64] = mqt[2 * 46];
-    uint32_t A = 0x8000u;
+    cx[0] = mq_word(2 * 4);
+    cx[CX_RL * 64] = mq_word(2 * 3);
+    cx[CX_UNI * 64] = mq_word(2 * 46);
+    uint32_t A = 0x8000u << 16;
     int nseg = 0, s = 0, k = 0, pass = 2, left = 0, Pt = 0;
     uint32_t cap = 0;
     const uint8_t *sbase = nullptr;
@@ -959,7 +945,7 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         const int buf = it & 1;
         sh.segs[buf][lane] = s;
         if (!__any(active)) {
-            sh.finA[lane] = A;
+            sh.finA[lane] = A >> 16;
             if (lane == 0) sh.more[buf] = 0;
             __syncthreads();
             break;
@@ -1010,10 +996,12 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
 __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
     const int lane = threadIdx.x & 63;
     const int b = sh.blk[lane];
-    uint8_t *ring = (uint8_t *)sh.rings + lane * kRingLaneStride;
-    int fl = 0;  // bytes already copied from the ring
+    uint8_t *ring = (uint8_t *)sh.rings;
+    const uint32_t lb = (uint32_t)lane << 6;  // the lane's ring
+    const int off = 4 * lane;                 // byte positions run off ahead (ring_at)
+    int fl = off;                             // bytes already copied from the ring
     Mq m;
-    m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = -1;
+    m.C = 0; m.A = 0x8000; m.B = 0; m.CT = 12; m.bp = off - 1;
     m.cap = 0;
     m.out = nullptr;
     int32_t *R = nullptr;
@@ -1033,7 +1021,7 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
         const int buf = it & 1;
         // passes that ended before this chunk end at the current length
         const int s_now = sh.segs[buf][lane];
-        for (; sdone < s_now; sdone++) R[sdone] = m.bp + 3;
+        for (; sdone < s_now; sdone++) R[sdone] = m.bp - off + 3;
         if (!sh.more[buf]) break;
         // the chunk's 16 words read up front (one wait, not one per decision)
         const uint32_t *in = &sh.code[buf][0][lane];
@@ -1042,18 +1030,16 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
         for (int j = 0; j < kMqChunk; j++) cw[j] = in[j * 64];
 #pragma unroll
         for (int j = 0; j < kMqChunk; j++) {
-            mq_code(m, cw[j], ring);
-            // a 32-byte ring is emptied twice a chunk: 8 decisions add at most
-            // 15 bytes (<= 15 shifts each), so <= 22 are pending
-            if (kRingLaneBytes < 64 && j == kMqChunk / 2 - 1) ring_flush(m, ring, fl);
+            mq_code(m, cw[j], ring, lb);
         }
-        ring_flush(m, ring, fl);
+        ring_flush(m, ring, lb, off, fl);
     }
     if (b < 0) return;
     const int nseg = sdone;
     m.A = sh.finA[lane];
     for (int i = fl; i < m.bp; i++)  // bytes still in the ring
-        if (i < m.cap) m.out[i] = ring[ring_slot(i)];
+        if (i - off < m.cap) m.out[i - off] = ring[ring_at(i, lb)];
+    m.bp -= off;
     const int len = mq_flush(m);
     if (len > m.cap) atomicOr(a.err, 1);
     R[nseg - 1] = len;
@@ -1087,8 +1073,7 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
     for (int e = tid; e < 94; e += 128) {
         const int i = e >> 1, mps = e & 1;
         const int sw = i == 0 || i == 6 || i == 14;
-        sh.mqt[e] = (uint32_t)c_qe[i] | ((uint32_t)(2 * c_nmps[i] + mps) << 16) |
-                    ((uint32_t)(2 * c_nlps[i] + (mps ^ sw)) << 23) | ((uint32_t)mps << 31);
+        sh.mqt[e] = make_uint2(mq_word(2 * c_nmps[i] + mps), mq_word(2 * c_nlps[i] + (mps ^ sw)));
     }
     if (tid < 64) {  // exclusive scan of the bucket fills, kOrderBuckets / 64 per lane
         uint32_t v[kOrderBuckets / 64], t = 0;

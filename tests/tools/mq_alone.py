@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""One C2 image at a time (and one C3 lossless image): min over 6 encodes of
+each stage's HIP-event time, for the library JP2HIP_LIBRARY names."""
+import os, sys, json
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+import torch  # noqa: E402
+torch.cuda.init()
+import bench  # noqa: E402
+import jp2hip  # noqa: E402
+import imaging as im  # noqa: E402
+enc = jp2hip.Encoder(0, profile=True)
+res = {"lib": os.path.basename(os.environ.get("JP2HIP_LIBRARY", "libjp2hip.so"))}
+for kind, conv, kw in (("c2", jp2hip.LOSSY, {}), ("c3", jp2hip.LOSSLESS, {"tile_w": 1024, "tile_h": 1024})):
+    img = bench.make_image(kind, seed=1234 if kind == "c2" else 2)
+    tif = im.tiff_bytes(img, rows_per_strip=64)
+    lay, _ = jp2hip.tiff_layout(tif)
+    d = torch.frombuffer(bytearray(tif), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    rc = jp2hip.recipe(conv, **kw)
+    best = {}
+    for _ in range(6):
+        o, st = enc.encode_device(d.data_ptr(), d.numel(), lay, conv, rc, copy=False)
+        o.close()
+        for k, v in st.as_dict().items():
+            if k.endswith("_ms"):
+                best[k] = min(best.get(k, 1e9), v)
+    res[kind] = {k: round(v, 3) for k, v in best.items() if k in ("t1_mq_ms", "t1_cm_ms", "total_ms")}
+    del d
+print(json.dumps(res), flush=True)
+enc.close()
