@@ -607,6 +607,7 @@ int oracle_t1_encode(const int32_t *sm, int w, int h, int band, int lossless,
 /* Planes P-1 .. pmin only: the codeword is flushed after the last coded
  * pass, so the truncation lengths of the coded passes are those of a block
  * whose lower planes do not exist. */
+static int64_t g_pass_dec[100];  /* experiments (ORACLE_PASS_WASTE): g_decisions at each pass end */
 int oracle_t1_encode_planes(const int32_t *sm, int w, int h, int band, int lossless, int pmin,
                             uint8_t *out, int cap, int *out_len, int32_t *rates, int64_t *dists,
                             int *nplanes) {
@@ -698,6 +699,7 @@ int oracle_t1_encode_planes(const int32_t *sm, int w, int h, int band, int lossl
             if (pass == 2) memset(t.pi, 0, fs);
             dists[np] = dd;
             rates[np] = mq_numbytes(&mq) + 3;
+            if (np < 100) g_pass_dec[np] = g_decisions;  /* experiments: decisions through each pass */
             np++;
             if (mq_numbytes(&mq) + 8 > cap) {
                 free(flags); free(buf);
@@ -837,6 +839,7 @@ typedef struct {
     int pmin;            /* lowest coded bit-plane */
     uint32_t est[32];    /* predicted coded size of plane p, 1/16 bit */
     int64_t pd[32];      /* exact distortion decrease of plane p */
+    int32_t *pdec;       /* experiments (ORACLE_PASS_WASTE): decisions per coded pass */
 } cblk;
 
 typedef struct {
@@ -1038,6 +1041,10 @@ static int predict_and_code(encoder *E, int64_t target) {
                 if (f) { fprintf(f, "%lld %d\n", (long long)(g_decisions - dec0), np); fclose(f); }
             }
             if (np < 0) return -1;
+            if (getenv("ORACLE_PASS_WASTE") && np > 0) {  /* experiments: decisions per coded pass */
+                if (!b->pdec) b->pdec = (int32_t *)malloc(sizeof(int32_t) * 100);
+                for (int q = 0; q < np && q < 100; q++) b->pdec[q] = (int32_t)(g_pass_dec[q] - (q ? g_pass_dec[q - 1] : dec0));
+            }
             b->npasses = np;
             total += b->len;
         }
@@ -1615,7 +1622,7 @@ static void free_encoder(encoder *E) {
         }
         free(E->tiles);
     }
-    for (int i = 0; i < E->nall; i++) { free(E->all[i]->data); free(E->all[i]->sm); free(E->all[i]); }
+    for (int i = 0; i < E->nall; i++) { free(E->all[i]->data); free(E->all[i]->sm); free(E->all[i]->pdec); free(E->all[i]); }
     free(E->all);
 }
 
@@ -1732,6 +1739,31 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         }
     }
     free(S);
+    if (getenv("ORACLE_PASS_WASTE")) {  /* experiments: coded decisions PCRD discards, by pass */
+        FILE *f = fopen(getenv("ORACLE_PASS_WASTE"), "a");
+        int64_t all = 0, kept = 0, lost[3] = {0, 0, 0}, lost_last[3] = {0, 0, 0}, lost_plane = 0;
+        for (int i = 0; f && i < E.nall; i++) {
+            cblk *b = E.all[i];
+            if (!b->pdec) continue;
+            int n = b->npasses, keep = b->nl[NL - 1];
+            for (int q = 0; q < n && q < 100; q++) {
+                int ty = q == 0 ? 2 : (q - 1) % 3;  /* 0 SPP, 1 MRP, 2 CUP */
+                all += b->pdec[q];
+                if (q < keep) { kept += b->pdec[q]; continue; }
+                lost[ty] += b->pdec[q];
+                if (q >= n - 3) lost_last[ty] += b->pdec[q];  /* the lowest coded plane */
+                if (keep <= n - 3) lost_plane += b->pdec[q];   /* a whole plane or more discarded */
+            }
+        }
+        if (f) {
+            fprintf(f, "{\"decisions\": %lld, \"kept\": %lld, \"lost_spp\": %lld, \"lost_mrp\": %lld, \"lost_cup\": %lld, "
+                       "\"lost_lowest_plane_spp\": %lld, \"lost_lowest_plane_mrp\": %lld, \"lost_lowest_plane_cup\": %lld, "
+                       "\"lost_in_blocks_dropping_a_whole_plane\": %lld}\n",
+                    (long long)all, (long long)kept, (long long)lost[0], (long long)lost[1], (long long)lost[2],
+                    (long long)lost_last[0], (long long)lost_last[1], (long long)lost_last[2], (long long)lost_plane);
+            fclose(f);
+        }
+    }
     bytes file = {0, 0, 0};
     if (rc->format == 0) file = cs;
     else { wrap_file(&E, &cs, &file); free(cs.d); }
