@@ -901,7 +901,12 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
     const uint4 *cntp = nullptr, *ptr = nullptr;
     const int64_t *dspp = nullptr, *dref = nullptr, *dsig = nullptr;
     int64_t *D = nullptr;
-    uint4 cnt = make_uint4(0u, 0u, 0u, 0u), cur = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
+    const uint4 pad4 = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
+    // the decision stream is read two chunks ahead: cur = this chunk, nx1 =
+    // the next (loaded iff the pass has more than 16 decisions left), and a
+    // chunk issues the load of the one after nx1 -- a 16-byte load's latency
+    // is about one chunk's 16 decisions
+    uint4 cnt = make_uint4(0u, 0u, 0u, 0u), cur = pad4, nx1 = pad4;
     int64_t ndec = 0;
     if (b >= 0) {
         const BlockDesc d = a.blocks[b];
@@ -920,6 +925,7 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         left = (int)cnt.z;
         ndec = left;
         cur = ptr[0];
+        if (left > 16) nx1 = ptr[1];
     }
     uint64_t cyc_wait = 0;  // debug census: shader cycles spent at the chunk barrier
     const uint64_t cyc0 = __builtin_readcyclecounter();
@@ -940,6 +946,7 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
             left = pass == 0 ? (int)cnt.x : (pass == 1 ? (int)cnt.y : (int)cnt.z);
             ndec += left;
             cur = ptr[0];
+            nx1 = left > 16 ? ptr[1] : pad4;
         }
         const bool active = s < nseg;
         const int buf = it & 1;
@@ -952,11 +959,12 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         }
         if (lane == 0) sh.more[buf] = 1;
         // one chunk of 16 decisions (a pass's last chunk is padded; a lane
-        // whose block is done codes padding); the next chunk's load is in
-        // flight behind it, and each context state is read one decision ahead
-        uint4 nxt = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
-        if (active) nxt = ptr[1];
-        if (!active) cur = make_uint4(kPadWord, kPadWord, kPadWord, kPadWord);
+        // whose block is done codes padding); the loads of the next two
+        // chunks are in flight behind it, and each context state is read one
+        // decision ahead
+        uint4 nx2 = pad4;
+        if (active && left > 32) nx2 = ptr[2];
+        if (!active) cur = pad4;
         const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
         uint32_t t = cx[__builtin_amdgcn_ubfe(w[0], 1, 5) * 64];
         uint32_t *out = &sh.code[buf][0][lane];
@@ -979,7 +987,8 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         if (active) {
             left -= min(16, left);
             ptr++;
-            cur = nxt;
+            cur = nx1;
+            nx1 = nx2;
         }
         const uint64_t c1 = a.dbg ? __builtin_readcyclecounter() : 0;
         __syncthreads();  // chunk `it` ready; the coder is done with chunk it - 1
