@@ -791,6 +791,9 @@ __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, cons
 // common) byte-out is applied by select and its byte written to the lane's
 // 64-byte LDS ring on every step -- so the only branch is the rare second
 // byte-out of one renormalisation.
+// TWO = false: no decision of the chunk shifts 8 or more (a second byte-out
+// in one renormalisation needs n >= CT + 7 >= 8), so its test is left out.
+template <bool TWO>
 __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *ring, uint32_t lb) {
     const uint32_t add = code >> 16;
     const int n = (int)(code & 0xFFFFu);
@@ -816,7 +819,7 @@ __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *rin
     int rem = n - s1;
     m.B = bo ? (C2 >> sh) : m.B;
     m.bp += bo ? 1 : 0;
-    if (bo && rem >= CTx) {  // rare: a second byte-out in this renormalisation
+    if (TWO && bo && rem >= CTx) {  // rare: a second byte-out in this renormalisation
         m.C = Cx << CTx;
         rem -= CTx;
         ring_byteout(m, ring, lb);
@@ -1037,9 +1040,16 @@ __device__ __forceinline__ void mq_coder(const T1MqArgs &a, MqShared &sh) {
         uint32_t cw[kMqChunk];
 #pragma unroll
         for (int j = 0; j < kMqChunk; j++) cw[j] = in[j * 64];
+        // a chunk whose shifts are all < 8 (about 9 in 10 on C2) takes the
+        // coder without the second-byte-out branch (bit 3 of the shift field)
+        const uint32_t any8 = (cw[0] | cw[1] | cw[2] | cw[3] | cw[4] | cw[5] | cw[6] | cw[7] | cw[8] | cw[9] |
+                               cw[10] | cw[11] | cw[12] | cw[13] | cw[14] | cw[15]) & 8u;
+        if (__any(any8 != 0u)) {
 #pragma unroll
-        for (int j = 0; j < kMqChunk; j++) {
-            mq_code(m, cw[j], ring, lb);
+            for (int j = 0; j < kMqChunk; j++) mq_code<true>(m, cw[j], ring, lb);
+        } else {
+#pragma unroll
+            for (int j = 0; j < kMqChunk; j++) mq_code<false>(m, cw[j], ring, lb);
         }
         ring_flush(m, ring, lb, off, fl);
     }
