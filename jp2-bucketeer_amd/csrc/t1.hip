@@ -111,73 +111,78 @@ __device__ __forceinline__ Nbr8 nbr8(uint64_t Vb, uint64_t Va, uint64_t LVb, uin
     return n;
 }
 
+// A 3-input bitwise function on both 32-bit halves (one v_bitop3_b32 each):
+// TT is the function's value on a = 0xF0, b = 0xCC, c = 0xAA (bit a b c of
+// the table = f(a, b, c)), e.g. (a & b) | c -> 0xEA.
+template <uint32_t TT>
+__device__ __forceinline__ uint64_t b3(uint64_t a, uint64_t b, uint64_t c) {
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, TT);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), TT);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Zero-coding context (Table D.1, zc_ctx) of every row, as 4 bit masks.
+// The table's cases reduced to a few 3-input functions of the neighbour
+// counts (diagonals as a thermometer dge1 / dge2 / dge3, horizontal and
+// vertical pairs); checked equal to the case-by-case form on all 256
+// neighbourhoods of each band.
 struct Ctx4 {
     uint64_t b0, b1, b2, b3;
 };
 __device__ __forceinline__ Ctx4 zc_masks(int band, const Nbr8 &n) {
-    const uint64_t s1x = n.UL ^ n.UR, s1a = n.UL & n.UR, s2x = n.DL ^ n.DR, s2a = n.DL & n.DR;
-    const uint64_t dge1 = s1x | s1a | s2x | s2a;
-    const uint64_t dge2 = s1a | s2a | (s1x & s2x);
-    uint64_t I1, I2, I3, I4, I5, I6, I7, I8;
+    const uint64_t u = n.UL | n.UR, d = n.DL | n.DR, dge1 = u | d;
+    const uint64_t s2a = n.DL & n.DR;
+    const uint64_t dge2 = b3<0xEA>(u, d, b3<0xEA>(n.UL, n.UR, s2a));  // (u & d) | (UL & UR) | (DL & DR)
+    Ctx4 z;
     if (band == 3) {
-        const uint64_t dge3 = (s1a & (s2x | s2a)) | (s2a & (s1x | s1a));
-        const uint64_t hvge1 = n.L | n.R | n.U | n.D;
-        const uint64_t hvge2 = (n.L & n.R) | (n.U & n.D) | ((n.L ^ n.R) & (n.U ^ n.D));
-        const uint64_t hv1 = hvge1 & ~hvge2;
-        const uint64_t d2 = dge2 & ~dge3, d1 = dge1 & ~dge2, d0 = ~dge1;
-        I8 = dge3;
-        I7 = d2 & hvge1;
-        I6 = d2 & ~hvge1;
-        I5 = d1 & hvge2;
-        I4 = d1 & hv1;
-        I3 = d1 & ~hvge1;
-        I2 = d0 & hvge2;
-        I1 = d0 & hv1;
+        const uint64_t dge3 = b3<0xEA>(s2a, u, (n.UL & n.UR) & d);  // three or four diagonals
+        const uint64_t a = n.L | n.R, c = n.U | n.D, hvge1 = a | c;
+        const uint64_t hvge2 = b3<0xEA>(a, c, b3<0xEA>(n.L, n.R, n.U & n.D));
+        const uint64_t d2 = b3<0x30>(dge2, dge3, dge3), d1 = b3<0x30>(dge1, dge2, dge2);  // exactly 2 / 1
+        const uint64_t hv1 = b3<0x30>(hvge1, hvge2, hvge2);                              // exactly 1
+        z.b3 = dge3;
+        z.b2 = b3<0xEA>(d1, hvge1, d2);                                  // d2 | (d1 & hvge1)
+        z.b1 = b3<0xAE>(dge1, hvge2, b3<0xBA>(d1, hvge1, d2));           // .. | (d1 & ~hvge1) | (d0 & hvge2)
+        z.b0 = b3<0xEA>(d2, hvge1, b3<0x72>(d1, dge1, hv1));             // (d2 & hvge1) | (d1 & ~hv1) | (d0 & hv1)
     } else {
-        // h: horizontal neighbours, v: vertical (swapped for the HL band)
+        // A: the pair that counts most (horizontal; vertical for HL), B: the other
         const uint64_t A1 = band == 1 ? n.U : n.L, A2 = band == 1 ? n.D : n.R;
         const uint64_t B1 = band == 1 ? n.L : n.U, B2 = band == 1 ? n.R : n.D;
-        const uint64_t h2 = A1 & A2, h1 = A1 ^ A2, h0 = ~(A1 | A2);
-        const uint64_t vge1 = B1 | B2, v2 = B1 & B2, v1 = B1 ^ B2;
-        I8 = h2;
-        I7 = h1 & vge1;
-        I6 = h1 & ~vge1 & dge1;
-        I5 = h1 & ~vge1 & ~dge1;
-        I4 = h0 & v2;
-        I3 = h0 & v1;
-        I2 = h0 & ~vge1 & dge2;
-        I1 = h0 & ~vge1 & dge1 & ~dge2;
+        const uint64_t e = b3<0x30>(dge1, dge2, dge2);  // exactly one diagonal
+        const uint64_t x = A1 ^ A2;                     // exactly one of A
+        z.b3 = A1 & A2;
+        z.b2 = b3<0x3E>(A1, A2, B1 & B2);               // x | (no A & both B)
+        z.b1 = b3<0xEA>(x, B1 | B2 | dge1, b3<0x02>(A1, A2, b3<0x3E>(B1, B2, dge2)));
+        z.b0 = b3<0xEA>(x, b3<0xFD>(B1, B2, dge1), b3<0x02>(A1, A2, b3<0x3E>(B1, B2, e)));
     }
-    Ctx4 z;
-    z.b0 = I1 | I3 | I5 | I7;
-    z.b1 = I2 | I3 | I6 | I7;
-    z.b2 = I4 | I5 | I6 | I7;
-    z.b3 = I8;
     return z;
 }
 
 // Sign-coding context (Tables D.2/D.3, sc_lut) of every row: context 9..13
-// (bit 3 always set) in b0..b2 and the XOR bit.
+// (bit 3 always set) in b0..b2 and the XOR bit.  A pair of neighbours
+// contributes p (their signs sum > 0) or n (< 0); the outputs are functions
+// of (hp, hn, vp, vn), checked equal to the table on all 256 cases.
 struct Sc4 {
     uint64_t b0, b1, b2, xr;
 };
+__device__ __forceinline__ void sc_pair(uint64_t As, uint64_t An, uint64_t Bs, uint64_t Bn, uint64_t &p, uint64_t &n) {
+    const uint64_t nA = As & An, nB = Bs & Bn;
+    const uint64_t pA = b3<0x30>(As, An, An), pB = b3<0x30>(Bs, Bn, Bn);
+    p = b3<0xBA>(pB, nA, b3<0x10>(As, An, nB));  // (pA & ~nB) | (pB & ~nA)
+    n = b3<0xBA>(nB, pA, b3<0x30>(nA, pB, pB));  // (nA & ~pB) | (nB & ~pA)
+}
 __device__ __forceinline__ Sc4 sc_masks(uint64_t Ls, uint64_t Ln, uint64_t Rs, uint64_t Rn, uint64_t Us, uint64_t Un,
                                         uint64_t Ds, uint64_t Dn) {
-    const uint64_t pL = Ls & ~Ln, nL = Ls & Ln, pR = Rs & ~Rn, nR = Rs & Rn;
-    const uint64_t pU = Us & ~Un, nU = Us & Un, pD = Ds & ~Dn, nD = Ds & Dn;
-    const uint64_t hp = (pL & pR) | ((pL | pR) & ~(nL | nR));
-    const uint64_t hn = (nL & nR) | ((nL | nR) & ~(pL | pR));
-    const uint64_t vp = (pU & pD) | ((pU | pD) & ~(nU | nD));
-    const uint64_t vn = (nU & nD) | ((nU | nD) & ~(pU | pD));
-    const uint64_t hz = ~(hp | hn), vz = ~(vp | vn);
-    const uint64_t I13 = (hp & vp) | (hn & vn), I12 = (hp | hn) & vz, I11 = (hp & vn) | (hn & vp);
-    const uint64_t I9 = hz & vz, I10 = hz & (vp | vn);
+    uint64_t hp, hn, vp, vn;
+    sc_pair(Ls, Ln, Rs, Rn, hp, hn);
+    sc_pair(Us, Un, Ds, Dn, vp, vn);
+    const uint64_t hnz = hp | hn, vnz = vp | vn;
+    const uint64_t opp = b3<0xEA>(hn, vp, hp & vn);  // opposite signs
     Sc4 c;
-    c.b0 = I9 | I11 | I13;
-    c.b1 = I10 | I11;
-    c.b2 = I12 | I13;
-    c.xr = hn | (hz & vn);
+    c.b0 = ~(hnz ^ vnz);               // ctx 9, 11, 13: both zero or both not
+    c.b1 = b3<0xAE>(hnz, vnz, opp);     // ctx 10, 11
+    c.b2 = b3<0x30>(hnz, opp, opp);     // ctx 12, 13
+    c.xr = b3<0xF2>(hn, hnz, vn);       // hn | (h zero & vn)
     return c;
 }
 
