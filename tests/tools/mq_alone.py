@@ -26,7 +26,7 @@ for kind, conv, kw in (("c2", jp2hip.LOSSY, {}), ("c3", jp2hip.LOSSLESS, {"tile_
         for k, v in st.as_dict().items():
             if k.endswith("_ms"):
                 best[k] = min(best.get(k, 1e9), v)
-    res[kind] = {k: round(v, 3) for k, v in best.items() if k in ("t1_mq_ms", "t1_cm_ms", "total_ms")}
+    res[kind] = {k: round(v, 3) for k, v in best.items() if k in ("t1_mq_ms", "t1_cm_ms", "quant_ms", "dwt_ms", "total_ms")}
     del d
 print(json.dumps(res), flush=True)
 enc.close()
