@@ -47,6 +47,10 @@ struct PlanCache {
 
 struct jp2hip_ctx {
     std::mutex mu;
+    // whole tile-split encodes on this context, one at a time: each rank
+    // takes its member's `mu`, so two concurrent splits could otherwise hold
+    // one member each and wait for each other in an exchange
+    std::mutex split_mu;
     jp2hip::GpuEncoder gpu;
     jp2hip_config cfg;
     int threads = 1;
@@ -842,7 +846,12 @@ class HostGroup {
     explicit HostGroup(int world) : world_(world) {}
     int reduce(int64_t *v, int n) {
         std::unique_lock<std::mutex> lk(mu_);
-        if (aborted_ || n < 0) return -1;
+        if (aborted_) return -1;
+        if (n < 0) {  // a bug in the caller: fail every rank, not just this one
+            aborted_ = true;
+            cv_.notify_all();
+            return -1;
+        }
         if (arrived_ == 0) {
             acc_.assign((size_t)n, 0);
             n_ = n;
@@ -968,7 +977,7 @@ void split_rank(jp2hip_ctx *m, int rank, int world, HostGroup &grp, const uint8_
     bl.strip_bytes = packed ? offs.data() + lay.nstrips : nullptr;
     {
         std::lock_guard<std::mutex> lk(m->mu);
-        if (!m->gpu.upload_source(h, std::max<size_t>(tot, 1), o.err)) {
+        if (!m->gpu.upload_source(h, std::max<size_t>(tot, 1), o.err) || !m->gpu.check_residency(o.err)) {
             grp.abort();
         } else {
             jp2hip_split sp{rank, world, &HostGroup::call, &grp};
@@ -1003,6 +1012,7 @@ int encode_split_host(jp2hip_ctx *ctx, const uint8_t *file, size_t flen, const j
     if (conversion != JP2HIP_LOSSY && conversion != JP2HIP_LOSSLESS)
         return fail("conversion must be JP2HIP_LOSSY (0) or JP2HIP_LOSSLESS (1)");
     const jp2hip_recipe rc = recipe_of(recipe, conversion);
+    std::lock_guard<std::mutex> split_lk(ctx->split_mu);
     std::vector<jp2hip_ctx *> members{ctx};
     members.insert(members.end(), ctx->peers.begin(), ctx->peers.end());
     const int world = (int)members.size();
@@ -1154,7 +1164,14 @@ int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg) {
     }
     if (c->cfg.device < 0 || c->cfg.device >= ndev) {
         delete c;
-        return fail("device ordinal out of range");
+        return fail("device ordinal " + std::to_string(c->cfg.device) + " out of range (" + std::to_string(ndev) +
+                    " visible)");
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->cfg.device) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        delete c;
+        return fail("device " + std::to_string(c->cfg.device) + " is not a gfx950 (MI355X) device");
     }
     std::string err;
     if (!c->gpu.init(c->cfg.device, err)) {

@@ -181,6 +181,10 @@ class GpuEncoder {
     // this encode's hull segments: slope keys (descending) and inclusive byte sums
     bool segments(const Plan &plan, std::vector<uint64_t> &keys, std::vector<int64_t> &cum, std::string &err);
     hipStream_t get_stream() const { return stream; }
+    int get_device() const { return device; }
+    // the stream and the main buffers are on this context's device (a
+    // tile-split member is checked before every split encode)
+    bool check_residency(std::string &err);
     // host waits since the last call (stats: host_waits per encode)
     int take_waits() {
         const int w = waits;

@@ -711,7 +711,12 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
         if (full) last = true;
     }
     bad = bad || b.P > b.end_bits;  // read past the end of the stream: truncated
-    if (lane == 0 && (bad || pos != cap)) atomicOr(a.err, 2);
+    if (bad || pos != cap) {
+        if (lane == 0) atomicOr(a.err, 2);
+        // a strip that stopped short: its remaining links become known bytes
+        // (0), so k_inflate_links never follows a stale or unwritten slot
+        for (uint32_t i = pos + (uint32_t)lane; i < cap; i += kInfLanes) L[i] = kLinkByte;
+    }
 }
 
 // Resolves every decoded strip's links (k_inflate) into its bytes: grid
@@ -722,20 +727,29 @@ __global__ void __launch_bounds__(kInfLanes) k_inflate(UnpackArgs a) {
 constexpr int kLinkChunk = 4096;
 __global__ void __launch_bounds__(256) k_inflate_links(UnpackArgs a, int chase) {
     const int s = blockIdx.y;
-    const uint32_t cap = (uint32_t)strip_out_bytes(a, s);
+    const uint64_t cap64 = strip_out_bytes(a, s);
+    if (cap64 >= (1ull << 31)) return;  // k_inflate refused the strip (error already set)
+    const uint32_t cap = (uint32_t)cap64;
     uint32_t *L = a.lnk + (uint64_t)s * a.stride;
     uint8_t *out = a.dst + (uint64_t)s * a.stride;
     const uint32_t p0 = blockIdx.x * (uint32_t)kLinkChunk;
+    // a well-formed link points strictly backwards; anything else (a corrupt
+    // strip's slot) ends the chain, so every chase terminates in bounds
     for (uint32_t p = p0 + threadIdx.x; p < min(cap, p0 + (uint32_t)kLinkChunk); p += 256) {
         uint32_t v = L[p];
         if (!chase) {
-            if (!(v & kLinkByte)) {
+            if (!(v & kLinkByte) && v < p) {
                 const uint32_t u = L[v];
                 if (u != v) L[p] = u;
             }
             continue;
         }
-        while (!(v & kLinkByte)) v = L[v];
+        uint32_t at = p;
+        while (!(v & kLinkByte)) {
+            if (v >= at) { v = kLinkByte; break; }
+            at = v;
+            v = L[v];
+        }
         out[p] = (uint8_t)v;
     }
 }
@@ -1803,6 +1817,27 @@ bool GpuEncoder::init(int dev, std::string &err) {
     HIPCHECK(hipEventCreateWithFlags(&sync_ev, hipEventBlockingSync | hipEventDisableTiming));
     HIPCHECK(hipEventCreateWithFlags(&stg_ev, hipEventDisableTiming));
     HIPCHECK(hipHostMalloc((void **)&h_tot, 8 * sizeof(int64_t), hipHostMallocDefault));
+    return true;
+}
+
+bool GpuEncoder::check_residency(std::string &err) {
+    hipDevice_t sd = -1;
+    HIPCHECK(hipStreamGetDevice(stream, &sd));
+    if ((int)sd != device) {
+        err = "context on device " + std::to_string(device) + ": its stream is on device " + std::to_string((int)sd);
+        return false;
+    }
+    const DevBuf *bufs[] = {&src, &coef, &bp, &t1out, &stream_buf, &t2out, &blocks};
+    for (const DevBuf *b : bufs) {
+        if (!b->ptr) continue;
+        hipPointerAttribute_t at;
+        HIPCHECK(hipPointerGetAttributes(&at, b->ptr));
+        if (at.device != device) {
+            err = "context on device " + std::to_string(device) + ": a buffer lives on device " +
+                  std::to_string(at.device);
+            return false;
+        }
+    }
     return true;
 }
 

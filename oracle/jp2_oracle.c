@@ -42,6 +42,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Experiment hooks (margin sweeps, decision censuses): read from the
+ * environment only in a build with -DORACLE_EXPERIMENTS (make experiments ->
+ * _build/liboracle_exp.so).  The parity oracle (liboracle.so) ignores the
+ * environment, so no variable can change what the tests compare against. */
+#ifdef ORACLE_EXPERIMENTS
+#define ORACLE_EXP(name) getenv(name)
+#else
+#define ORACLE_EXP(name) ((const char *)0)
+#endif
+
 static char g_err[512];
 static void set_err(const char *fmt, ...) {
     va_list ap;
@@ -1003,7 +1013,7 @@ static int predict_cut(const int64_t *hist, int64_t target) {
         acc += hist[k];
         if (acc >= goal) break;
     }
-    const char *m = getenv("ORACLE_SKIP_MARGIN");  /* experiments only (margin sweeps) */
+    const char *m = ORACLE_EXP("ORACLE_SKIP_MARGIN");  /* experiments only (margin sweeps) */
     return k - (m ? atoi(m) : kSkipMargin);
 }
 
@@ -1018,7 +1028,7 @@ static int predict_and_code(encoder *E, int64_t target) {
         }
     }
     int kcut = predict_cut(hist, target);
-    if (getenv("ORACLE_SKIP_DEBUG")) { int64_t tot = 0; int lo = -1, hi = -1; for (int k = 0; k < kSlopeBins; k++) { tot += hist[k]; if (hist[k] && lo < 0) lo = k; if (hist[k]) hi = k; } fprintf(stderr, "skip: target %lld est_total_bytes %lld bins %d..%d kcut %d\n", (long long)target, (long long)(tot / 128), lo, hi, kcut); }
+    if (ORACLE_EXP("ORACLE_SKIP_DEBUG")) { int64_t tot = 0; int lo = -1, hi = -1; for (int k = 0; k < kSlopeBins; k++) { tot += hist[k]; if (hist[k] && lo < 0) lo = k; if (hist[k]) hi = k; } fprintf(stderr, "skip: target %lld est_total_bytes %lld bins %d..%d kcut %d\n", (long long)target, (long long)(tot / 128), lo, hi, kcut); }
     free(hist);
     int lossless = E->rc->reversible;
     /* pass 0: predicted plane ranges.  Safety net: if every coded byte
@@ -1036,19 +1046,19 @@ static int predict_and_code(encoder *E, int64_t target) {
             const int64_t dec0 = g_decisions;
             int np = oracle_t1_encode_planes(b->sm, b->w, b->h, b->band, lossless, b->pmin, b->data, cap,
                                              &b->len, b->rates, b->dd, &b->P);
-            if (getenv("ORACLE_BLOCK_DECISIONS")) {  /* experiments: decisions per block */
-                FILE *f = fopen(getenv("ORACLE_BLOCK_DECISIONS"), "a");
+            if (ORACLE_EXP("ORACLE_BLOCK_DECISIONS")) {  /* experiments: decisions per block */
+                FILE *f = fopen(ORACLE_EXP("ORACLE_BLOCK_DECISIONS"), "a");
                 if (f) { fprintf(f, "%lld %d\n", (long long)(g_decisions - dec0), np); fclose(f); }
             }
             if (np < 0) return -1;
-            if (getenv("ORACLE_PASS_WASTE") && np > 0) {  /* experiments: decisions per coded pass */
+            if (ORACLE_EXP("ORACLE_PASS_WASTE") && np > 0) {  /* experiments: decisions per coded pass */
                 if (!b->pdec) b->pdec = (int32_t *)malloc(sizeof(int32_t) * 100);
                 for (int q = 0; q < np && q < 100; q++) b->pdec[q] = (int32_t)(g_pass_dec[q] - (q ? g_pass_dec[q - 1] : dec0));
             }
             b->npasses = np;
             total += b->len;
         }
-        if (getenv("ORACLE_SKIP_DEBUG")) fprintf(stderr, "skip pass %d: coded %lld bytes, %lld decisions so far\n", pass, (long long)total, (long long)g_decisions);
+        if (ORACLE_EXP("ORACLE_SKIP_DEBUG")) fprintf(stderr, "skip pass %d: coded %lld bytes, %lld decisions so far\n", pass, (long long)total, (long long)g_decisions);
         if (pass == 0 && !(skipped && total < target)) break;
     }
     for (int i = 0; i < E->nall; i++) { free(E->all[i]->sm); E->all[i]->sm = NULL; }
@@ -1155,8 +1165,8 @@ static int code_tilecomp(encoder *E, tileinfo *T, int c, void *buf, int tw, int 
                             int64_t dec0 = g_decisions;
                             int np = oracle_t1_encode(sm, b->w, b->h, band, rc->reversible, b->data, cap,
                                                       &b->len, b->rates, b->dd, &b->P);
-                            if (getenv("ORACLE_T1_STATS")) {
-                                FILE *sf = fopen(getenv("ORACLE_T1_STATS"), "a");
+                            if (ORACLE_EXP("ORACLE_T1_STATS")) {
+                                FILE *sf = fopen(ORACLE_EXP("ORACLE_T1_STATS"), "a");
                                 if (sf) {
                                     fprintf(sf, "%d %d %d %d %d %d %lld %d\n", c, d, band, b->w, b->h, b->P,
                                             (long long)(g_decisions - dec0), b->len);
@@ -1731,7 +1741,7 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
             cs.n = 0;
             write_codestream(&E, &cs);
             if ((int64_t)cs.n <= target) break;
-            if (getenv("ORACLE_RATE_DEBUG")) fprintf(stderr, "rate it %d budget %lld size %zu target %lld\n", it, (long long)budget, cs.n, (long long)target);
+            if (ORACLE_EXP("ORACLE_RATE_DEBUG")) fprintf(stderr, "rate it %d budget %lld size %zu target %lld\n", it, (long long)budget, cs.n, (long long)target);
             /* exponential back-off, plus 1/16 of the overshoot and 64 bytes so
              * the second pass (headers grow with the data they describe)
              * normally lands under the target instead of needing a third */
@@ -1739,8 +1749,8 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         }
     }
     free(S);
-    if (getenv("ORACLE_PASS_WASTE")) {  /* experiments: coded decisions PCRD discards, by pass */
-        FILE *f = fopen(getenv("ORACLE_PASS_WASTE"), "a");
+    if (ORACLE_EXP("ORACLE_PASS_WASTE")) {  /* experiments: coded decisions PCRD discards, by pass */
+        FILE *f = fopen(ORACLE_EXP("ORACLE_PASS_WASTE"), "a");
         int64_t all = 0, kept = 0, lost[3] = {0, 0, 0}, lost_last[3] = {0, 0, 0}, lost_plane = 0;
         for (int i = 0; f && i < E.nall; i++) {
             cblk *b = E.all[i];

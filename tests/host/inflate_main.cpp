@@ -33,11 +33,14 @@ using std::min;
 // [[MAIN]]
 using namespace jp2hip;
 
-static int run(const std::vector<uint8_t> &z, int off, const std::vector<uint8_t> &raw) {
+// lnk_init: what the link buffer holds before the decode (a fresh context's
+// hipMalloc memory may hold zeros, a reused one stale links of another image)
+static int run(const std::vector<uint8_t> &z, int off, const std::vector<uint8_t> &raw,
+               uint32_t lnk_init = 0xDEADBEEFu) {
     std::vector<uint8_t> buf(z.size() + 16, 0xA5);
     std::memcpy(buf.data() + off, z.data(), z.size());
     std::vector<uint8_t> out(raw.size() + 256);
-    std::vector<uint32_t> lnk(raw.size() + 256, 0xDEADBEEFu);
+    std::vector<uint32_t> lnk(raw.size() + 256, lnk_init);
     uint64_t o = off, c = z.size();
     int err = 0;
     UnpackArgs a{};
@@ -46,8 +49,9 @@ static int run(const std::vector<uint8_t> &z, int off, const std::vector<uint8_t
     a.lnk = lnk.data();
     blockIdx.x = 0; blockIdx.y = 0; threadIdx.x = 0;
     k_inflate(a);
-    if (err) return 1;
-    // k_inflate_links as the GPU runs it: doubling rounds, then the chase
+    // k_inflate_links as the GPU runs it (also after a failed decode: it is
+    // launched unconditionally, so it must end in bounds on any link
+    // contents): doubling rounds, then the chase
     const int chunks = (int)((raw.size() + kLinkChunk - 1) / kLinkChunk);
     for (int r = 0; r <= kLinkDoublings; r++)
         for (int bx = 0; bx < chunks; bx++)
@@ -56,6 +60,7 @@ static int run(const std::vector<uint8_t> &z, int off, const std::vector<uint8_t
                 k_inflate_links(a, r == kLinkDoublings ? 1 : 0);
             }
     blockIdx.x = 0; threadIdx.x = 0;
+    if (err) return 1;
     return std::memcmp(out.data(), raw.data(), raw.size()) ? 2 : 0;
 }
 
@@ -81,6 +86,13 @@ int main() {
         const int rt = run(t, 1, raw);
         printf("level %d truncated -> %d\n", lvl, rt);
         fails += rt != 1;
+        // the same with a zeroed / self-referencing link buffer (ADVICE r4:
+        // a zero link used to chase L[0] = 0 forever)
+        for (uint32_t init : {0u, 5u, 0x7FFFFFFFu}) {
+            const int rz = run(t, 1, raw, init);
+            printf("level %d truncated, links preset %u -> %d\n", lvl, init, rz);
+            fails += rz != 1;
+        }
     }
     uLongf cl = compressBound(raw.size());
     std::vector<uint8_t> z(cl);
@@ -90,6 +102,9 @@ int main() {
     const int rb = run(z, 0, raw);
     printf("reserved block -> %d\n", rb);
     fails += rb != 1;
+    const int rb0 = run(z, 0, raw, 0u);
+    printf("reserved block, links preset 0 -> %d\n", rb0);
+    fails += rb0 != 1;
     // long runs: chains of matches of matches (the links' doubling + chase),
     // and the strip ending inside a match / inside a stored block (a decoded
     // stream longer than the strip is cut, as libtiff does)

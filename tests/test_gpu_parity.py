@@ -286,6 +286,27 @@ def test_corrupt_deflate_strip_fails_loudly(encoder, damage):
         encoder.encode_tiff(bytes(data), jp2hip.LOSSLESS)
 
 
+def test_corrupt_deflate_first_decode_of_fresh_context():
+    """a corrupt Deflate strip as the FIRST Deflate decode of a new
+    context (its link buffer fresh from hipMalloc, never holding valid links)
+    fails as corrupt -- k_inflate fills the strip's unwritten links and
+    k_inflate_links follows only backward links -- and the context then
+    encodes a good Deflate TIFF normally."""
+    img = im.synth_rgb8(64, 64, seed=1)
+    good = im.tiff_bytes_compressed(img, "tiff_adobe_deflate", rows_per_strip=32)
+    data = bytearray(good)
+    lay, keep = jp2hip.tiff_layout(bytes(data))
+    data[lay.strip_offsets[1] + 2] = 0x07  # BFINAL 1, BTYPE 3 (reserved)
+    enc = jp2hip.Encoder(0)
+    try:
+        with pytest.raises(jp2hip.Jp2hipError, match="corrupt"):
+            enc.encode_tiff(bytes(data), jp2hip.LOSSLESS)
+        got, _ = enc.encode_tiff(good, jp2hip.LOSSLESS)
+        assert got == ol.encode(img, ol.copy_recipe(jp2hip.recipe(jp2hip.LOSSLESS)))
+    finally:
+        enc.close()
+
+
 def test_inflate_every_match_distance_and_length(encoder):
     """the lane-strided match copies (dist >= 64 rounds and the
     overlapping dist < 64 pattern) and the window flushes, on crafted

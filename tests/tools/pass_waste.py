@@ -11,8 +11,12 @@ if len(sys.argv) > 2:
     os.environ["ORACLE_SKIP_MARGIN"] = sys.argv[2]
 out = tempfile.mktemp(suffix=".jsonl")
 os.environ["ORACLE_PASS_WASTE"] = out
+import subprocess  # noqa: E402
 import bench  # noqa: E402
 import oracle_lib as ol  # noqa: E402
+# the hooks exist only in the experiments build of the oracle
+subprocess.run(["make", "-s", "-C", os.path.join(HERE, "..", "..", "oracle"), "experiments"], check=True)
+ol.LIB = os.path.join(os.path.dirname(ol.LIB), "liboracle_exp.so")
 img = bench.make_image("c2", seed=1234)
 rc = ol.recipe(False)
 data = ol.encode(img, rc)
