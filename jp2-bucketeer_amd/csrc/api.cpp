@@ -568,7 +568,8 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     int iters = 0;
     int64_t cs_bytes = 0;
     if (rc.rate_bpp <= 0.0) {
-        // lossless: layer l keeps every pass whose slope clears total >> (L-1-l)
+        // lossless: per -flush_period stripe, layer l keeps the passes whose
+        // slopes clear lossless_layer_frac(l) of the stripe's tier-1 bytes
         if (!ctx->gpu.select_lossless(plan, err) || !ctx->gpu.t2_size(plan, true, prof, st, sum, err))
             return fail(err);
         if (sum.err) return fail("tier-1 output capacity exceeded");
@@ -742,23 +743,45 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
             skip_target = 0;
             iters = 0;
         }
+        if (rc.rate_bpp <= 0.0) {
+            // lossless: every -flush_period stripe's layers come from its own
+            // tier-1 bytes (the plan's rate-control groups; a rank holds
+            // whole stripes), so the selection needs no exchange -- only the
+            // part sizes, the Kdu-Layer-Info bytes and each layer's slope
+            // key (the largest over the ranks' stripes) are shared
+            bool rok = ok && (!have || (ctx->gpu.select_lossless(sub, err) && ctx->gpu.t2_size(sub, true, prof, st, sum, err)));
+            if (rok && have && sum.err) {
+                rok = false;
+                err = "tier-1 output capacity exceeded";
+            }
+            std::vector<int64_t> v((size_t)L + 3 + (size_t)world * L, 0);
+            v[1] = rok ? 0 : 1;
+            if (rok && have) {
+                v[0] = sum.part_bytes;
+                v[2] = sum.tp_hdr_bytes;
+                for (int l = 0; l < L; l++) {
+                    v[3 + l] = sum.layer_bytes[l];
+                    v[3 + L + (size_t)rank * L + l] = (int64_t)sum.kc[l];  // (keys of positive doubles: < 2^63)
+                }
+            }
+            if (!allreduce(v.data(), (int)v.size())) return fail("split: all-reduce failed");
+            if (v[1]) return fail(rok ? std::string("split: another rank failed") : err);
+            cs_bytes = (int64_t)mh.size() + 2 + v[0];
+            g_tp_hdr = v[2];
+            g_layer.assign(v.begin() + 3, v.begin() + 3 + L);
+            for (int l = 0; l < L; l++) {
+                K[l] = 0;
+                for (int r = 0; r < world; r++) K[l] = std::max(K[l], (uint64_t)v[3 + L + (size_t)r * L + l]);
+            }
+            iters = 1;
+            break;
+        }
         ok = ok && (!have || ctx->gpu.segments(sub, keys, cum, err));
         {
             int64_t flag = ok ? 0 : 1;
             if (!allreduce(&flag, 1)) return fail("split: all-reduce failed");
             if (!ok) return fail(err);
             if (flag) return fail("split: another rank failed");
-        }
-        if (rc.rate_bpp <= 0.0) {
-            int64_t total = 0;
-            if (have && !ctx->gpu.t1_totals(sub, total, err)) ok = false;
-            int64_t v[2] = {total, ok ? 0 : 1};
-            if (!allreduce(v, 2)) return fail("split: all-reduce failed");
-            if (!ok) return fail(err);
-            if (v[1]) return fail("split: another rank failed");
-            for (int l = 0; l < L; l++) budgets[l] = v[0] >> (L - 1 - l);
-            if (!round()) return fail(err);
-            break;
         }
         const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)full.w * (double)full.h / 8.0);
         int64_t budget = target - 12 * full.npackets - 16 * full.ntileparts - 256;

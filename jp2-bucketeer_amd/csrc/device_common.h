@@ -158,6 +158,18 @@ __device__ __forceinline__ uint64_t wg_excl_scan64(uint64_t n, uint64_t *wsum, u
     return ex;
 }
 
+// The rate-control group of block b (Plan::grp_b0: ngroups + 1 ascending
+// block indices): the last g with grp_b0[g] <= b
+__device__ __forceinline__ int block_group(const int32_t *grp_b0, int ngroups, int b) {
+    int lo = 0, hi = ngroups - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (grp_b0[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 // --------------------------------------------------------------------------
 // Device rate loop (RateState, jp2hip_internal.h): the same arithmetic as the
 // oracle's loop (oracle_encode, rate_bpp > 0).  One step, after a tier-2

@@ -147,11 +147,9 @@ class GpuEncoder {
     bool run_front(const void *d_src, const jp2hip_layout &lay, const Plan &plan, bool profile,
                    StageTimes &st, std::string &err, int64_t skip_target = 0,
                    const HistReduce *reduce = nullptr);
-    // layer thresholds for the given data budgets -> per-block layer tables
-    // in HBM (enqueued only; t2_size reads the result)
-    bool select(const Plan &plan, const std::vector<int64_t> &budgets, std::string &err);
-    // lossless "-rate -": budgets total >> (L-1-l) from the tier-1 lengths,
-    // computed on the device
+    // lossless "-rate -": per -flush_period stripe (the plan's rate-control
+    // groups), layer budgets lossless_layer_frac of the stripe's tier-1
+    // bytes, computed on the device (enqueued only; t2_size reads the result)
     bool select_lossless(const Plan &plan, std::string &err);
     // per-block layer tables for explicit slope thresholds K[layer]
     // (tile-split: thresholds agreed across ranks)
@@ -173,8 +171,6 @@ class GpuEncoder {
     // host_dst must be pinned (hipHostMalloc) memory
     bool t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
                  StageTimes &st, std::string &err);
-    // tier-1 totals (one host wait; the tile-split path's lossless budget)
-    bool t1_totals(const Plan &plan, int64_t &bytes, std::string &err);
     // stage times of the last encode from its events (profile mode; call
     // after the encode's last host wait)
     bool collect_profile(StageTimes &st, std::string &err);
@@ -227,6 +223,9 @@ class GpuEncoder {
     // PCRD selection (k_hull / k_select): slope-bin histogram, ticket + list
     // fills, candidate lists
     DevBuf pcrd_hb, pcrd_hc, sel_ctl, sel_key, sel_size;
+    // rate-control groups (Plan::grp_b0, then each group's first candidate
+    // slot) and each group's tier-1 bytes (k_hull)
+    DevBuf grptab, gtot;
     // device tier-2 (t2_device.hip)
     DevBuf hdist, rstate, t2ticket;
     RateState *h_rs = nullptr;      // host-mapped: rate state, then the T2Summary (k_rate_step)

@@ -93,6 +93,15 @@ struct Plan {
     // [tile0, tile0 + ntc/nc) = image rows [row0, row0 + band_h); its blocks
     // are the full plan's blocks [block0, block0 + blocks.size())
     int row0 = 0, band_h = 0, tile0 = 0, block0 = 0;
+    // first block of each tile of this plan (tiles in raster order; blocks
+    // are emitted tile by tile), ntiles + 1 entries
+    std::vector<int32_t> tile_b0;
+    // rate-control groups: block ranges [grp_b0[g], grp_b0[g + 1]) whose
+    // layer thresholds are chosen together.  Lossless ("-rate -"): one group
+    // per -flush_period stripe (each stripe's layers from its own tier-1
+    // bytes, oracle lossless_budget); rate-driven: the whole image, one group
+    std::vector<int32_t> grp_b0;
+    int ngroups() const { return (int)grp_b0.size() - 1; }
     // identity of this plan's contents (build_plan / make_subplan): a device
     // context that already holds the tables of generation `gen` skips
     // uploading them again
@@ -103,6 +112,12 @@ bool build_plan(Plan &plan, const jp2hip_recipe &rc, int w, int h, int nc, int b
                 std::string &err);
 
 int prec_log2(const jp2hip_recipe &rc, int r, bool vertical);
+
+// Lossless layer l of NL: the fraction (1/65536 units) of its stripe's
+// tier-1 bytes the layer's threshold fits (oracle/jp2_oracle.c
+// lossless_layer_frac, fitted to test.jpx's Kdu-Layer-Info); the last layer
+// takes every pass (65536).
+int32_t lossless_layer_frac(int l, int NL);
 
 // Tile rows grouped the way "-flush_period P" flushes them
 // (KakaduConverter.java:40; oracle flush_stripes): a stripe ends once the rows

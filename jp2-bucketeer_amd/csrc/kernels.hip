@@ -798,6 +798,7 @@ __global__ void __launch_bounds__(256) k_untile(const uint8_t *base, const uint6
 // Layout per block (uint64 words, lane c = column c, bit y = row y): B[p][64]
 // for p < Mb, then S[p][64] = OR_{q>=p} B[q], then sign[64].
 // --------------------------------------------------------------------------
+constexpr int kZeroSpans = 9;
 struct QuantArgs {
     const BlockDesc *blocks;
     const void *coef;
@@ -810,10 +811,10 @@ struct QuantArgs {
     int max_mb;            // largest Mb of the plan (LDS: max_mb * 512 bytes per wave)
     int keep_sm;           // write the sign-magnitude copy of every block (debug dumps)
     int nblocks;
-    // per-encode counters of later kernels, zeroed here by workgroup 0 (no
-    // memset launch): dword spans
-    uint32_t *zero[8];
-    uint32_t nzero[8];
+    // per-encode counters of later kernels, zeroed here (no memset launch):
+    // dword spans, spread over the workgroups
+    uint32_t *zero[kZeroSpans];
+    uint32_t nzero[kZeroSpans];
 };
 
 constexpr int kQuantWaves = 2;  // code-blocks (waves) per workgroup
@@ -822,10 +823,10 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     extern __shared__ uint64_t lds_planes[];  // [wave][plane][lane], a.max_mb planes per wave
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.x * kQuantWaves + wv;
-    if (blockIdx.x == 0)
 #pragma unroll
-        for (int z = 0; z < 8; z++)
-            for (uint32_t i = threadIdx.x; i < a.nzero[z]; i += 64 * kQuantWaves) a.zero[z][i] = 0u;
+    for (int z = 0; z < kZeroSpans; z++)
+        for (uint32_t i = blockIdx.x * 64 * kQuantWaves + threadIdx.x; i < a.nzero[z]; i += gridDim.x * 64 * kQuantWaves)
+            a.zero[z][i] = 0u;
     if (b >= a.nblocks) return;
     uint64_t *planes = lds_planes + (size_t)wv * a.max_mb * 64;
     BlockDesc d = a.blocks[b];
@@ -1147,8 +1148,10 @@ struct HullArgs {
     uint8_t *hpass;   // [block][kMaxPasses+1]
     uint64_t *hkey;   // [block][kMaxPasses+1]
     int64_t *hdist;   // [block][kMaxPasses+1] HullPt: the stack's distortion and rate at each point
-    unsigned long long *hbytes;  // [kPcrdBins] segment bytes per slope bin (zeroed by k_quant)
-    uint32_t *hcount;            // [kPcrdBins] segments per slope bin
+    unsigned long long *hbytes;  // [group][kPcrdBins] segment bytes per slope bin (zeroed by k_quant)
+    uint32_t *hcount;            // [group][kPcrdBins] segments per slope bin
+    const int32_t *grp_b0;       // rate-control groups' block ranges (Plan::grp_b0): grid.y = group
+    unsigned long long *gtot;    // [group] tier-1 bytes (lossless budgets; zeroed by k_quant)
     // the tier-1 totals of T2Summary (t1_bytes, coded_passes, decisions,
     // skipped; zeroed by k_quant), summed here once per encode instead of by
     // every rate iteration's totals
@@ -1271,10 +1274,12 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
         lc[i] = 0;
     }
     __syncthreads();
-    const int b = blockIdx.x * kHullThreads + threadIdx.x;
+    const int g = blockIdx.y, gb1 = a.grp_b0[g + 1];
+    const int b = a.grp_b0[g] + blockIdx.x * kHullThreads + threadIdx.x;
+    if (a.grp_b0[g] + blockIdx.x * kHullThreads >= gb1) return;  // (the whole workgroup)
     int64_t tb = 0, tp = 0, nd = 0;
     bool sk = false;
-    if (b < a.nblocks) {
+    if (b < gb1) {
         hull_one(a, b, lb, lc);
         tb = a.lengths[b];
         tp = a.npasses[b];
@@ -1286,6 +1291,7 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
     nd = wave_sum64(nd);
     sk = __any(sk);
     if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&a.gtot[g], (unsigned long long)tb);
         atomicAdd((unsigned long long *)&a.sum->t1_bytes, (unsigned long long)tb);
         atomicAdd((unsigned long long *)&a.sum->coded_passes, (unsigned long long)tp);
         atomicAdd((unsigned long long *)&a.sum->decisions, (unsigned long long)nd);
@@ -1294,8 +1300,8 @@ __global__ void __launch_bounds__(kHullThreads) k_hull(HullArgs a) {
     __syncthreads();
     for (int i = threadIdx.x; i < kPcrdBins; i += kHullThreads)
         if (lc[i]) {
-            atomicAdd(&a.hbytes[i], (unsigned long long)lb[i]);
-            atomicAdd(&a.hcount[i], lc[i]);
+            atomicAdd(&a.hbytes[(size_t)g * kPcrdBins + i], (unsigned long long)lb[i]);
+            atomicAdd(&a.hcount[(size_t)g * kPcrdBins + i], lc[i]);
         }
 }
 
@@ -1331,12 +1337,23 @@ struct SelectArgs {
     const uint8_t *nhull, *hpass;
     const uint64_t *hkey;
     const int32_t *rates;
+    // rate-control groups (grid.y = group): block ranges, first candidate
+    // slot (the bound on the hull segments of the groups before), and per
+    // group: histogram kPcrdBins apart, budgets / thresholds kMaxLayers
+    // apart, list fills kMaxLayers + 1 apart
+    const int32_t *grp_b0;
+    const uint32_t *grp_seg0;
     const unsigned long long *hbytes;
     const uint32_t *hcount;
     const int64_t *budget;
+    // lossless: group g's layer-l budget is gtot[g] * frac[l] >> 16 (the
+    // group's tier-1 bytes, k_hull), not budget[]
+    int lossless;
+    const unsigned long long *gtot;
+    int32_t frac[kMaxLayers];
     uint64_t *lkey;   // candidate lists, capacity >= every hull segment
     uint32_t *lsize;
-    uint32_t *ctl;    // [1 + i] fill of list i ([0] unused)
+    uint32_t *ctl;    // [group][1 + i] fill of list i ([0] unused)
     uint64_t *K, *Kc;
     int64_t *dbg;     // debug builds: [0] lists, [1 + i] list sizes, [33 + l] rounds, [65 + l] survivors
 };
@@ -1363,8 +1380,10 @@ struct SelBins {
 // instead of a 32 KB table per bin (and no 4 KB bin -> list map): a layer's
 // bin is found by a binary search over the chunks, then a walk down its
 // chunk's bins (re-read from L2).
-__device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
+__device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh, int g) {
     const int tid = threadIdx.x, L = a.layers;
+    const unsigned long long *hbytes = a.hbytes + (size_t)g * kPcrdBins;
+    const uint32_t *hcount = a.hcount + (size_t)g * kPcrdBins;
     uint64_t *csfx = sh.csfx;
     int *lbin = sh.lbin, *lli = sh.lli, *list_bin = sh.list_bin;
     int64_t *lneed = sh.lneed;
@@ -1372,7 +1391,7 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
     {
         uint64_t s = 0;
 #pragma unroll
-        for (int i = 0; i < kSelPer; i++) s += a.hbytes[kSelPer * tid + i];
+        for (int i = 0; i < kSelPer; i++) s += hbytes[kSelPer * tid + i];
         uint64_t tot;
         const uint64_t pre = wg_excl_scan64<kSelThreads>(s, sh.wsum, tot);
         csfx[tid] = tot - pre;
@@ -1381,7 +1400,9 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
     __syncthreads();
     if (tid < L) {
         // (a negative budget takes nothing, as 0 does: every segment has bytes)
-        const int64_t B = a.init_on ? (a.init.budget < 0 ? 0 : a.init.budget) >> (L - 1 - tid) : a.budget[tid];
+        const int64_t B = a.init_on    ? (a.init.budget < 0 ? 0 : a.init.budget) >> (L - 1 - tid)
+                          : a.lossless ? (int64_t)((a.gtot[g] * (unsigned long long)a.frac[tid]) >> 16)
+                                       : a.budget[(size_t)g * kMaxLayers + tid];
         const int64_t T = B < 0 ? 0 : B;
         int b = -1;
         int64_t above = 0;  // S(b + 1)
@@ -1396,7 +1417,7 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
             // ... then its largest bin b with S(b) > T
             uint64_t S = csfx[lo + 1];
             for (int i = kSelPer - 1; i >= 0; i--) {
-                const uint64_t Sb = S + a.hbytes[kSelPer * lo + i];
+                const uint64_t Sb = S + hbytes[kSelPer * lo + i];
                 if ((int64_t)Sb > T) {
                     b = kSelPer * lo + i;
                     break;
@@ -1419,7 +1440,7 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
             if (i == n) {
                 list_bin[n] = lbin[l];
                 list_off[n] = o;
-                o += a.hcount[lbin[l]];
+                o += hcount[lbin[l]];
                 n++;
             }
             lli[l] = i;
@@ -1432,9 +1453,10 @@ __device__ __forceinline__ void select_bins(const SelectArgs &a, SelBins &sh) {
 
 __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
     __shared__ SelBins sh;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, g = blockIdx.y;
     if (!a.init_on && a.halt && *a.halt) return;
-    if (a.init_on && blockIdx.x == 0 && tid == 0) {  // the rate loop's state (rate_step continues it)
+    const int gb0 = a.grp_b0[g], gb1 = a.grp_b0[g + 1];
+    if (a.init_on && blockIdx.x == 0 && g == 0 && tid == 0) {  // the rate loop's state (rate_step continues it)
         RateState r = a.init;
         r.it = 0;
         r.halt = 0;
@@ -1445,13 +1467,16 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
         *a.rs = r;
         rate_budgets(r, a.layers, a.budget_w);
     }
-    select_bins(a, sh);
+    if (gb0 + (int)blockIdx.x * kSelThreads >= gb1) return;  // (the whole workgroup)
+    select_bins(a, sh, g);
     const uint32_t *list_off = sh.list_off;
     const int *list_bin = sh.list_bin;
     const int nlist = sh.nlist;
-    // 2. candidates of those bins, thread per code-block
+    const uint32_t seg0 = a.grp_seg0[g];
+    uint32_t *ctl = a.ctl + (size_t)g * (kMaxLayers + 1);
+    // 2. candidates of those bins, thread per code-block of the group
     if (nlist > 0)
-        for (int b = blockIdx.x * kSelThreads + tid; b < a.nblocks; b += gridDim.x * kSelThreads) {
+        for (int b = gb0 + blockIdx.x * kSelThreads + tid; b < gb1; b += gridDim.x * kSelThreads) {
             const int nh = a.nhull[b];
             const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
             const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
@@ -1477,11 +1502,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
                         const int lj = __shfl(li, lead, 64);
                         const uint64_t grp = __ballot(li == lj);
                         uint32_t base = 0;
-                        if (lane == lead) base = atomicAdd(&a.ctl[1 + lj], (uint32_t)__popcll(grp));
+                        if (lane == lead) base = atomicAdd(&ctl[1 + lj], (uint32_t)__popcll(grp));
                         base = (uint32_t)__shfl((int)base, lead, 64);
                         if (li == lj) {
                             const uint32_t at =
-                                list_off[lj] + base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+                                seg0 + list_off[lj] + base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
                             a.lkey[at] = key;
                             a.lsize[at] = (uint32_t)(R[hp[i] - 1] - (hp[i - 1] ? R[hp[i - 1] - 1] : 0));
                         }
@@ -1507,16 +1532,18 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
     __shared__ uint32_t bsize[kSelBrute];
     __shared__ uint64_t hist[kResBins];
     __shared__ uint32_t hcnt[kResBins];
-    const int tid = threadIdx.x, lane = tid & 63, l = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, l = blockIdx.x, g = blockIdx.y;
     if (a.halt && *a.halt) return;  // (k_select has reset it on a first iteration)
-    select_bins(a, sh);
+    select_bins(a, sh, g);
     uint64_t *wsum = sh.wsum;
     const int *lbin = sh.lbin, *lli = sh.lli;
     const int64_t *lneed = sh.lneed;
     const uint32_t *list_off = sh.list_off;
     const int nlist = sh.nlist;
-    if (l == 0 && tid <= nlist) a.ctl[tid] = 0u;  // (k_select has finished: stream order)
-    if (a.dbg && l == 0 && tid == 0) {
+    const uint32_t seg0 = a.grp_seg0[g];
+    uint64_t *Kg = a.K + (size_t)g * kMaxLayers, *Kcg = a.Kc + (size_t)g * kMaxLayers;
+    if (l == 0 && tid <= nlist) a.ctl[(size_t)g * (kMaxLayers + 1) + tid] = 0u;  // (k_select has finished: stream order)
+    if (a.dbg && l == 0 && g == 0 && tid == 0) {
         a.dbg[0] = nlist;
         for (int i = 0; i < nlist; i++) a.dbg[1 + i] = list_off[i + 1] - list_off[i];
     }
@@ -1527,11 +1554,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
     // kSelBrute remain, whose totals are then summed directly.
     {
         if (lbin[l] < 0) {
-            if (tid == 0) a.K[l] = a.Kc[l] = 0ull;  // every segment fits
+            if (tid == 0) Kg[l] = Kcg[l] = 0ull;  // every segment fits
             return;
         }
         const int li = lli[l];
-        const uint32_t i0 = list_off[li], i1 = list_off[li + 1];
+        const uint32_t i0 = seg0 + list_off[li], i1 = seg0 + list_off[li + 1];
         const int bn = lbin[l];
         if (tid == 0) {
             rcount = i1 - i0;
@@ -1596,8 +1623,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
                 }
                 __syncthreads();
                 if (tid == 0) {
-                    a.K[l] = a.Kc[l] = rmax + 1;
-                    if (a.dbg) {
+                    Kg[l] = Kcg[l] = rmax + 1;
+                    if (a.dbg && g == 0) {
                         a.dbg[33 + l] = round;
                         a.dbg[65 + l] = cnt;
                     }
@@ -1735,6 +1762,8 @@ __device__ __forceinline__ int hull_pick(const uint64_t *hk, int nh, uint64_t K)
 struct ApplyArgs {
     const int *halt;  // device rate loop: nothing to do once it has stopped
     int nblocks, layers, lossless;
+    int ngroups;
+    const int32_t *grp_b0;  // the block's rate-control group: its thresholds at K + group * kMaxLayers
     const uint8_t *nhull, *hpass, *npasses;
     const uint64_t *hkey, *K;
     const int32_t *rates;
@@ -1750,8 +1779,9 @@ __global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
     const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
     const int32_t *R = a.rates + (size_t)b * kMaxPasses;
     int nh = a.nhull[b];
+    const uint64_t *K = a.K + (size_t)block_group(a.grp_b0, a.ngroups, b) * kMaxLayers;
     for (int l = 0; l < L; l++) {
-        int n = (a.lossless && l == L - 1) ? (int)a.npasses[b] : (int)hp[hull_pick(hk, nh, a.K[l])];
+        int n = (a.lossless && l == L - 1) ? (int)a.npasses[b] : (int)hp[hull_pick(hk, nh, K[l])];
         a.nl[(size_t)b * L + l] = (uint8_t)n;
         a.lrate[(size_t)b * L + l] = n ? R[n - 1] : 0;
     }
@@ -1786,6 +1816,13 @@ static bool ensure(DevBuf &b, size_t count, std::string &err) {
     return true;
 }
 
+// the largest rate-control group (its blocks set the grid's x extent)
+static int grp_max_blocks(const Plan &plan) {
+    int m = 0;
+    for (int g = 0; g < plan.ngroups(); g++) m = std::max(m, plan.grp_b0[(size_t)g + 1] - plan.grp_b0[(size_t)g]);
+    return std::max(m, 1);
+}
+
 GpuEncoder::~GpuEncoder() {
     DevBuf *all[] = {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
                      &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
@@ -1794,7 +1831,7 @@ GpuEncoder::~GpuEncoder() {
                      &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
                      &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
                      &t2blkdst, &t2out, &t2sum, &hdist, &rstate, &t2ticket,
-                     &t1fill, &dbgsel};
+                     &t1fill, &dbgsel, &grptab, &gtot};
     for (DevBuf *b : all)
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
@@ -2053,7 +2090,8 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<uint8_t>(hpass, (size_t)nb * (kMaxPasses + 1), err)) return false;
     if (!ensure<uint64_t>(hkey, (size_t)nb * (kMaxPasses + 1), err)) return false;
     if (!ensure<int64_t>(hdist, (size_t)nb * (kMaxPasses + 1) * 2, err)) return false;  // HullPt
-    if (!ensure<int64_t>(budget, kMaxLayers, err)) return false;
+    const int G = plan.ngroups();
+    if (!ensure<int64_t>(budget, (size_t)G * kMaxLayers, err)) return false;
     if (!ensure<uint8_t>(nl, (size_t)nb * plan.rc.layers, err)) return false;
     if (!ensure<int32_t>(lrate, (size_t)nb * plan.rc.layers, err)) return false;
     if (!ensure<int>(this->err, 4, err)) return false;
@@ -2092,6 +2130,19 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
             o += (uint64_t)plan.blocks[i].Mb * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
         }
         if (nb && !h2d(slotoff.ptr, slots.data(), sizeof(uint64_t) * nb, err)) return false;
+        // rate-control groups: block ranges and each group's first
+        // candidate slot (the bound sum(3 Mb - 2) over the groups before)
+        std::vector<int32_t> gtab(2 * ((size_t)G + 1));
+        int64_t sb = 0;
+        for (int g = 0; g <= G; g++) {
+            gtab[(size_t)g] = plan.grp_b0[(size_t)g];
+            gtab[(size_t)G + 1 + g] = (int32_t)sb;
+            if (g < G)
+                for (int i = plan.grp_b0[(size_t)g]; i < plan.grp_b0[(size_t)g + 1]; i++)
+                    sb += std::max(0, 3 * (int)plan.blocks[i].Mb - 2);
+        }
+        if (!ensure<int32_t>(grptab, gtab.size(), err) || !h2d(grptab.ptr, gtab.data(), sizeof(int32_t) * gtab.size(), err))
+            return false;
         front_gen = plan.gen;
     }
     // (the error word is zeroed by k_quant, which every encode with blocks runs)
@@ -2172,8 +2223,10 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     int kmax = 0;
     for (int i = 0; i < nb; i++) kmax = std::max(kmax, (int)plan.blocks[i].Mb);
     const size_t nflags = (size_t)nb * kmax;
-    if (!ensure<unsigned long long>(pcrd_hb, kPcrdBins, err) || !ensure<uint32_t>(pcrd_hc, kPcrdBins, err) ||
-        !ensure<uint32_t>(sel_ctl, kMaxLayers + 1, err) || !ensure<uint32_t>(t1fill, 64 + kOrderBuckets, err) ||
+    if (!ensure<unsigned long long>(pcrd_hb, (size_t)G * kPcrdBins, err) ||
+        !ensure<uint32_t>(pcrd_hc, (size_t)G * kPcrdBins, err) ||
+        !ensure<uint32_t>(sel_ctl, (size_t)G * (kMaxLayers + 1), err) ||
+        !ensure<unsigned long long>(gtot, G, err) || !ensure<uint32_t>(t1fill, 64 + kOrderBuckets, err) ||
         !ensure<int32_t>(items, std::max<size_t>(nflags, 1), err) ||
         !ensure<int32_t>(order, (size_t)kOrderBuckets * std::max(nb, 1), err) ||
         !ensure<uint4>(counts, (size_t)nb * 32, err) || !ensure<int64_t>(dspp, (size_t)nb * 32, err) ||
@@ -2183,15 +2236,19 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     std::memset(qa.zero, 0, sizeof qa.zero);
     std::memset(qa.nzero, 0, sizeof qa.nzero);
     qa.zero[0] = (uint32_t *)pcrd_hb.ptr;
-    qa.nzero[0] = 2 * kPcrdBins;
+    qa.nzero[0] = 2 * kPcrdBins * G;
     qa.zero[1] = (uint32_t *)pcrd_hc.ptr;
-    qa.nzero[1] = kPcrdBins;
+    qa.nzero[1] = kPcrdBins * G;
     qa.zero[2] = (uint32_t *)sel_ctl.ptr;
-    qa.nzero[2] = kMaxLayers + 1;
+    qa.nzero[2] = (kMaxLayers + 1) * G;
     qa.zero[3] = dfill;
     qa.nzero[3] = 64 + kOrderBuckets;
     qa.zero[4] = (uint32_t *)mqspan.ptr;
     qa.nzero[4] = 4;
+    // (span 5: the error word; span 6: the slope histogram; span 7: tier-1
+    // totals; span 8: the rate-control groups' tier-1 bytes)
+    qa.zero[8] = (uint32_t *)gtot.ptr;
+    qa.nzero[8] = 2 * G;
     qa.zero[5] = (uint32_t *)this->err.ptr;
     qa.nzero[5] = 1;
     // the tier-1 totals k_hull sums (t1_bytes .. skipped: contiguous)
@@ -2329,14 +2386,17 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ha.acc = (const unsigned long long *)ordkey.ptr;
     ha.pmin = (const uint8_t *)pmin.ptr;
     ha.sum = (T2Summary *)t2sum.ptr;
-    REPEAT_IF(4) if (nb) hipLaunchKernelGGL(k_hull, dim3((nb + kHullThreads - 1) / kHullThreads), dim3(kHullThreads), 0, stream, ha);
+    ha.grp_b0 = (const int32_t *)grptab.ptr;
+    ha.gtot = (unsigned long long *)gtot.ptr;
+    REPEAT_IF(4) if (nb) hipLaunchKernelGGL(k_hull, dim3((grp_max_blocks(plan) + kHullThreads - 1) / kHullThreads, G),
+                                            dim3(kHullThreads), 0, stream, ha);
     HIPCHECK(hipGetLastError());
     // candidate lists: room for every hull segment (the bound sum(3 Mb - 2))
     int64_t nseg_bound = 0;
     for (int i = 0; i < nb; i++) nseg_bound += std::max(0, 3 * (int)plan.blocks[i].Mb - 2);
     nseg = (int)nseg_bound;
     if (!ensure<uint64_t>(sel_key, std::max(nseg, 1), err) || !ensure<uint32_t>(sel_size, std::max(nseg, 1), err) ||
-        !ensure<uint64_t>(thr, 2 * kMaxLayers, err))
+        !ensure<uint64_t>(thr, 2 * (size_t)G * kMaxLayers, err))
         return false;
     HIPCHECK(hipEventRecord(ev[5], stream));
     profiled = profile;
@@ -2378,21 +2438,14 @@ bool GpuEncoder::collect_profile(StageTimes &st, std::string &err) {
     return true;
 }
 
-bool GpuEncoder::select(const Plan &plan, const std::vector<int64_t> &budgets, std::string &err) {
-    HIPCHECK(hipSetDevice(device));
-    const int L = plan.rc.layers;
-    if (!h2d(budget.ptr, budgets.data(), sizeof(int64_t) * L, err)) return false;
-    HIPCHECK(hipEventRecord(ev[6], stream));
-    select_launch(plan, nullptr);
-    HIPCHECK(hipGetLastError());
-    return apply_thresholds(plan, nullptr, err);
-}
-
-// k_select for the budgets in `budget` (thresholds -> thr[0..L), Kc -> thr[kMaxLayers..))
+// k_select per rate-control group: lossless budgets from each group's tier-1
+// bytes, else from `budget` (the device rate loop's) -- thresholds of group g
+// -> thr[g * kMaxLayers ..), Kc -> thr[(G + g) * kMaxLayers ..)
 void GpuEncoder::select_launch(const Plan &plan, const int *halt, const RateState *init, RateState *rs) {
-    const int nb = (int)plan.blocks.size();
+    const int nb = (int)plan.blocks.size(), G = plan.ngroups();
     if (!nb) return;
     SelectArgs sa;
+    std::memset(&sa, 0, sizeof sa);
     sa.halt = halt;
     sa.nblocks = nb;
     sa.layers = plan.rc.layers;
@@ -2407,7 +2460,12 @@ void GpuEncoder::select_launch(const Plan &plan, const int *halt, const RateStat
     sa.lsize = (uint32_t *)sel_size.ptr;
     sa.ctl = (uint32_t *)sel_ctl.ptr;
     sa.K = (uint64_t *)thr.ptr;
-    sa.Kc = (uint64_t *)thr.ptr + kMaxLayers;
+    sa.Kc = (uint64_t *)thr.ptr + (size_t)G * kMaxLayers;
+    sa.grp_b0 = (const int32_t *)grptab.ptr;
+    sa.grp_seg0 = (const uint32_t *)grptab.ptr + G + 1;
+    sa.lossless = plan.rc.rate_bpp <= 0.0;
+    sa.gtot = (const unsigned long long *)gtot.ptr;
+    for (int l = 0; l < plan.rc.layers; l++) sa.frac[l] = lossless_layer_frac(l, plan.rc.layers);
     sa.init_on = init != nullptr;
     if (init) sa.init = *init;
     sa.rs = rs;
@@ -2419,32 +2477,17 @@ void GpuEncoder::select_launch(const Plan &plan, const int *halt, const RateStat
         if (ensure<int64_t>(dbgsel, 128, e)) sa.dbg = (int64_t *)dbgsel.ptr;
     }
 #endif
-    hipLaunchKernelGGL(k_select, dim3((nb + kSelThreads - 1) / kSelThreads), dim3(kSelThreads), 0, stream, sa);
-    hipLaunchKernelGGL(k_select_resolve, dim3(plan.rc.layers), dim3(kSelThreads), 0, stream, sa);
+    hipLaunchKernelGGL(k_select, dim3((grp_max_blocks(plan) + kSelThreads - 1) / kSelThreads, G), dim3(kSelThreads), 0,
+                       stream, sa);
+    hipLaunchKernelGGL(k_select_resolve, dim3(plan.rc.layers, G), dim3(kSelThreads), 0, stream, sa);
 }
 
-// lossless "-rate -": layer l's budget is total >> (L-1-l), total = every
-// coded byte (api.cpp encode_core restates the rule for the split path)
-__global__ void __launch_bounds__(256) k_budget_lossless(int nblocks, const int32_t *lengths, int layers,
-                                                         int64_t *budget) {
-    __shared__ int64_t part[256];
-    int64_t s = 0;
-    for (int b = threadIdx.x; b < nblocks; b += 256) s += lengths[b];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t tot = 0;
-        for (int i = 0; i < 256; i++) tot += part[i];
-        for (int l = 0; l < layers; l++) budget[l] = tot >> (layers - 1 - l);
-    }
-}
-
+// lossless "-rate -": each -flush_period stripe (rate-control group) keeps
+// per layer the passes that fit lossless_layer_frac of its own tier-1 bytes
+// (k_hull summed them per group); the last layer takes every pass
 bool GpuEncoder::select_lossless(const Plan &plan, std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    const int L = plan.rc.layers, nb = (int)plan.blocks.size();
     HIPCHECK(hipEventRecord(ev[6], stream));
-    hipLaunchKernelGGL(k_budget_lossless, dim3(1), dim3(256), 0, stream, nb, (const int32_t *)lengths.ptr, L,
-                       (int64_t *)budget.ptr);
     select_launch(plan, nullptr);
     HIPCHECK(hipGetLastError());
     return apply_thresholds(plan, nullptr, err);
@@ -2452,6 +2495,10 @@ bool GpuEncoder::select_lossless(const Plan &plan, std::string &err) {
 
 bool GpuEncoder::select_keys(const Plan &plan, const std::vector<uint64_t> &K, std::string &err) {
     HIPCHECK(hipSetDevice(device));
+    if (plan.ngroups() != 1) {
+        err = "select_keys: one rate-control group expected";
+        return false;
+    }
     if (!h2d(thr.ptr, K.data(), sizeof(uint64_t) * plan.rc.layers, err)) return false;
     HIPCHECK(hipEventRecord(ev[6], stream));
     return apply_thresholds(plan, nullptr, err);
@@ -2474,6 +2521,8 @@ bool GpuEncoder::apply_thresholds(const Plan &plan, const int *halt, std::string
     aa.rates = (const int32_t *)rates.ptr;
     aa.nl = (uint8_t *)nl.ptr;
     aa.lrate = (int32_t *)lrate.ptr;
+    aa.ngroups = plan.ngroups();
+    aa.grp_b0 = (const int32_t *)grptab.ptr;
     // (k_t2_wave assigns the layers itself in its sizing pass)
     if (nb && !t2_wave) hipLaunchKernelGGL(k_apply, dim3((nb + 255) / 256), dim3(256), 0, stream, aa);
     HIPCHECK(hipGetLastError());
@@ -2520,32 +2569,6 @@ bool GpuEncoder::rate_loop(const Plan &plan, const RateState &init, bool restart
         HIPCHECK(hipEventElapsedTime(&t, ev[6], ev[9]));
         st.t2 += t;
     }
-    return true;
-}
-
-// tier-1 byte total (tile-split lossless budget); one host wait
-__global__ void __launch_bounds__(256) k_sum_lengths(int nblocks, const int32_t *lengths, int64_t *out) {
-    __shared__ int64_t part[256];
-    int64_t s = 0;
-    for (int b = threadIdx.x; b < nblocks; b += 256) s += lengths[b];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t tot = 0;
-        for (int i = 0; i < 256; i++) tot += part[i];
-        *out = tot;
-    }
-}
-
-bool GpuEncoder::t1_totals(const Plan &plan, int64_t &bytes, std::string &err) {
-    HIPCHECK(hipSetDevice(device));
-    if (!ensure<int64_t>(hist, kSlopeBins, err)) return false;
-    hipLaunchKernelGGL(k_sum_lengths, dim3(1), dim3(256), 0, stream, (int)plan.blocks.size(),
-                       (const int32_t *)lengths.ptr, (int64_t *)hist.ptr);
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipMemcpyAsync(h_tot, hist.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
-    if (!host_wait(err)) return false;
-    bytes = h_tot[0];
     return true;
 }
 

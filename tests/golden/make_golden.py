@@ -68,14 +68,42 @@ def c5_full_sha(w=40000, h=30000):
             "oracle_sha256": hashlib.sha256(cs).hexdigest()}
 
 
+def c4_lossless():
+    """Lossless at full C4 size (BASELINE.json configs[3]: one 5000x7000 RGB8
+    batch image, seed 0, JPX as the batch writes it): the oracle file's
+    SHA-256 pins the GPU batch output without running the oracle there."""
+    import hashlib
+    import oracle_lib as ol
+    img = im.synth_rgb8(7000, 5000, seed=0)
+    cs = ol.encode(img, ol.recipe(True))
+    assert np.array_equal(im.decode_pillow(cs), img)
+    return [{"name": "c4_synth_rgb8_5000x7000_seed0_jpx", "oracle_bytes": len(cs),
+             "oracle_sha256": hashlib.sha256(cs).hexdigest()}]
+
+
+def kdu_layer_info(cs):
+    """(log2 slope, bytes) per quality layer from a Kdu-Layer-Info COM."""
+    p = cs.find(b"Kdu-Layer-Info")
+    n = int.from_bytes(cs[p - 4:p - 2], "big")
+    lines = cs[p:p + n - 4].decode("latin-1").splitlines()[1:]
+    return [[float(x.split(",")[0]), float(x.split(",")[1])] for x in lines]
+
+
 def main(only=None):
     if only:
-        # recompute the named lossy cases / the C5 file only, keep the rest
+        # recompute the named lossy cases / the C5 file / the C4 lossless
+        # file / test.jpx's layer info only, keep the rest
         g = json.load(open(os.path.join(HERE, "golden.json")))
-        pix = im.decode_opj(open(os.path.join(HERE, "test.jpx"), "rb").read(), ".j2k")
+        tj = open(os.path.join(HERE, "test.jpx"), "rb").read()
+        pix = im.decode_opj(tj, ".j2k")
         if "c5_full" in only:
             g["c5_full"] = c5_full_sha()
             print(g["c5_full"])
+        if "lossless" in only:
+            g["lossless"] = c4_lossless()
+            print(g["lossless"])
+        if "testjpx_layers" in only:
+            g["testjpx"]["kdu_layer_info"] = kdu_layer_info(tj)
         g["lossy"] = [c for c in g["lossy"] if c["name"] not in only]
         g["lossy"] += lossy_cases(pix, only)
         with open(os.path.join(HERE, "golden.json"), "w") as f:
@@ -97,18 +125,11 @@ def main(only=None):
         # every tile-part: (Isot, TPsot, TNsot), in code-stream order
         "tp_order": [[t[0], t[2], t[3]] for t in im.tile_parts(tj)],
         "min_size_assert": 30000,   # KakaduConverterTest.java:107
+        # Kakadu's (log2 slope, code-stream bytes through the layer) per layer
+        "kdu_layer_info": kdu_layer_info(tj),
     }
     g["lossy"] = lossy_cases(pix)
-    # lossless at full C4 size (BASELINE.json configs[3]: one 5000x7000 RGB8
-    # batch image, seed 0, JPX as the batch writes it): the oracle file's
-    # SHA-256 pins the GPU batch output without running the oracle there
-    import oracle_lib as ol
-    img = im.synth_rgb8(7000, 5000, seed=0)
-    cs = ol.encode(img, ol.recipe(True))
-    assert np.array_equal(im.decode_pillow(cs), img)
-    import hashlib
-    g["lossless"] = [{"name": "c4_synth_rgb8_5000x7000_seed0_jpx", "oracle_bytes": len(cs),
-                      "oracle_sha256": hashlib.sha256(cs).hexdigest()}]
+    g["lossless"] = c4_lossless()
     print(g["lossless"])
     g["c5_full"] = c5_full_sha()
     with open(os.path.join(HERE, "golden.json"), "w") as f:

@@ -88,6 +88,11 @@ def test_testjpx_pixels_lossless(encoder, testjpx_pixels, golden):
     assert [[t[0], t[2], t[3]] for t in im.tile_parts(got)] == g["tp_order"]
     assert np.array_equal(im.decode_pillow(got), testjpx_pixels)
     assert len(got) > g["min_size_assert"]
+    # Kakadu's quality layers: each layer's bytes
+    # within 10 % of test.jpx's Kdu-Layer-Info
+    from test_oracle import kdu_layer_bytes
+    for got_l, ref_l in zip(kdu_layer_bytes(got), [b for _, b in g["kdu_layer_info"]]):
+        assert abs(got_l - ref_l) / ref_l < 0.10
 
 
 def _golden_lossy_names():

@@ -79,6 +79,65 @@ def test_oracle_com_markers_follow_kakadu_layout(testjpx_pixels, testjpx_bytes):
     assert abs(last - len(cs)) / len(cs) < 0.05
 
 
+def kdu_layer_bytes(cs):
+    """Code-stream bytes through each layer, from a Kdu-Layer-Info COM."""
+    p = cs.find(b"Kdu-Layer-Info")
+    n = int.from_bytes(cs[p - 4:p - 2], "big")
+    return [float(x.split(",")[1]) for x in cs[p:p + n - 4].decode("latin-1").splitlines()[1:]]
+
+
+def test_oracle_lossless_layers_match_testjpx(testjpx_pixels, golden):
+    """the lossless recipe's quality layers
+    (Clayers=6 with "-rate -", KakaduConverter.java:38-42) hold the bytes
+    Kakadu's do on the reference fixture -- each layer's L within 10 % of
+    test.jpx's Kdu-Layer-Info (5.1e4 .. 3.0e5 B; the oracle's own COM prints
+    the same %8.1e column)."""
+    cs = ol.encode(testjpx_pixels, ol.recipe(True, format=0))
+    ref = [b for _, b in golden["testjpx"]["kdu_layer_info"]]
+    got = kdu_layer_bytes(cs)
+    assert len(got) == len(ref) == 6
+    for g, r in zip(got, ref):
+        assert abs(g - r) / r < 0.10, (got, ref)
+
+
+def tile_part_bytes(cs):
+    """{(tile, TPsot): tile-part bytes} of a raw code-stream."""
+    out, p = {}, cs.find(b"\xff\x90")
+    while p >= 0 and cs[p:p + 2] == b"\xff\x90":
+        n = int.from_bytes(cs[p + 6:p + 10], "big")
+        out[(int.from_bytes(cs[p + 4:p + 6], "big"), cs[p + 10])] = cs[p:p + n]
+        p += n
+    return out
+
+
+@pytest.mark.parametrize("flush", [1024, 512, 0])
+def test_oracle_lossless_stripes_are_independent(flush):
+    """-flush_period incremental flushing (KakaduConverter.java:40): a
+    lossless stripe's layers come from its own tier-1 bytes, so changing the
+    pixels of one flush stripe leaves every other stripe's tile-parts
+    byte-identical (SOT, PLT, packet headers and bodies)."""
+    img = im.synth_rgb8(1300, 700, seed=21)
+    img2 = img.copy()
+    img2[1100:1250, 100:600] ^= 0x5A  # inside tile row 2 (rows 1024..1299)
+    rc = ol.recipe(True, format=0, tile_w=256, tile_h=256, flush_period=flush)
+    a, b = tile_part_bytes(ol.encode(img, rc)), tile_part_bytes(ol.encode(img2, rc))
+    ntx = 3  # 700 / 256
+    changed = {t for t in a if a[t] != b[t]}
+    assert changed and all(t[0] // ntx >= 4 for t in changed)  # the stripe of tile rows 4..5 only
+    if flush == 0:  # a stripe per tile row: tile row 4 alone
+        assert {t[0] // ntx for t in changed} == {4}
+
+
+def test_oracle_ignores_experiment_environment(monkeypatch):
+    """the parity oracle reads no environment variable (the
+    experiment hooks exist only in the -DORACLE_EXPERIMENTS build)."""
+    img = im.synth_rgb8(300, 400, seed=9)
+    want = ol.encode(img, ol.recipe(False, format=0))
+    monkeypatch.setenv("ORACLE_SKIP_MARGIN", "-40")
+    monkeypatch.setenv("ORACLE_LAYER_FRACS", "1,1,1,1,1")
+    assert ol.encode(img, ol.recipe(False, format=0)) == want
+
+
 def _golden_lossy_names():
     import json
     from conftest import GOLDEN
