@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <functional>
 #include <string>
@@ -199,6 +201,19 @@ class GpuEncoder {
     void t2_size_launch(const Plan &plan, bool with_kc, const int *halt, RateState *rs = nullptr,
                         RateState *out_rs = nullptr);
     bool host_wait(std::string &err);
+    // The code-stream D2H on an SDMA engine (ROCr hsa_amd_memory_async_copy):
+    // the HIP runtime moves a device -> pinned-host copy with a blit kernel
+    // on the CUs (tests/tools/d2h_engine_probe.sh), which under load waits
+    // for CU slots like any kernel.  The copy is queued behind `dma_dep`,
+    // which the stream's last kernel (k_release_dma) sets to 0 after the
+    // emission kernels, so it starts with no host round trip; the host
+    // waits on `dma_done`.
+    bool dma_init(std::string &err);
+    bool dma_to_host(uint8_t *host_dst, const void *src, size_t bytes, std::string &err);
+    hsa_signal_t dma_dep{0}, dma_done{0};
+    volatile hsa_signal_value_t *dma_dep_val = nullptr;
+    hsa_agent_t dma_gpu{0}, dma_cpu{0};
+    bool dma_ok = false, hsa_up = false;
     // host -> device copy through this context's pinned staging memory: a
     // pageable source goes through the runtime's shared staging buffer and
     // blocks until the stream reaches the copy, serialising the contexts

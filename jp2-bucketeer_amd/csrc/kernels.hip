@@ -1844,6 +1844,9 @@ GpuEncoder::~GpuEncoder() {
     if (h_sum) (void)hipHostFree(h_sum);
     if (h_tot) (void)hipHostFree(h_tot);
     if (h_rs) (void)hipHostFree(h_rs);
+    if (dma_dep.handle) (void)hsa_signal_destroy(dma_dep);
+    if (dma_done.handle) (void)hsa_signal_destroy(dma_done);
+    if (hsa_up) (void)hsa_shut_down();
 }
 
 bool GpuEncoder::init(int dev, std::string &err) {

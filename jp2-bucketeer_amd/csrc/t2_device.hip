@@ -982,9 +982,87 @@ __global__ void __launch_bounds__(256) k_t2_copy(T2Args a, int nblocks, const ui
     }
 }
 
+// Releases the SDMA copy of the code-stream (GpuEncoder::dma_to_host): the
+// stream's earlier kernels have completed (their writes reached memory at
+// kernel end), and this system-scope release store sets the copy's
+// dependency signal to 0.
+__global__ void __launch_bounds__(64) k_release_dma(int64_t *dep) {
+    if (threadIdx.x == 0) __hip_atomic_store(dep, (int64_t)0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // --------------------------------------------------------------------------
 // Host side (GpuEncoder)
 // --------------------------------------------------------------------------
+#define HSACHECK(x)                                                                    \
+    do {                                                                               \
+        hsa_status_t s_ = (x);                                                         \
+        if (s_ != HSA_STATUS_SUCCESS) {                                                \
+            const char *m_ = "?";                                                      \
+            hsa_status_string(s_, &m_);                                                \
+            err = std::string(#x) + ": " + m_;                                         \
+            return false;                                                              \
+        }                                                                              \
+    } while (0)
+
+static hsa_status_t first_cpu_agent(hsa_agent_t a, void *out) {
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+        *(hsa_agent_t *)out = a;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+bool GpuEncoder::dma_init(std::string &err) {
+    if (dma_ok) return true;
+    if (!t2out.ptr) {
+        err = "dma_init: no device buffer yet";
+        return false;
+    }
+    if (!hsa_up) {  // the HIP runtime has initialised ROCr already; this takes a reference
+        HSACHECK(hsa_init());
+        hsa_up = true;
+    }
+    hsa_amd_pointer_info_t pi;
+    std::memset(&pi, 0, sizeof pi);
+    pi.size = sizeof pi;
+    HSACHECK(hsa_amd_pointer_info(t2out.ptr, &pi, nullptr, nullptr, nullptr));
+    dma_gpu = pi.agentOwner;
+    if (hsa_iterate_agents(first_cpu_agent, &dma_cpu) != HSA_STATUS_INFO_BREAK) {
+        err = "dma_init: no CPU agent";
+        return false;
+    }
+    if (!dma_dep.handle) HSACHECK(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &dma_dep));
+    if (!dma_done.handle) HSACHECK(hsa_signal_create(1, 0, nullptr, &dma_done));
+    HSACHECK(hsa_amd_signal_value_pointer(dma_dep, &dma_dep_val));
+    dma_ok = true;
+    return true;
+}
+
+// Everything enqueued on the stream so far, then `bytes` from device `src` to
+// pinned `host_dst` on a DMA engine; returns when the bytes are in host memory.
+bool GpuEncoder::dma_to_host(uint8_t *host_dst, const void *src, size_t bytes, std::string &err) {
+    if (!dma_init(err)) return false;
+    hsa_signal_store_relaxed(dma_dep, 1);
+    hsa_signal_store_relaxed(dma_done, 1);
+    hipLaunchKernelGGL(k_release_dma, dim3(1), dim3(64), 0, stream, (int64_t *)dma_dep_val);
+    HIPCHECK(hipGetLastError());
+    const hsa_status_t s = hsa_amd_memory_async_copy(host_dst, dma_cpu, src, dma_gpu, bytes, 1, &dma_dep, dma_done);
+    if (s != HSA_STATUS_SUCCESS) {
+        const char *m = "?";
+        hsa_status_string(s, &m);
+        std::string e2;
+        (void)host_wait(e2);  // the stream's kernels still own the buffers
+        err = std::string("code-stream copy: hsa_amd_memory_async_copy: ") + m;
+        return false;
+    }
+    waits++;
+    if (hsa_signal_wait_scacquire(dma_done, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) < 0) {
+        err = "code-stream copy failed (DMA engine reported an error)";
+        return false;
+    }
+    return true;
+}
 template <typename T>
 static bool ensure_t2(DevBuf &b, size_t count, std::string &err) {
     size_t bytes = count * sizeof(T);
@@ -1152,13 +1230,24 @@ bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, u
         hipLaunchKernelGGL(k_t2_code<true>, dim3((t2_nprec + 63) / 64), dim3(64), 0, stream, a);
     if (nb) hipLaunchKernelGGL(k_t2_copy, dim3((nb + 3) / 4), dim3(256), 0, stream, a, nb, (const uint8_t *)t1out.ptr);
     HIPCHECK(hipGetLastError());
-    // host_dst is pinned (api.cpp out_alloc): an async D2H on this context's
-    // stream (a copy into pageable memory goes through the runtime's shared
-    // staging path, which serialises the contexts)
+    // host_dst is pinned (api.cpp out_alloc)
+#ifndef JP2HIP_D2H_BLIT
+    if (part_bytes) {
+        // on a DMA engine, released by the stream (dma_to_host): no blit
+        // kernel competes with the other contexts' kernels for CUs
+        if (!dma_to_host(host_dst, (const uint8_t *)t2out.ptr + base, part_bytes, err)) return false;
+        HIPCHECK(hipEventRecord(ev[9], stream));
+        if (profile && !host_wait(err)) return false;  // (the events below must be complete)
+    } else {
+        HIPCHECK(hipEventRecord(ev[9], stream));
+        if (!host_wait(err)) return false;
+    }
+#else  // A/B builds: the HIP runtime's copy (a blit kernel for pinned memory)
     if (part_bytes)
         HIPCHECK(hipMemcpyAsync(host_dst, (const uint8_t *)t2out.ptr + base, part_bytes, hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipEventRecord(ev[9], stream));
     if (!host_wait(err)) return false;
+#endif
     if (profile) {
         float t;
         HIPCHECK(hipEventElapsedTime(&t, ev[8], ev[9]));

@@ -1,0 +1,210 @@
+/*
+ * glue_replay.c -- replays, without a JVM, the native call sequence that
+ * Bucketeer's GpuConverter (jp2-bucketeer_amd/java) makes through its JNI
+ * natives, on the same glue functions the natives wrap (jp2hip_glue.c):
+ *
+ *   ConverterFactory:  glue_probe                        (checkSystemKakadu analogue)
+ *   new GpuConverter:  glue_open = device_ordinals, create x N, [create + split_peers]
+ *                      glue_env_check
+ *   convert() x M:     glue_tiff_pixels -> split or pooled context (a pool of
+ *                      borrowed handles, as the Java BlockingQueue), glue_encode_file,
+ *                      the error text of the calling thread on failure
+ *   close():           glue_close
+ *
+ * plus the failure paths the converter must survive: a constructor that fails
+ * part-way (created contexts released), an out-of-range split ordinal, a
+ * missing TIFF, an unwritable output.  Built with AddressSanitizer by
+ * tests/test_java_glue.py (host code only) and run on the CPU (no GPU: the
+ * unavailable paths) and on the GPU box.
+ *
+ *   glue_replay <out_dir> <conversion 0|1> <threads> <tiff>...
+ * prints one line per event; "REPLAY OK" at the end when every check held.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "jp2hip_glue.h"
+
+static int g_fail = 0;
+#define CHECK(c, ...)                                        \
+    do {                                                     \
+        if (!(c)) {                                          \
+            printf("CHECK FAILED line %d: ", __LINE__);      \
+            printf(__VA_ARGS__);                             \
+            printf("\n");                                    \
+            g_fail = 1;                                      \
+        }                                                    \
+    } while (0)
+
+/* the converter's context pool (GpuConverter.myContexts) */
+typedef struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int64_t *h;
+    int n, top;
+} pool_t;
+
+static int64_t pool_take(pool_t *p) {
+    pthread_mutex_lock(&p->mu);
+    while (p->top == 0) pthread_cond_wait(&p->cv, &p->mu);
+    const int64_t h = p->h[--p->top];
+    pthread_mutex_unlock(&p->mu);
+    return h;
+}
+
+static void pool_put(pool_t *p, int64_t h) {
+    pthread_mutex_lock(&p->mu);
+    p->h[p->top++] = h;
+    pthread_cond_signal(&p->cv);
+    pthread_mutex_unlock(&p->mu);
+}
+
+typedef struct {
+    pool_t *pool;
+    int64_t split, split_min;
+    pthread_mutex_t *split_mu;
+    const char *const *tiffs;
+    int ntiffs, first, step, conversion;
+    const char *out_dir;
+    int errors;
+} worker_t;
+
+/* GpuConverter.convert() */
+static int convert(worker_t *w, const char *tiff, const char *out, char *err) {
+    const int64_t px = glue_tiff_pixels(tiff, strlen(tiff));
+    if (w->split && px >= w->split_min) {
+        pthread_mutex_lock(w->split_mu);  /* one oversized image at a time holds every GPU */
+        const int rc = glue_encode_file(w->split, tiff, strlen(tiff), out, strlen(out), w->conversion, err, GLUE_ERR_LEN);
+        pthread_mutex_unlock(w->split_mu);
+        printf("convert %s -> %s via split context: %s\n", tiff, out, rc ? err : "ok");
+        return rc;
+    }
+    const int64_t ctx = pool_take(w->pool);
+    const int rc = glue_encode_file(ctx, tiff, strlen(tiff), out, strlen(out), w->conversion, err, GLUE_ERR_LEN);
+    pool_put(w->pool, ctx);
+    printf("convert %s -> %s via pooled context: %s\n", tiff, out, rc ? err : "ok");
+    return rc;
+}
+
+static void *worker(void *arg) {
+    worker_t *w = (worker_t *)arg;
+    char err[GLUE_ERR_LEN], out[4096];
+    for (int i = w->first; i < w->ntiffs; i += w->step) {
+        snprintf(out, sizeof out, "%s/out%03d.jpx", w->out_dir, i);
+        if (convert(w, w->tiffs[i], out, err) != 0) w->errors++;
+    }
+    return NULL;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: glue_replay <out_dir> <conversion> <threads> <tiff>...\n");
+        return 2;
+    }
+    setvbuf(stdout, NULL, _IOLBF, 0);
+    const char *out_dir = argv[1];
+    const int conversion = atoi(argv[2]), nthreads = atoi(argv[3]) > 0 ? atoi(argv[3]) : 1;
+    const char *const *tiffs = (const char *const *)(argv + 4);
+    const int ntiffs = argc - 4;
+    char err[GLUE_ERR_LEN];
+
+    /* ConverterFactory.getConverter(GpuConverter.class): probe first */
+    const int probe = glue_probe();
+    printf("probe %d\n", probe);
+    for (int i = 0; i < ntiffs; i++) printf("tiff_pixels %s %lld\n", tiffs[i], (long long)glue_tiff_pixels(tiffs[i], strlen(tiffs[i])));
+    CHECK(glue_tiff_pixels("/nonexistent.tif", 16) == -1, "missing TIFF has pixels");
+    int64_t handles[64];
+    int n = -1;
+    int64_t split = -1;
+    if (!probe) {
+        /* no GPU: the converter is unavailable; nothing may be allocated */
+        const int rc = glue_open(2, 1, handles, 64, &n, &split, err, sizeof err);
+        printf("open without a GPU: rc %d n %d split %lld: %s\n", rc, n, (long long)split, err);
+        CHECK(rc == -1 && n == 0 && split == 0, "open must fail cleanly");
+        int64_t h = 7;
+        CHECK(glue_create(0, 0, &h, err, sizeof err) == -1 && h == 0, "create without a GPU");
+        printf("create without a GPU: %s\n", err);
+        CHECK(glue_encode_file(0, "a.tif", 5, "b.jpx", 5, conversion, err, sizeof err) == -1, "encode on no context");
+        printf("encode on no context: %s\n", err);
+        glue_close(handles, 0, 0);
+        printf("%s\n", g_fail ? "REPLAY FAILED" : "REPLAY OK");
+        return g_fail;
+    }
+
+    /* a constructor failing part-way (GpuConverter(): nothing leaks): a good
+     * context, then a device ordinal that does not exist */
+    {
+        int32_t ord[64];
+        const int ng = glue_device_ordinals(ord, 64);
+        CHECK(ng >= 1, "probe said yes but no ordinals");
+        int64_t a = 0, b = 5;
+        CHECK(glue_create(ord[0], 0, &a, err, sizeof err) == 0, "create on GPU %d: %s", ord[0], err);
+        const int rc = glue_create(4096, 0, &b, err, sizeof err);
+        printf("create on ordinal 4096: rc %d: %s\n", rc, err);
+        CHECK(rc == -1 && b == 0 && strstr(err, "out of range"), "bad ordinal must fail cleanly");
+        /* split peers on an ordinal past the device count: a clean failure, no fault */
+        const int32_t bad[2] = {ord[0], 4096};
+        const int rs = glue_split_peers(a, bad, 2, 1, err, sizeof err);
+        printf("split_peers with ordinal 4096: rc %d: %s\n", rs, err);
+        CHECK(rs == -1 && strstr(err, "4096"), "bad split ordinal must fail cleanly");
+        glue_destroy(a);
+    }
+
+    /* new GpuConverter(): two contexts per GPU */
+    const int64_t split_min = 3000000;  /* images of >= 3 MP take the split context */
+    CHECK(glue_open(2, split_min, handles, 64, &n, &split, err, sizeof err) == 0, "open: %s", err);
+    printf("open: %d pooled contexts, split %s\n", n, split ? "yes" : "no (one GPU)");
+    if (!split) {
+        /* one GPU: a split context whose peer is the same device, so the
+         * split route of convert() runs too (jp2hip_split_peers allows it) */
+        int32_t ord[1];
+        glue_device_ordinals(ord, 1);
+        CHECK(glue_create(ord[0], 0, &split, err, sizeof err) == 0, "split create: %s", err);
+        CHECK(glue_split_peers(split, ord, 1, split_min, err, sizeof err) == 0, "split peers: %s", err);
+    }
+    printf("env_check '%s'\n", glue_env_check());
+
+    pool_t pool;
+    pthread_mutex_init(&pool.mu, NULL);
+    pthread_cond_init(&pool.cv, NULL);
+    pool.h = handles;
+    pool.n = pool.top = n;
+    pthread_mutex_t split_mu;
+    pthread_mutex_init(&split_mu, NULL);
+    pthread_t th[64];
+    worker_t w[64];
+    const int nt = nthreads > 64 ? 64 : nthreads;
+    for (int t = 0; t < nt; t++) {
+        w[t] = (worker_t){&pool, split, split_min, &split_mu, tiffs, ntiffs, t, nt, conversion, out_dir, 0};
+        pthread_create(&th[t], NULL, worker, &w[t]);
+    }
+    int errors = 0;
+    for (int t = 0; t < nt; t++) {
+        pthread_join(th[t], NULL);
+        errors += w[t].errors;
+    }
+    CHECK(errors == 0, "%d conversions failed", errors);
+
+    /* failures surface as text, never as a crash; no partial file is left */
+    worker_t one = {&pool, 0, 0, &split_mu, NULL, 0, 0, 1, conversion, out_dir, 0};
+    char out[4096];
+    snprintf(out, sizeof out, "%s/missing.jpx", out_dir);
+    CHECK(convert(&one, "/nonexistent/x.tif", out, err) == -1 && strstr(err, "cannot open TIFF"), "missing TIFF: %s", err);
+    FILE *f = fopen(out, "rb");
+    CHECK(!f, "a failed conversion left %s", out);
+    if (f) fclose(f);
+    if (ntiffs) {
+        CHECK(convert(&one, tiffs[0], "/nonexistent-dir/x.jpx", err) == -1 && strstr(err, "cannot write output"),
+              "unwritable output: %s", err);
+    }
+
+    /* GpuConverter.close() */
+    glue_close(handles, n, split);
+    pthread_mutex_destroy(&pool.mu);
+    pthread_cond_destroy(&pool.cv);
+    pthread_mutex_destroy(&split_mu);
+    printf("%s\n", g_fail ? "REPLAY FAILED" : "REPLAY OK");
+    return g_fail;
+}
