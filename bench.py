@@ -246,6 +246,35 @@ def d2h_peak(nbytes=256 << 20, reps=5):
     return best
 
 
+def h2d_peak(nbytes=256 << 20, reps=5):
+    """Pinned host -> device copy rate (GB/s) on this box: the bound of the
+    file-to-file span, whose TIFF bytes (72 MB per C2 image) cross PCIe."""
+    import torch
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    best = 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
+    return best
+
+
+def evict_from_page_cache(paths):
+    """Drop the files' pages from the page cache (written pages are flushed
+    first), so the timed region reads them from the device, not from RAM."""
+    for p in paths:
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        finally:
+            os.close(fd)
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN/pmc_traffic.json, made by tests/tools/pmc_summary.py from two
@@ -465,7 +494,10 @@ def run(args):
                                        "achieved": round(dwt_alg / (dwt_alone * 1e-3) / 1e9, 2),
                                        "frac": round(dwt_alg / (dwt_alone * 1e-3) / HBM_PEAK, 5)}}
                              if avg["dwt_ms"] > 0 and dwt_alone > 0 else None),
-            "t1_counters": {"k_t1_mq": sq_counters("k_t1_mq"), "k_t1_cm3": sq_counters("k_t1_cm3"),
+            # SQ counters are per launch (one launch per image: sq_summary.py
+            # averages the rocprofv3 --pmc rows over the launches)
+            "t1_counters": {"units": "per kernel launch (one per image)",
+                            "k_t1_mq": sq_counters("k_t1_mq"), "k_t1_cm3": sq_counters("k_t1_cm3"),
                             "k_quant": sq_counters("k_quant")},
             "stages_ms": {k: round(avg[k], 4) for k in ("ingest_ms", "dwt_ms", "quant_ms", "t1_cm_ms",
                                                         "t1_mq_ms", "pcrd_ms", "d2h_ms", "t2_ms",
@@ -559,6 +591,7 @@ def run_c4(args):
             for k, it in enumerate(items[:12]):
                 q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k))
             q.drain()
+            evict_from_page_cache(paths)
             if world > 1:
                 dist.barrier()
             t0 = time.perf_counter()
@@ -580,7 +613,8 @@ def run_c4(args):
         return {"metric": METRIC, "value": round(mp / dt, 3), "unit": "MP/s", "n_gpus": world,
                 "steps": rows, "warmup": 1, "ms_per_step": round(dt * 1e3 / rows, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "i32",
-                "data": f"synthetic 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0..{ndistinct - 1}) on local disk",
+                "data": f"synthetic 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0..{ndistinct - 1}) on local "
+                        "disk, evicted from the page cache before the timed region",
                 "config": {"workload": "C4: Bucketeer batch CSV -> per-GPU native queue (read, lossless 5/3 encode, "
                                        "JPX write, stub upload, delete-after-upload), Kakadu recipe",
                            "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"shards x{world}",
@@ -833,13 +867,15 @@ def lossless_c3(enc, steps=2, inflight=6, n_each=4):
 
 
 def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=None, reader_threads=4,
-             uploader_threads=4, shape=(7000, 5000)):
-    """C4 (configs[3]) on one GPU, reduced: a Bucketeer batch CSV of `rows`
-    synthetic 5000x7000 RGB8 TIFFs (cycling over `ndistinct` files, as
-    SURVEY.md 8(d) prescribes for the 10k-row batch) through the native batch
-    queue: TIFF read from disk -> lossless encode -> JPX write -> stub upload
-    (reads every byte) -> delete.  Timed from the first submit to the last
-    upload, file I/O included.  Returns (MP/s, seconds, results)."""
+             uploader_threads=4, shape=(7000, 5000), gen_threads=8):
+    """C4 (configs[3]) on one GPU: a Bucketeer batch CSV of `rows` synthetic
+    5000x7000 RGB8 TIFFs (cycling over `ndistinct` files, as SURVEY.md 8(d)
+    prescribes for the 10k-row batch) through the native batch queue: TIFF
+    read from disk -> lossless encode -> JPX write -> stub upload (reads every
+    byte) -> delete.  The files are evicted from the page cache before the
+    timed region (POSIX_FADV_DONTNEED), which runs from the first submit to
+    the last upload, file I/O included.  Returns (MP/s, seconds, results,
+    bytes of TIFF read)."""
     import csv as _csv
     import shutil
     from concurrent.futures import ThreadPoolExecutor
@@ -857,8 +893,9 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
                 f.write(im.tiff_bytes(make(i), rows_per_strip=64))
             return pth
 
-        with ThreadPoolExecutor(ndistinct) as ex:
+        with ThreadPoolExecutor(min(ndistinct, gen_threads)) as ex:
             paths = list(ex.map(gen, range(ndistinct)))
+        sizes = {p: os.path.getsize(p) for p in paths}
         csv_path = os.path.join(work, "batch.csv")
         with open(csv_path, "w", newline="", encoding="utf-8") as f:
             wr = _csv.writer(f)
@@ -873,48 +910,63 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
             for k, it in enumerate(items[:contexts]):  # warm-up: device buffers of every context
                 q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k), conv)
             q.drain()
+            evict_from_page_cache(paths)
             t0 = time.perf_counter()
             for it in items:
                 q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)), conv)
             res = q.drain()
             dt = time.perf_counter() - t0
         ok = sum(1 for r in res if r["status"] == 0)
-        return shape[0] * shape[1] / 1e6 * ok / dt, dt, res
+        read = sum(sizes[paths[i % ndistinct]] for i in range(rows))
+        return shape[0] * shape[1] / 1e6 * ok / dt, dt, res, read
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
 
-def lossless_c4(device):
-    rows = 640  # >= 2 s of batch at ~10 GP/s
-    value, dt, res = c4_batch(device, rows=rows)
+def lossless_c4(device, rows=10000, ndistinct=16):
+    """SURVEY.md 8(d) C4: a 10 000-row CSV (16 distinct files of seeds 0-15;
+    the survey's 64 would be 6.7 GB of fixtures per bench run)."""
+    value, dt, res, _ = c4_batch(device, rows=rows, ndistinct=ndistinct)
     ok = [r for r in res if r["status"] == 0]
     bpp = 8 * float(np.mean([r["out_bytes"] for r in ok])) / (5000 * 7000) if ok else 0.0
     b_path = dwt_bytes_per_px(3, 1, 6) + 4 * 3 + 3 * bpp / 8
-    return {"workload": "C4: Bucketeer batch CSV of 5000x7000 RGB8 TIFFs (2 distinct, seeds 0-1) -> native "
-                        "per-GPU queue (disk read, lossless 5/3 encode, JPX write, stub upload, delete)",
-            "rows": rows, "images_ok": len(ok), "mp_per_s": round(value, 3), "seconds": round(dt, 3),
+    return {"workload": f"C4: Bucketeer batch CSV of 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0-"
+                        f"{ndistinct - 1}) -> native per-GPU queue (disk read, lossless 5/3 encode, JPX write, "
+                        "stub upload, delete)",
+            "rows": rows, "distinct_files": ndistinct, "page_cache": "files evicted before the timed region",
+            "images_ok": len(ok), "mp_per_s": round(value, 3), "seconds": round(dt, 3),
             "bpp": round(bpp, 4), "timed_span": "first submit -> last upload, file I/O included",
             "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
                               "achieved": round(b_path * value * 1e6 / 1e9, 2), "peak": HBM_PEAK / 1e9,
                               "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}}
 
 
-def c2_file_span(device, images=1024, contexts=16):
+def c2_file_span(device, images=1024, contexts=16, ndistinct=16):
     """SURVEY.md 8(d)'s span for the headline workload: C2 (lossy 3 bpp) from
     TIFF files on disk to JPX files written, through the native per-GPU queue
     (reader threads: file -> pinned buffer + header parse; `contexts` encodes
     in flight; uploader threads: atomic JPX write, stub upload reading every
-    byte, delete-after-upload), `images` images cycling over 4 distinct files,
-    timed from the first submit to the last upload."""
+    byte, delete-after-upload), `images` images cycling over `ndistinct`
+    distinct files evicted from the page cache first, timed from the first
+    submit to the last upload.  Every TIFF byte crosses PCIe host -> device:
+    roofline_pcie is that rate against the measured pinned H2D rate."""
     import imaging as im
     import jp2hip
-    value, dt, res = c4_batch(device, rows=images, ndistinct=4, contexts=contexts, conversion=jp2hip.LOSSY,
-                              make=lambda i: im.synth_rgb8(4000, 6000, seed=1234 + i), reader_threads=8,
-                              uploader_threads=8, shape=(4000, 6000))
+    value, dt, res, read = c4_batch(device, rows=images, ndistinct=ndistinct, contexts=contexts,
+                                    conversion=jp2hip.LOSSY,
+                                    make=lambda i: im.synth_rgb8(4000, 6000, seed=1234 + i), reader_threads=8,
+                                    uploader_threads=8, shape=(4000, 6000))
     ok = [r for r in res if r["status"] == 0]
+    peak = h2d_peak()
+    h2d = read / dt / 1e9
     return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok),
+            "distinct_files": ndistinct, "page_cache": "files evicted before the timed region",
             "seconds": round(dt, 3), "contexts": contexts,
             "out_bytes": int(np.mean([r["out_bytes"] for r in ok])) if ok else 0,
+            "roofline_pcie": {"bound": "pcie_h2d", "achieved": round(h2d, 2), "peak": round(peak, 2), "unit": "GB/s",
+                              "frac": round(h2d / peak, 4),
+                              "def": "TIFF bytes read per second (every byte is uploaded) / measured pinned "
+                                     "host->device copy rate"},
             "timed_span": "first TIFF open -> last JPX written, uploaded (stub) and deleted; "
                           "file read, H2D, encode, D2H, file write included"}
 

@@ -213,6 +213,7 @@ class GpuEncoder {
     hsa_signal_t dma_dep{0}, dma_done{0};
     volatile hsa_signal_value_t *dma_dep_val = nullptr;
     hsa_agent_t dma_gpu{0}, dma_cpu{0};
+    int dma_engine = -1;  // SDMA engine of this context (-1: the runtime's choice)
     bool dma_ok = false, hsa_up = false;
     // host -> device copy through this context's pinned staging memory: a
     // pageable source goes through the runtime's shared staging buffer and

@@ -21,7 +21,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -1013,6 +1016,63 @@ static hsa_status_t first_cpu_agent(hsa_agent_t a, void *out) {
     return HSA_STATUS_SUCCESS;
 }
 
+// SDMA engines differ a lot in their device -> host rate (MI355X box,
+// profiles/r05/sdma_engines.txt: engines 0, 2, 3 at 56.6 GB/s, engine 1 --
+// the runtime's own pick -- at 30, engines 4-15 at 7-13), so the engines are
+// timed once per process and GPU on a 32 MiB copy, and the contexts spread
+// over the ones within 10 % of the fastest.
+struct DmaEngines {
+    std::mutex mu;
+    std::map<uint64_t, std::vector<int>> fast;  // GPU agent handle -> engine ids
+    std::map<uint64_t, int> next;               // round-robin cursor
+};
+static DmaEngines &dma_engines() {
+    static DmaEngines *e = new DmaEngines();  // never destroyed: contexts may outlive static teardown
+    return *e;
+}
+
+static int pick_dma_engine(hsa_agent_t gpu, hsa_agent_t cpu, hsa_signal_t sig) {
+    DmaEngines &E = dma_engines();
+    std::lock_guard<std::mutex> lk(E.mu);
+    auto it = E.fast.find(gpu.handle);
+    if (it == E.fast.end()) {
+        std::vector<int> fast;
+        uint32_t mask = 0;
+        const size_t n = 32u << 20;
+        void *d = nullptr, *h = nullptr;
+        if (hsa_amd_memory_copy_engine_status(cpu, gpu, &mask) == HSA_STATUS_SUCCESS && mask &&
+            hipMalloc(&d, n) == hipSuccess && hipHostMalloc(&h, n, hipHostMallocDefault) == hipSuccess) {
+            std::vector<std::pair<double, int>> rate;
+            for (int e = 0; e < 16; e++) {
+                if (!(mask & (1u << e))) continue;
+                double best = 0.0;
+                for (int r = 0; r < 2; r++) {  // the first copy also maps the pages
+                    hsa_signal_store_relaxed(sig, 1);
+                    const auto t0 = std::chrono::steady_clock::now();
+                    if (hsa_amd_memory_async_copy_on_engine(h, cpu, d, gpu, n, 0, nullptr, sig,
+                                                            (hsa_amd_sdma_engine_id_t)(1u << e), true) != HSA_STATUS_SUCCESS)
+                        break;
+                    if (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) < 0)
+                        break;
+                    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                    best = std::max(best, n / s);
+                }
+                if (best > 0.0) rate.emplace_back(best, e);
+            }
+            double top = 0.0;
+            for (auto &r : rate) top = std::max(top, r.first);
+            for (auto &r : rate)
+                if (r.first >= 0.9 * top) fast.push_back(r.second);
+        }
+        if (d) (void)hipFree(d);
+        if (h) (void)hipHostFree(h);
+        it = E.fast.emplace(gpu.handle, fast).first;  // empty: the runtime picks the engine
+    }
+    if (it->second.empty()) return -1;
+    int &k = E.next[gpu.handle];
+    return it->second[(size_t)(k++) % it->second.size()];
+}
+
 bool GpuEncoder::dma_init(std::string &err) {
     if (dma_ok) return true;
     if (!t2out.ptr) {
@@ -1035,6 +1095,7 @@ bool GpuEncoder::dma_init(std::string &err) {
     if (!dma_dep.handle) HSACHECK(hsa_amd_signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &dma_dep));
     if (!dma_done.handle) HSACHECK(hsa_signal_create(1, 0, nullptr, &dma_done));
     HSACHECK(hsa_amd_signal_value_pointer(dma_dep, &dma_dep_val));
+    dma_engine = pick_dma_engine(dma_gpu, dma_cpu, dma_done);
     dma_ok = true;
     return true;
 }
@@ -1047,7 +1108,11 @@ bool GpuEncoder::dma_to_host(uint8_t *host_dst, const void *src, size_t bytes, s
     hsa_signal_store_relaxed(dma_done, 1);
     hipLaunchKernelGGL(k_release_dma, dim3(1), dim3(64), 0, stream, (int64_t *)dma_dep_val);
     HIPCHECK(hipGetLastError());
-    const hsa_status_t s = hsa_amd_memory_async_copy(host_dst, dma_cpu, src, dma_gpu, bytes, 1, &dma_dep, dma_done);
+    const hsa_status_t s =
+        dma_engine >= 0
+            ? hsa_amd_memory_async_copy_on_engine(host_dst, dma_cpu, src, dma_gpu, bytes, 1, &dma_dep, dma_done,
+                                                  (hsa_amd_sdma_engine_id_t)(1u << dma_engine), true)
+            : hsa_amd_memory_async_copy(host_dst, dma_cpu, src, dma_gpu, bytes, 1, &dma_dep, dma_done);
     if (s != HSA_STATUS_SUCCESS) {
         const char *m = "?";
         hsa_status_string(s, &m);
