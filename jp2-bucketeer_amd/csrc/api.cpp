@@ -576,19 +576,21 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         iters = 1;
         cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
     } else {
-        // the rate loop runs on the device (GpuEncoder::rate_loop): two
-        // iterations are enqueued per host wait, what the usual encode needs
-        // (a third would be launched only to return at once)
+        // the rate loop runs on the device (GpuEncoder::rate_loop): one
+        // iteration per host wait, what the usual encode needs -- the first
+        // budget's header estimate (16 bytes per packet) lands it under the
+        // target (C2: 8 985 521 of 9 000 000 bytes); an encode whose headers
+        // are heavier takes a second wait for its next iterations
         RateState init;
         std::memset(&init, 0, sizeof init);
         init.target = (int64_t)std::floor(rc.rate_bpp * (double)plan.w * (double)plan.h / 8.0);
-        init.budget = init.target - 12 * plan.npackets - 16 * plan.ntileparts - 256;
+        init.budget = init.target - 16 * plan.npackets - 16 * plan.ntileparts - 256;
         init.fixed = (int64_t)mh.size() + 2;
         init.skip_target = skip_target;
         RateState rs;
         bool restart = true;
         for (;;) {
-            if (!ctx->gpu.rate_loop(plan, init, restart, 2, prof, st, rs, sum, err)) return fail(err);
+            if (!ctx->gpu.rate_loop(plan, init, restart, restart ? 1 : 2, prof, st, rs, sum, err)) return fail(err);
             restart = false;
             if (sum.err) return fail("tier-1 output capacity exceeded");
             if (rs.safety) {
@@ -784,7 +786,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
             if (flag) return fail("split: another rank failed");
         }
         const int64_t target = (int64_t)std::floor(rc.rate_bpp * (double)full.w * (double)full.h / 8.0);
-        int64_t budget = target - 12 * full.npackets - 16 * full.ntileparts - 256;
+        int64_t budget = target - 16 * full.npackets - 16 * full.ntileparts - 256;
         bool rerun = false;
         for (int it = 0; it < 8; it++) {
             if (budget < 0) budget = 0;

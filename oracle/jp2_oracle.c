@@ -1790,7 +1790,7 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         write_codestream(&E, &cs);
     } else {
         int64_t target = (int64_t)floor(rc->rate_bpp * (double)w * (double)h / 8.0);
-        int64_t budget = target - 12 * (int64_t)npackets - 16 * (int64_t)ntparts - 256;
+        int64_t budget = target - 16 * (int64_t)npackets - 16 * (int64_t)ntparts - 256;
         for (int it = 0; it < 8; it++) {
             if (budget < 0) budget = 0;
             for (int l = 0; l < NL; l++) {
