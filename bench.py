@@ -36,9 +36,24 @@ METRIC = "encoded megapixels/sec (node), lossless 5/3 + lossy 9/7, at 1/2/4/8 MI
 HBM_PEAK = 8.0e12  # MI355X_MICROARCH.md chip table (spec)
 
 
-def dwt_bytes_per_px(C, s, L):
-    """B_dwt = C*[s + 4 + (8/3)(1 - 4^-(L-1))]."""
-    return C * (s + 4 + (8.0 / 3.0) * (1 - 4.0 ** (-(L - 1))))
+def dwt_bytes_per_px(C, s, L, e=4):
+    """DWT bytes per pixel: level 1 reads the s-byte TIFF samples, level k > 1
+    reads the previous LL (4-byte words); each level writes its three high
+    bands as e-byte final coefficients and its LL as 4-byte words (the last
+    level's LL final, e bytes).  e = 4 is SURVEY.md 8(d)'s B_dwt = C*[s + 4 +
+    (8/3)(1 - 4^-(L-1))] (up to the last LL); the DWT writes 16-bit
+    quantisation indices (e = 2) wherever every band fits 15 magnitude
+    bit-planes (csrc/plan.cpp quant_tab: 8-bit sources, and lossy 16-bit)."""
+    b = 0.0
+    for k in range(1, L + 1):
+        f = 4.0 ** (-(k - 1))  # samples of level k's input, per pixel and component
+        b += (s if k == 1 else 4 * f) + f * (0.75 * e + 0.25 * (4 if k < L else e))
+    return C * b
+
+
+def coef_bytes(bits, lossy):
+    """Bytes per final coefficient the DWT writes and k_quant reads."""
+    return 2 if (bits == 8 or lossy) else 4
 
 
 def make_image(kind: str, seed: int):
@@ -436,12 +451,14 @@ def run(args):
         # counts / distortions it also reads are < 1 %)
         mq_alg = avg_all["mq_decisions"] + avg_all["t1_bytes"]
         ach = mq_alg / (avg_all["t1_mq_ms"] * 1e-3) / 1e9 if avg_all["t1_mq_ms"] > 0 else 0.0
-        dwt_alg = dwt_bytes_per_px(C, 1, L) * npx
+        ce = coef_bytes(8, True)
+        dwt_alg = dwt_bytes_per_px(C, 1, L, ce) * npx
         dwt_alone = float(np.mean([x["dwt_ms"] for x in alone]))
         traffic, traffic_src = pmc_traffic(dom)
-        # SURVEY.md 8(d) full path: B_path = B_dwt + 4C + 3*bpp/8 per pixel
+        # SURVEY.md 8(d) full path: B_path = B_dwt + (coefficient read) C +
+        # 3*bpp/8 per pixel (4C there: 4-byte coefficients)
         bpp = 8 * avg["out_bytes"] / npx
-        b_path = dwt_bytes_per_px(C, 1, L) + 4 * C + 3 * bpp / 8
+        b_path = dwt_bytes_per_px(C, 1, L, ce) + ce * C + 3 * bpp / 8
         px_per_s_gpu = value / world * 1e6
         res = {
             "metric": METRIC, "value": round(value, 3), "unit": "MP/s", "n_gpus": world,
@@ -488,7 +505,8 @@ def run(args):
             "roofline_dwt": ({"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                              "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                              "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
-                             "alg_bytes_per_px": round(dwt_bytes_per_px(C, 1, L), 3),
+                             "alg_bytes_per_px": round(dwt_bytes_per_px(C, 1, L, ce), 3),
+                             "coef_bytes": ce,
                              "stage_ms": round(avg["dwt_ms"], 4),
                              "alone": {"stage_ms": round(dwt_alone, 4),
                                        "achieved": round(dwt_alg / (dwt_alone * 1e-3) / 1e9, 2),
@@ -675,7 +693,7 @@ def run_c5(args):
     if rank != 0:
         return None
     avg = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
-    dwt_alg = dwt_bytes_per_px(1, 2, C5["levels"]) * (rows[1] - rows[0]) * C5["w"]
+    dwt_alg = dwt_bytes_per_px(1, 2, C5["levels"], coef_bytes(16, True)) * (rows[1] - rows[0]) * C5["w"]
     return {
         "metric": METRIC, "value": round(value, 3), "unit": "MP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 3), "higher_is_better": True,
@@ -691,7 +709,7 @@ def run_c5(args):
         "roofline_dwt": {"bound": "hbm", "achieved": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / 1e9, 2),
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": round(dwt_alg / (avg["dwt_ms"] * 1e-3) / HBM_PEAK, 5),
-                         "alg_bytes_per_px": round(dwt_bytes_per_px(1, 2, C5["levels"]), 3)},
+                         "alg_bytes_per_px": round(dwt_bytes_per_px(1, 2, C5["levels"], coef_bytes(16, True)), 3)},
         "stages_ms_rank0": {k: round(avg[k], 4) for k in ("ingest_ms", "dwt_ms", "quant_ms", "t1_cm_ms",
                                                           "t1_mq_ms", "pcrd_ms", "d2h_ms", "t2_ms", "total_ms")},
         "rate_iterations": int(avg["rate_iterations"]),
@@ -847,7 +865,7 @@ def lossless_c3(enc, steps=2, inflight=6, n_each=4):
     dt = time.perf_counter() - t0
     value = npx / 1e6 * n_each * inflight / dt
     # SURVEY.md 8(d) full path at the measured bpp: B_dwt + 4C + 3 bpp / 8
-    b_path = dwt_bytes_per_px(3, 2, 6) + 4 * 3 + 3 * bpp / 8
+    b_path = dwt_bytes_per_px(3, 2, 6, coef_bytes(16, False)) + coef_bytes(16, False) * 3 + 3 * bpp / 8
     # the bound that matters for lossless: every code-stream byte (~34 bpp
     # for C3) crosses PCIe to the host; device->pinned-host peak measured here
     d2h = d2h_peak()
@@ -929,7 +947,7 @@ def lossless_c4(device, rows=10000, ndistinct=16):
     value, dt, res, _ = c4_batch(device, rows=rows, ndistinct=ndistinct)
     ok = [r for r in res if r["status"] == 0]
     bpp = 8 * float(np.mean([r["out_bytes"] for r in ok])) / (5000 * 7000) if ok else 0.0
-    b_path = dwt_bytes_per_px(3, 1, 6) + 4 * 3 + 3 * bpp / 8
+    b_path = dwt_bytes_per_px(3, 1, 6, coef_bytes(8, False)) + coef_bytes(8, False) * 3 + 3 * bpp / 8
     return {"workload": f"C4: Bucketeer batch CSV of 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0-"
                         f"{ndistinct - 1}) -> native per-GPU queue (disk read, lossless 5/3 encode, JPX write, "
                         "stub upload, delete)",

@@ -44,6 +44,25 @@ __device__ __forceinline__ int64_t dist_gain_small(uint32_t v, int p, bool lossl
     return (int64_t)(e1 * e1) - (int64_t)(e0 * e0);
 }
 
+// Deadzone quantisation of one final DWT coefficient (Annex E.1; oracle
+// quantise): the index min(floor(|x| / Delta), 2^Mb - 1) -- |x| for the
+// reversible path -- with the coefficient's sign bit at bit `sbit` (15: the
+// 16-bit plane, 31: the 32-bit one).  The sign of a zero index is stored as
+// the coefficient had it and never coded.
+// (The float product is non-negative, so the truncating conversion is the
+// floor: one v_mul with the |x| source modifier and one v_cvt.)
+template <bool REV>
+__device__ __forceinline__ uint32_t quant_mag(int32_t x, float inv, uint32_t lim) {
+    uint32_t m;
+    if (REV) m = (uint32_t)abs(x);
+    else m = (uint32_t)(__builtin_fabsf(__int_as_float(x)) * inv);
+    return min(m, lim);
+}
+template <bool REV>
+__device__ __forceinline__ uint32_t quant_sm(int32_t x, float inv, uint32_t lim, int sbit) {
+    return quant_mag<REV>(x, inv, lim) | (((uint32_t)x >> 31) << sbit);
+}
+
 // Whole-wave lane shifts by DPP (wave_shr:1 / wave_shl:1, GFX9 family): a
 // VALU move, not an LDS-crossbar ds_bpermute with its latency.  Lane 0
 // (shr) / lane 63 (shl) receive 0.

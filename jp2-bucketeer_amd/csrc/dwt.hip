@@ -25,11 +25,18 @@
 // as oracle/jp2_oracle.c (fwd53_1d / fwd97_1d, oracle_fdwt): the halo rows
 // reproduce exactly the values the full-column lifting would produce, so the
 // output is bit-identical (built with -ffp-contract=off).
+//
+// Final coefficients leave as quantisation indices (quant_sm: the deadzone
+// quantiser k_quant applied before, same expression): 16-bit sign-magnitude
+// words for 8-bit sources (QuantTab::q16), so the plane k_quant reads back is
+// half the f32 plane.  Only the LL of a non-final level stays raw (the LL
+// scratch the next level reads).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
 
+#include "device_common.h"
 #include "gpu_encoder.h"
 
 namespace jp2hip {
@@ -131,6 +138,7 @@ struct DwtBandArgs {
     const int32_t *tc_w, *tc_h;
     int level, R;
     int ragged;  // some tile width is not a multiple of 16 (k_dwt_l1s second launch)
+    QuantTab qt;
 };
 
 __device__ __forceinline__ int32_t tiff_sample(const DwtBandArgs &a, size_t rowoff, int x, int c) {
@@ -213,8 +221,8 @@ __device__ __forceinline__ void lift_regs(int32_t (&v)[NR], int y0, int H) {
 // Horizontal lifting (in LDS, thread = sample, row loop uniform), then
 // scaling and the de-interleaved write -- consecutive threads store
 // consecutive words, whole 256-byte runs per wave-instruction -- of NROWS
-// staged rows (LDS row r at lds + kPadL + r * ld).  rows(r, lrow, hrow)
-// names row r's output rows (false: row r was not staged).  A register
+// staged rows (LDS row r at lds + kPadL + r * ld).  rows(r, o) fills row
+// r's outputs (QRow; false: row r was not staged).  A register
 // variant (16-sample segments, 16-byte stores) measured slower: its stores
 // scatter over many lines per wave-instruction.
 constexpr int kPadL = 4;   // LDS words in front of row 0 (the first segment's left halo)
@@ -223,8 +231,87 @@ constexpr int kPadL = 4;   // LDS words in front of row 0 (the first segment's l
 __host__ __device__ constexpr int lds_row_stride(int W) { return ((W + 63) & ~63) + 4; }
 constexpr int kPadR = 24;  // LDS words after the last row (the last segment's right halo)
 
+// Where one staged row's outputs go: its low half raw to the next level's LL
+// row `ll` (a non-final level's even rows), or -- like its high half --
+// quantised into the coefficient-plane row at `q` (element 0 = column 0 of
+// the tile-component row; 2- or 4-byte elements), with the quantisers of
+// the row's two bands.
+struct QRow {
+    int32_t *ll;
+    uint8_t *q;
+    float inv_lo, inv_hi;
+    uint32_t lim_lo, lim_hi;
+};
+// Level lv's four quantisers (uniform: scalar loads from the arguments)
+struct QLevel {
+    float inv[4];
+    uint32_t lim[4];
+};
+__device__ __forceinline__ QLevel qlevel(const QuantTab &qt, int lv) {
+    QLevel l;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        l.inv[b] = qt.inv[lv][b];
+        l.lim[b] = qt.lim[lv][b];
+    }
+    return l;
+}
+// even rows: LL (final at the last level) + HL; odd rows: LH + HH
+__device__ __forceinline__ void qrow_bands(QRow &o, const QLevel &l, bool yodd) {
+    o.inv_lo = yodd ? l.inv[2] : l.inv[0];
+    o.lim_lo = yodd ? l.lim[2] : l.lim[0];
+    o.inv_hi = yodd ? l.inv[3] : l.inv[1];
+    o.lim_hi = yodd ? l.lim[3] : l.lim[1];
+}
+// the coefficient-plane row `row` of tile-component tc
+__device__ __forceinline__ uint8_t *qplane_row(void *dst, size_t plane, int tc, size_t row, int plane_w, bool q16) {
+    return (uint8_t *)dst + (((size_t)tc * plane + row * (size_t)plane_w) << (q16 ? 1 : 2));
+}
+template <bool REV>
+__device__ __forceinline__ void store_q1(uint8_t *q, int e, int32_t x, float inv, uint32_t lim, bool q16) {
+    if (q16) ((uint16_t *)q)[e] = (uint16_t)quant_sm<REV>(x, inv, lim, 15);
+    else ((uint32_t *)q)[e] = quant_sm<REV>(x, inv, lim, 31);
+}
+// n (<= 8) values v[s0], v[s0 + 2], ... quantised to elements e0 .. e0+n-1:
+// one 16-byte store (16-bit) or two (32-bit) when whole and aligned
+template <bool REV>
+__device__ __forceinline__ void store_q8(uint8_t *q, int e0, const int32_t (&v)[24], int s0, int n, float inv,
+                                         uint32_t lim, bool q16) {
+    uint32_t w[8];
+    if (q16) {
+        // pairs: magnitudes in the halves, then the two sign bits (15, 31)
+        uint32_t p[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int32_t x0 = v[s0 + 4 * i], x1 = v[s0 + 4 * i + 2];
+            const uint32_t m = quant_mag<REV>(x0, inv, lim) | (quant_mag<REV>(x1, inv, lim) << 16);
+            p[i] = (m | (((uint32_t)x0 >> 16) & 0x8000u)) | ((uint32_t)x1 & 0x80000000u);
+        }
+        uint16_t *d = (uint16_t *)q + e0;
+        if (n == 8 && ((uintptr_t)d & 15) == 0) {
+            *(uint4 *)d = make_uint4(p[0], p[1], p[2], p[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (i < n) d[i] = (uint16_t)(p[i >> 1] >> (16 * (i & 1)));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) w[i] = quant_sm<REV>(v[s0 + 2 * i], inv, lim, 31);
+        uint32_t *d = (uint32_t *)q + e0;
+        if (n == 8 && ((uintptr_t)d & 15) == 0) {
+            ((uint4 *)d)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+            ((uint4 *)d)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (i < n) d[i] = w[i];
+        }
+    }
+}
+
 template <bool REV, int NROWS, typename RowFn>
-__device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn rows) {
+__device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, bool q16, RowFn rows) {
     const int tid = threadIdx.x;
     int32_t *base = lds + kPadL;
     if (W > 1) {
@@ -233,8 +320,8 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn r
             const int par = (s & 1) ? 0 : 1;
             const int cnt = par ? W / 2 : (W + 1) / 2;
             for (int r = 0; r < NROWS; r++) {
-                int32_t *lr, *hr;
-                if (!rows(r, lr, hr)) continue;
+                QRow o;
+                if (!rows(r, o)) continue;
                 int32_t *row = base + r * ld;
                 for (int j = tid; j < cnt; j += kDwtThreads) {
                     const int x = par + 2 * j;
@@ -249,15 +336,16 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn r
     // scale + de-interleave: consecutive threads write consecutive words
     const int nlh = (W + 1) / 2;
     for (int r = 0; r < NROWS; r++) {
-        int32_t *lrow, *hrow;
-        if (!rows(r, lrow, hrow)) continue;
+        QRow o;
+        if (!rows(r, o)) continue;
         const int32_t *row = base + r * ld;
         for (int j = tid; j < W; j += kDwtThreads) {
             const bool lo = j < nlh;
             const int x = lo ? 2 * j : 2 * (j - nlh) + 1;
             int32_t v = row[x];
             if (!REV && W > 1) v = __float_as_int(__int_as_float(v) * (lo ? INVK97 : K97));
-            (lo ? lrow : hrow)[j] = v;
+            if (lo && o.ll) o.ll[j] = v;
+            else store_q1<REV>(o.q, j, v, lo ? o.inv_lo : o.inv_hi, lo ? o.lim_lo : o.lim_hi, q16);
         }
     }
 }
@@ -269,13 +357,12 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, RowFn r
 // scaled and written de-interleaved as 8 low + 8 high words (two 16-byte
 // stores each when the row is aligned).  Rows as in hlift_write.
 template <bool REV, int NROWS, bool ALIGNED, int NT = kDwtThreads, typename RowFn>
-__device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, RowFn rows, int nrows = NROWS) {
+__device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, bool q16, RowFn rows,
+                                          int nrows = NROWS) {
     const int nseg = (W + 15) >> 4;
     const int nlh = (W + 1) / 2;
     for (int it = threadIdx.x; it < nrows * nseg; it += NT) {
         const int r = it / nseg, k = it - r * nseg;
-        int32_t *lrow, *hrow;
-        if (!rows(r, lrow, hrow)) continue;
         const int x0 = (k << 4) - 4;  // window: samples x0 .. x0+23 (even start)
         const int4 *src = (const int4 *)(lds + kPadL + r * ld + x0);
         int32_t v[24];
@@ -343,6 +430,11 @@ __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, Row
                 }
             }
         }
+        // the row's outputs, looked up only now (their registers are not held
+        // through the lifting); a row that was not staged is lifted for
+        // nothing and stores nothing
+        QRow o;
+        if (!rows(r, o)) continue;
         // slots 4..19 = samples k*16 .. k*16+15: even -> low j = x/2, odd -> high
         if (!REV && W > 1) {
 #pragma unroll
@@ -352,21 +444,22 @@ __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, Row
             }
         }
         const int j0 = k << 3;
-        int32_t *ld_ = lrow + j0, *hd = hrow + nlh + j0;
-        const bool full = (k << 4) + 16 <= W;
-        if (full && (((uintptr_t)ld_ | (uintptr_t)hd) & 15) == 0) {
-            ((int4 *)ld_)[0] = make_int4(v[4], v[6], v[8], v[10]);
-            ((int4 *)ld_)[1] = make_int4(v[12], v[14], v[16], v[18]);
-            ((int4 *)hd)[0] = make_int4(v[5], v[7], v[9], v[11]);
-            ((int4 *)hd)[1] = make_int4(v[13], v[15], v[17], v[19]);
-        } else {
+        const int rem = W - (k << 4);  // samples of the row from this segment's first on
+        const int nlo = min(8, (rem + 1) >> 1), nhi = min(8, rem >> 1);
+        if (o.ll) {
+            int32_t *ld_ = o.ll + j0;
+            if (nlo == 8 && ((uintptr_t)ld_ & 15) == 0) {
+                ((int4 *)ld_)[0] = make_int4(v[4], v[6], v[8], v[10]);
+                ((int4 *)ld_)[1] = make_int4(v[12], v[14], v[16], v[18]);
+            } else {
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int x = (k << 4) + 2 * q;
-                if (x < W) ld_[q] = v[4 + 2 * q];
-                if (x + 1 < W) hd[q] = v[5 + 2 * q];
+                for (int q = 0; q < 8; q++)
+                    if (q < nlo) ld_[q] = v[4 + 2 * q];
             }
+        } else {
+            store_q8<REV>(o.q, j0, v, 4, nlo, o.inv_lo, o.lim_lo, q16);
         }
+        store_q8<REV>(o.q, nlh + j0, v, 5, nhi, o.inv_hi, o.lim_hi, q16);
     }
 }
 
@@ -412,18 +505,20 @@ __global__ void __launch_bounds__(NT) k_dwt_band(DwtBandArgs a) {
     __syncthreads();
     // ---- horizontal lifting, scaling and de-interleaved write ----
     const int nlv = (H + 1) / 2;
-    int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
     int32_t *ll = a.ll ? (int32_t *)a.ll + (size_t)tc * a.ll_tc : nullptr;
-    auto rows = [&](int k, int32_t *&lrow, int32_t *&hrow) -> bool {
+    const bool q16 = a.qt.q16 != 0;
+    const QLevel ql = qlevel(a.qt, a.level);
+    auto rows = [&](int k, QRow &o) -> bool {
         if (k >= nkeep) return false;
         const int y = r0 + k;
         const bool ylo = (y & 1) == 0;
-        hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
-        lrow = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : hrow;
+        o.q = qplane_row(a.dst, a.plane, tc, ylo ? (y >> 1) : nlv + (y >> 1), a.plane_w, q16);
+        o.ll = (ylo && ll) ? ll + (size_t)(y >> 1) * a.ll_stride : nullptr;
+        qrow_bands(o, ql, !ylo);
         return true;
     };
-    if (W > 1 && (W & 15) == 0) hlift_seg<REV, RB, true, NT>(lds, W, ld, rows);
-    else hlift_seg<REV, RB, false, NT>(lds, W, ld, rows);
+    if (W > 1 && (W & 15) == 0) hlift_seg<REV, RB, true, NT>(lds, W, ld, q16, rows);
+    else hlift_seg<REV, RB, false, NT>(lds, W, ld, q16, rows);
 }
 
 // Level 1 with ingest, every component of a tile at once: a workgroup owns
@@ -522,14 +617,16 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
     __syncthreads();
     // ---- horizontal lifting, scaling and de-interleaved write ----
     const int nlv = (H + 1) / 2;
-    hlift_write<REV, NC * RB>(lds, W, ld, [&](int r, int32_t *&lrow, int32_t *&hrow) -> bool {
+    const bool q16 = a.qt.q16 != 0;
+    const QLevel ql = qlevel(a.qt, a.level);
+    hlift_write<REV, NC * RB>(lds, W, ld, q16, [&](int r, QRow &o) -> bool {
         const int c = r / RB, k = r - c * RB;
         if (k >= nkeep) return false;
         const int tc = tc0 + c, y = r0 + k;
         const bool ylo = (y & 1) == 0;
-        int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
-        hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
-        lrow = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride : hrow;
+        o.q = qplane_row(a.dst, a.plane, tc, ylo ? (y >> 1) : nlv + (y >> 1), a.plane_w, q16);
+        o.ll = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride : nullptr;
+        qrow_bands(o, ql, !ylo);
         return true;
     });
 }
@@ -555,6 +652,9 @@ constexpr int kStreamBand = JP2HIP_STREAM_BAND;
 #ifndef JP2HIP_L1S_R
 #define JP2HIP_L1S_R 4  // rows per horizontal batch (4 or 8)
 #endif
+// (101 VGPRs, 4 waves per SIMD for the C2 variant; a budget for 5 --
+// amdgpu_waves_per_eu(5), 5 VGPRs spilled -- measured no faster: 146.7 vs
+// 146.4 us, profiles/r05/ab_select_fold.txt)
 template <bool REV, int NC, int CPT, int RB, bool ALIGNED>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     extern __shared__ int32_t lds[];
@@ -654,6 +754,8 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     };
     fetch(1);  // row s (iteration m = s takes rows s-1, s)
     const int nlv = (H + 1) / 2;
+    const bool q16 = a.qt.q16 != 0;
+    const QLevel ql = qlevel(a.qt, 1);
     int bb = r0;  // first row of the batch being filled
     // iteration m (even): rows m-1, m arrive; the last iteration emits row r1-1
     const int m_last = ((r1 - 1 + NS - 1) + 1) & ~1;
@@ -743,15 +845,15 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         if (ylast >= r0 && (ylast - bb == RB - 1 || ylast >= r1 - 1)) {
             __syncthreads();
             const int nkeep = min(RB, r1 - bb);
-            hlift_seg<REV, NC * RB, ALIGNED>(lds, W, ld, [&](int r, int32_t *&lrow, int32_t *&hrow) -> bool {
+            hlift_seg<REV, NC * RB, ALIGNED>(lds, W, ld, q16, [&](int r, QRow &o) -> bool {
                 const int c = r / RB, k = r - c * RB;
                 if (k >= nkeep) return false;
                 const int tc = tc0 + c, y = bb + k;
                 const bool ylo = (y & 1) == 0;
-                int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
-                hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
-                lrow = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride
-                                     : hrow;
+                o.q = qplane_row(a.dst, a.plane, tc, ylo ? (y >> 1) : nlv + (y >> 1), a.plane_w, q16);
+                o.ll = (ylo && a.ll) ? (int32_t *)a.ll + (size_t)tc * a.ll_tc + (size_t)(y >> 1) * a.ll_stride
+                                     : nullptr;
+                qrow_bands(o, ql, !ylo);
                 return true;
             });
             __syncthreads();
@@ -769,6 +871,7 @@ struct DwtTailArgs {
     size_t plane;
     const int32_t *tc_w, *tc_h;
     int level, levels;
+    QuantTab qt;
 };
 
 // Levels level..levels of one tile-component, entirely in LDS, with the
@@ -806,7 +909,7 @@ __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
     // later levels the LL the previous one left in `ll` (two inlined copies of
     // the vertical pass, so each knows its address space)
     const int32_t *g_src = (const int32_t *)a.src + (size_t)tc * a.src_tc;
-    int32_t *dst = (int32_t *)a.dst + (size_t)tc * a.plane;
+    const bool q16 = a.qt.q16 != 0;
     constexpr int NR = kTailRG + 2 * kDwtHalo;
     for (int lv = a.level; lv <= a.levels; lv++) {
         const int ld = lds_row_stride(W);
@@ -845,19 +948,23 @@ __global__ void __launch_bounds__(kTailThreads) k_dwt_tail(DwtTailArgs a) {
         const int nlv = (H + 1) / 2;
         const bool last = lv == a.levels;
         const int nlh = (W + 1) / 2;
-        auto rowfn = [&](int y, int32_t *&lrow, int32_t *&hrow) -> bool {
+        const QLevel ql = qlevel(a.qt, lv);
+        auto rowfn = [&](int y, QRow &o) -> bool {
             const bool ylo = (y & 1) == 0;
-            hrow = dst + (size_t)(ylo ? (y >> 1) : nlv + (y >> 1)) * a.plane_w;
-            lrow = (ylo && !last) ? ll + (y >> 1) * nlh : hrow;
+            o.q = qplane_row(a.dst, a.plane, tc, ylo ? (y >> 1) : nlv + (y >> 1), a.plane_w, q16);
+            o.ll = (ylo && !last) ? ll + (y >> 1) * nlh : nullptr;
+            qrow_bands(o, ql, !ylo);
             return true;
         };
-        if (W > 1 && (W & 15) == 0) hlift_seg<REV, 0, true, kTailThreads>(rows_, W, ld, rowfn, H);
-        else if (W > 1) hlift_seg<REV, 0, false, kTailThreads>(rows_, W, ld, rowfn, H);
+        if (W > 1 && (W & 15) == 0) hlift_seg<REV, 0, true, kTailThreads>(rows_, W, ld, q16, rowfn, H);
+        else if (W > 1) hlift_seg<REV, 0, false, kTailThreads>(rows_, W, ld, q16, rowfn, H);
         else {  // one column: no horizontal transform (the LL is the column itself)
             for (int y = tid; y < H; y += kTailThreads) {
-                int32_t *lrow, *hrow;
-                rowfn(y, lrow, hrow);
-                lrow[0] = rows_[kPadL + y * ld];
+                QRow o;
+                rowfn(y, o);
+                const int32_t v = rows_[kPadL + y * ld];
+                if (o.ll) o.ll[0] = v;
+                else store_q1<REV>(o.q, 0, v, o.inv_lo, o.lim_lo, q16);
             }
         }
         if (last) break;
@@ -953,6 +1060,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
     a.big_endian = p.big_endian; a.mct = p.mct; a.spp_strips = p.spp_strips;
     a.ntx = p.ntx; a.tile_w = p.tile_w; a.tile_h = p.tile_h; a.row0 = p.row0;
     a.dst = p.coef;
+    a.qt = p.qt;
     a.plane_w = p.plane_w;
     a.plane = (size_t)p.plane_w * p.plane_h;
     a.tc_w = p.tc_w; a.tc_h = p.tc_h;
@@ -974,6 +1082,7 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             t.plane = a.plane;
             t.tc_w = p.tc_w; t.tc_h = p.tc_h;
             t.level = lv; t.levels = p.levels;
+            t.qt = p.qt;
             if (p.reversible) hipLaunchKernelGGL(k_dwt_tail<true>, dim3(p.ntc), dim3(kTailThreads), 0, st, t);
             else hipLaunchKernelGGL(k_dwt_tail<false>, dim3(p.ntc), dim3(kTailThreads), 0, st, t);
             return hipGetLastError() == hipSuccess;

@@ -116,6 +116,7 @@ struct DwtLaunch {
     int last_tile_w;  // width of the last tile column (the others are tile_w)
     const int32_t *tc_w, *tc_h;
     void *coef, *scratch0, *scratch1;  // scratch: ntc * ceil(plane_w/2) * ceil(plane_h/2) words each
+    QuantTab qt;                       // final coefficients are written as quantisation indices
 };
 bool launch_dwt(const DwtLaunch &p, hipStream_t st);
 

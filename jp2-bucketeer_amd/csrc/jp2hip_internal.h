@@ -37,6 +37,18 @@ struct BandQuant {
 
 BandQuant band_quant(const jp2hip_recipe &rc, int bits, int level, int band);
 
+// Every band's deadzone quantiser as the DWT's final writes apply it
+// (dwt.hip): the coefficient plane holds quantisation indices in
+// sign-magnitude, 16-bit when every band has at most 15 magnitude bit-planes
+// (8-bit sources), else 32-bit; k_quant reads them.  Entry [d][b] = level d,
+// band b (the LL band only at d = levels; levels = 0: [0][0]).
+struct QuantTab {
+    float inv[kMaxLevels + 1][4];    // 1 / Delta (1 for the reversible path)
+    uint32_t lim[kMaxLevels + 1][4]; // 2^Mb - 1: the largest index
+    int q16;
+};
+QuantTab quant_tab(const jp2hip_recipe &rc, int bits);
+
 // One code-block, as the kernels see it (uploaded as-is).
 struct BlockDesc {
     int32_t tc;         // tile-component plane index
@@ -47,7 +59,7 @@ struct BlockDesc {
     int8_t pad0, pad1;
     float inv_delta;    // irreversible quantiser reciprocal
     uint32_t pad2;
-    uint64_t bp_off;    // bit-plane storage offset, in uint64 words: (2Mb+1)*64 column masks
+    uint64_t bp_off;    // bit-plane storage offset, in uint64 words: (Mb+1)*64 column masks
                         // (kernels.hip k_quant)
     uint64_t sm_off;    // sign-magnitude storage offset, in int32 words
     uint64_t out_off;   // tier-1 output offset, bytes

@@ -52,6 +52,9 @@ struct IngestArgs {
     int ntx, tile_w, tile_h, plane_w, plane_h, spp_strips;  // strips per plane
     int row0;  // image row of local row 0 (tile-split bands)
     void *coef;
+    float inv;     // no decomposition: the one band's quantiser (QuantTab [0][0])
+    uint32_t lim;
+    int q16;
 };
 
 __device__ __forceinline__ int32_t read_sample(const IngestArgs &a, int x, int y, int c) {
@@ -81,8 +84,13 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
     size_t base = ((size_t)(ty * a.ntx + tx) * a.nc) * plane + (size_t)(y - ty * a.tile_h) * a.plane_w +
                   (x - tx * a.tile_w);
     bool domct = a.mct && a.nc >= 3;
+    // the samples are the final coefficients: quantisation indices, as the
+    // DWT writes them (dwt.hip)
+    auto put = [&](int c, uint32_t q) {
+        if (a.q16) ((uint16_t *)a.coef)[base + (size_t)c * plane] = (uint16_t)q;
+        else ((uint32_t *)a.coef)[base + (size_t)c * plane] = q;
+    };
     if (a.reversible) {
-        int32_t *o = (int32_t *)a.coef;
         int32_t v[4] = {s[0], s[1], s[2], s[3]};
         if (domct) {
             v[0] = (s[0] + 2 * s[1] + s[2]) >> 2;
@@ -91,9 +99,8 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
         }
 #pragma unroll
         for (int c = 0; c < 4; c++)
-            if (c < a.nc) o[base + (size_t)c * plane] = v[c];
+            if (c < a.nc) put(c, quant_sm<true>(v[c], a.inv, a.lim, a.q16 ? 15 : 31));
     } else {
-        float *o = (float *)a.coef;
         float f[4] = {(float)s[0], (float)s[1], (float)s[2], (float)s[3]};
         if (domct) {
             float R = f[0], G = f[1], B = f[2];
@@ -104,7 +111,7 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
         }
 #pragma unroll
         for (int c = 0; c < 4; c++)
-            if (c < a.nc) o[base + (size_t)c * plane] = f[c];
+            if (c < a.nc) put(c, quant_sm<false>(__float_as_int(f[c]), a.inv, a.lim, a.q16 ? 15 : 31));
     }
 }
 
@@ -796,7 +803,9 @@ __global__ void __launch_bounds__(256) k_untile(const uint8_t *base, const uint6
 // --------------------------------------------------------------------------
 // S4: quantisation + bit-planes.  One wavefront per code-block; lane = column.
 // Layout per block (uint64 words, lane c = column c, bit y = row y): B[p][64]
-// for p < Mb, then S[p][64] = OR_{q>=p} B[q], then sign[64].
+// for p < Mb, then sign[64].  (S[p] = OR_{q>=p} B[q], the significance state
+// after plane p, is not stored: k_t1_cm3 walks the planes top-down and builds
+// it as it goes.)
 // --------------------------------------------------------------------------
 constexpr int kZeroSpans = 9;
 struct QuantArgs {
@@ -818,7 +827,9 @@ struct QuantArgs {
 };
 
 constexpr int kQuantWaves = 2;  // code-blocks (waves) per workgroup
-template <bool REV>
+// The coefficient plane holds the quantisation indices the DWT wrote
+// (sign-magnitude, 16-bit words when Q16: QuantTab::q16)
+template <bool REV, bool Q16>
 __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     extern __shared__ uint64_t lds_planes[];  // [wave][plane][lane], a.max_mb planes per wave
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -834,40 +845,40 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     bool act = lane < d.w;
     // the block's first row (wave-uniform: each row load is a scalar base +
     // the lane's column offset, no per-row address registers)
-    const int32_t *src = (const int32_t *)a.coef + (size_t)d.tc * a.plane_w * a.plane_h +
-                         (size_t)d.y0 * a.plane_w + d.x0;
+    const size_t e0 = (size_t)d.tc * a.plane_w * a.plane_h + (size_t)d.y0 * a.plane_w + d.x0;
     const int cl = act ? lane : 0;
     int32_t *sm = a.sm + d.sm_off + lane;
     // the sign-magnitude copy is read only by the 64-bit distortion path of
     // planes above 23 (below) and by the debug dumps
     const bool keep_sm = a.keep_sm || d.Mb > 24;
     uint32_t vmax = 0;
-    uint32_t lim = (1u << d.Mb) - 1u;
     // the lane's column stays in registers (sign | magnitude) for the
-    // bit-plane and distortion passes: the coefficients are read from HBM
-    // once.  All 64 row loads are in flight at once; rows past the block end
+    // bit-plane and distortion passes: the indices are read from HBM once.
+    // All 64 row loads are in flight at once; rows past the block end
     // re-read its last row and lanes past its width read column 0 -- values
     // of the block, so its maximum is unchanged -- and are cleared from the
     // bit-plane masks (`valid`), not row by row.
     uint32_t col[64];
     const int hm1 = d.h - 1;
+    if constexpr (Q16) {
+        const uint16_t *src = (const uint16_t *)a.coef + e0;
 #pragma unroll
-    for (int y = 0; y < 64; y++) col[y] = (uint32_t)src[(size_t)min(y, hm1) * a.plane_w + cl];
+        for (int y = 0; y < 64; y++) col[y] = src[(size_t)min(y, hm1) * a.plane_w + cl];
+    } else {
+        const uint32_t *src = (const uint32_t *)a.coef + e0;
+#pragma unroll
+        for (int y = 0; y < 64; y++) col[y] = src[(size_t)min(y, hm1) * a.plane_w + cl];
+    }
     // magnitudes in col[], the signs straight into the sign column (the sign
     // bit as stored: a -0.0 quantises to 0, and a zero's sign is never coded)
+    constexpr int kSb = Q16 ? 15 : 31;
     uint32_t sg_lo = 0, sg_hi = 0;
 #pragma unroll
     for (int y = 0; y < 64; y++) {
         const uint32_t raw = col[y];
-        uint32_t v;
-        if constexpr (REV) {
-            v = (uint32_t)abs((int32_t)raw);
-        } else {
-            v = (uint32_t)floorf(__uint_as_float(raw & 0x7FFFFFFFu) * d.inv_delta);
-        }
-        if (y < 32) sg_lo |= (raw >> 31) << y;
-        else sg_hi |= (raw >> 31) << (y - 32);
-        v = min(v, lim);
+        const uint32_t v = raw & ((1u << kSb) - 1u);
+        if (y < 32) sg_lo |= (raw >> kSb) << y;
+        else sg_hi |= (raw >> kSb) << (y - 32);
         col[y] = v;
         vmax = max(vmax, v);
     }
@@ -885,11 +896,10 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
     const int P = __builtin_amdgcn_readfirstlane(vmax ? 32 - __clz(vmax) : 0);
     if (lane == 0) a.P[b] = (uint8_t)P;
     // column masks (lane c, bit y = row y): BT[p][c] = bit p of the
-    // column, ST[p][c] = OR of BT[q], q >= p, then the sign column SGT[c] --
-    // the layout the tier-1 context modelling reads (t1.hip k_t1_cm3)
+    // column, then the sign column SGT[c] -- the layout the tier-1 context
+    // modelling reads (t1.hip k_t1_cm3)
     uint64_t *BT = a.bp + d.bp_off;
-    uint64_t *ST = BT + (size_t)d.Mb * 64;
-    uint64_t *SGT = BT + (size_t)2 * d.Mb * 64;
+    uint64_t *SGT = BT + (size_t)d.Mb * 64;
     SGT[lane] = sgcol;
     // every plane's column mask, kept in LDS for the distortion sums below.
     // Four planes at a time: a row's 4 bits are spread to the 4 bytes of a
@@ -962,7 +972,6 @@ __global__ void __launch_bounds__(64 * kQuantWaves) k_quant(QuantArgs a) {
             }
         }
         colS |= Bp;
-        ST[(size_t)p * 64 + lane] = colS;
         // insignificant samples with a significant 8-neighbour (rows < h,
         // columns < w)
         // (DPP whole-wave shifts on every lane: lanes 0 / 63 receive 0)
@@ -1521,7 +1530,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select(SelectArgs a) {
 // candidate key v with (bytes above the bin) + (candidate bytes with key >= v)
 // > budget is the first key not taken, K' = v + 1.  Workgroup 0 also zeroes
 // the list fill counters for the next k_select (the device rate loop runs
-// several).
+// several).  (Folded into k_select -- its group's last workgroup to finish
+// resolving the layers, after a device-scope release/acquire count -- the
+// pair took 104.5 us alone instead of 53 + 23 with the layers in turn, and
+// 116.9 with a wave per layer, 4x longer candidate walks per wave; the C2
+// bench did not move: profiles/r05/ab_select_fold.txt.)
 __global__ void __launch_bounds__(kSelThreads) k_select_resolve(SelectArgs a) {
     __shared__ SelBins sh;
     // the narrowing state and the survivors
@@ -2164,6 +2177,8 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
 #else
     const char *dd = nullptr;
 #endif
+    // the final coefficients are written as quantisation indices
+    const QuantTab qt = quant_tab(plan.rc, plan.bits);
     if (plan.rc.levels == 0) {
         // S1+S2 only: no decomposition
         IngestArgs ia;
@@ -2178,6 +2193,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         ia.plane_w = plan.plane_w; ia.plane_h = plan.plane_h;
         ia.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
         ia.coef = coef.ptr;
+        ia.inv = qt.inv[0][0]; ia.lim = qt.lim[0][0]; ia.q16 = qt.q16;
         dim3 gi((plan.w + 63) / 64, (plan.band_h + 3) / 4);
         hipLaunchKernelGGL(k_ingest, gi, dim3(256), 0, stream, ia);
         HIPCHECK(hipGetLastError());
@@ -2198,6 +2214,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.levels = plan.rc.levels; dl.reversible = plan.rc.reversible;
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
         dl.coef = coef.ptr; dl.scratch0 = llbuf0.ptr; dl.scratch1 = llbuf1.ptr;
+        dl.qt = qt;
         bool dwt_ok = true;
         REPEAT_IF(1) dwt_ok = dwt_ok && launch_dwt(dl, stream);
         if (!dwt_ok) {
@@ -2206,7 +2223,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         }
     }
     HIPCHECK(hipEventRecord(ev[2], stream));
-    if (dd && !dump(dd, "dwt.bin", coef, plane * plan.ntc * 4, err)) return false;
+    if (dd && !dump(dd, "dwt.bin", coef, plane * plan.ntc * (qt.q16 ? 2 : 4), err)) return false;
     // S4
     QuantArgs qa;
     qa.blocks = (const BlockDesc *)blocks.ptr;
@@ -2268,8 +2285,14 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (nb) {
         const dim3 gq((nb + kQuantWaves - 1) / kQuantWaves), bq(64 * kQuantWaves);
         REPEAT_IF(2) {
-            if (plan.rc.reversible) hipLaunchKernelGGL(k_quant<true>, gq, bq, qlds * kQuantWaves, stream, qa);
-            else hipLaunchKernelGGL(k_quant<false>, gq, bq, qlds * kQuantWaves, stream, qa);
+            const size_t ql = qlds * kQuantWaves;
+            if (plan.rc.reversible) {
+                if (qt.q16) hipLaunchKernelGGL((k_quant<true, true>), gq, bq, ql, stream, qa);
+                else hipLaunchKernelGGL((k_quant<true, false>), gq, bq, ql, stream, qa);
+            } else {
+                if (qt.q16) hipLaunchKernelGGL((k_quant<false, true>), gq, bq, ql, stream, qa);
+                else hipLaunchKernelGGL((k_quant<false, false>), gq, bq, ql, stream, qa);
+            }
         }
     }
     HIPCHECK(hipGetLastError());

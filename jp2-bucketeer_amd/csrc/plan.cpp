@@ -164,6 +164,23 @@ BandQuant band_quant(const jp2hip_recipe &rc, int bits, int d, int band) {
     return q;
 }
 
+QuantTab quant_tab(const jp2hip_recipe &rc, int bits) {
+    QuantTab t;
+    std::memset(&t, 0, sizeof t);
+    int mb = 0;
+    auto put = [&](int d, int b) {
+        const BandQuant q = band_quant(rc, bits, d, b);
+        t.inv[d][b] = q.inv_delta;
+        t.lim[d][b] = q.Mb >= 32 ? ~0u : (1u << q.Mb) - 1u;
+        mb = std::max(mb, q.Mb);
+    };
+    for (int d = 1; d <= rc.levels; d++)
+        for (int b = 1; b < 4; b++) put(d, b);
+    put(rc.levels, 0);
+    t.q16 = mb <= 15;
+    return t;
+}
+
 bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits,
                 std::string &err) {
     if (w <= 0 || h <= 0 || nc < 1 || nc > 4 || (bits != 8 && bits != 16)) {
@@ -288,7 +305,7 @@ bool build_plan(Plan &P, const jp2hip_recipe &rc, int w, int h, int nc, int bits
                                         uint64_t cap = ((uint64_t)bd.w * bd.h * (q.Mb + 1)) / 2 + 1024;
                                         cap = (cap + 15) & ~(uint64_t)15;
                                         bd.out_cap = (uint32_t)cap;
-                                        bpw += (uint64_t)(2 * q.Mb + 1) * 64;  // column masks (kernels.hip k_quant)
+                                        bpw += (uint64_t)(q.Mb + 1) * 64;  // column masks (kernels.hip k_quant)
                                         smw += (uint64_t)64 * bd.h;
                                         ob += cap;
                                         P.blocks.push_back(bd);
@@ -378,7 +395,7 @@ void make_subplan(const Plan &full, int tr0, int tr1, Plan &S) {
             b.out_off -= f.out_off;
         }
         const BlockDesc &l = S.blocks.back();
-        S.bp_words = l.bp_off + (uint64_t)(2 * l.Mb + 1) * 64;
+        S.bp_words = l.bp_off + (uint64_t)(l.Mb + 1) * 64;
         S.sm_words = l.sm_off + (uint64_t)64 * l.h;
         S.out_bytes = l.out_off + l.out_cap;
     }

@@ -554,7 +554,7 @@ __device__ __forceinline__ uint2 cm_selectors(int K) {
 }
 
 // A block's descriptor fields k_t1_cm3 uses (wave-uniform), and its first
-// masks (the sign column, B and S of the top plane).
+// masks (the sign column and B of the top plane).
 struct CmBlk {
     int b, P, c, w, h, Mb, band;
     uint64_t bp_off, slot;
@@ -574,14 +574,13 @@ __device__ __forceinline__ CmBlk cm_blk_load(const T1CmArgs &a, int b) {
     return k;
 }
 struct CmMasks {
-    uint64_t SG, B, S0;
+    uint64_t SG, B;
 };
 __device__ __forceinline__ CmMasks cm_masks_load(const T1CmArgs &a, const CmBlk &k, int lane) {
     const uint64_t *CT = a.bp + k.bp_off;
     CmMasks m;
-    m.SG = CT[(size_t)2 * k.Mb * 64 + lane];
+    m.SG = CT[(size_t)k.Mb * 64 + lane];
     m.B = CT[(size_t)(k.P - 1) * 64 + lane];
-    m.S0 = CT[(size_t)(k.Mb + k.P - 1) * 64 + lane];
     return m;
 }
 
@@ -620,10 +619,10 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
     CmMasks mk = cm_masks_load(a, cur, lane);
     int idx_next = bi + stride < nblk ? a.dlist[bi + stride] : -1;
     for (;;) {
-        const int b = cur.b, P = cur.P, c = cur.c, w = cur.w, h = cur.h, Mb = cur.Mb, band = cur.band;
+        const int b = cur.b, P = cur.P, c = cur.c, w = cur.w, h = cur.h, band = cur.band;
         const bool vl = lane < w;
         const uint64_t *CT = a.bp + cur.bp_off;
-        uint64_t Bl = mk.B, S0l = mk.S0;
+        uint64_t Bl = mk.B;
         const uint64_t SG = vl ? mk.SG : 0ull;
         const uint64_t LSG = col_left(SG, lane), RSG = col_right(SG, lane);
         uint64_t S1 = 0, S2 = 0;
@@ -634,11 +633,9 @@ __global__ void __launch_bounds__(64 * kCmWaves) k_t1_cm3(T1CmArgs a) {
         int idx_after = -1;
         for (int k = 0; k < c; k++) {
             const int p = P - 1 - k;
-            const uint64_t B = vl ? Bl : 0ull, S0 = vl ? S0l : 0ull;
-            if (k + 1 < c) {  // the next plane's masks, in flight during this one
-                Bl = CT[(size_t)(p - 1) * 64 + lane];
-                S0l = CT[(size_t)(Mb + p - 1) * 64 + lane];
-            }
+            // S[p] = S[p+1] | B[p] (planes above the top one are empty)
+            const uint64_t B = vl ? Bl : 0ull, S0 = S1 | B;
+            if (k + 1 < c) Bl = CT[(size_t)(p - 1) * 64 + lane];  // the next plane's mask, in flight during this one
             if (k == 0 && idx_next >= 0) {  // the next block's descriptor, and the index after it
                 nxt = cm_blk_load(a, idx_next);
                 if (bi + 2 * stride < nblk) idx_after = a.dlist[bi + 2 * stride];
@@ -769,17 +766,56 @@ __device__ __forceinline__ void ring_byteout(Mq &m, uint8_t *ring, uint32_t lb) 
 // code padding.
 // --------------------------------------------------------------------------
 constexpr int kMqChunk = 16;
+// Census experiments (debug builds, tests/tools/mq_census.py; output not
+// valid): 2 = the modeller alone (no coder wave, no chunk barrier); 3 = as 2
+// and the next-state table read replaced by register values (what the LDS
+// round trip costs the modeller)
+#ifndef JP2HIP_MQ_EXP
+#define JP2HIP_MQ_EXP 0
+#endif
 constexpr uint32_t kPadWord = 0x01010101u * kPadDecision;
+// The modeller's interval register and the state words' Qe field are scaled
+// by 2^kQeShift.  At 2^15 (JP2HIP_MQ_MASKS, the product) A and Qe stay below
+// 2^31, so "A - Qe < Qe" and "A < 0x8000" are sign bits of 32-bit
+// differences: every select of a decision is a bit-field select on VGPR masks
+// (v_bfi), with no compare -> VCC -> v_cndmask or SALU mask hop on the
+// chain (a dependent VALU op costs 9 cycles on gfx950, a v_cmp -> v_cndmask
+// hop 14.5: tests/tools/probe/latency_probe.hip).
+#ifndef JP2HIP_MQ_MASKS
+#define JP2HIP_MQ_MASKS 0
+#endif
+constexpr int kQeShift = JP2HIP_MQ_MASKS ? 15 : 16;
 
-// the state word of entry e (Qe << 16 | 8 e | MPS)
-__device__ __forceinline__ uint32_t mq_word(int e) { return ((uint32_t)c_qe[e >> 1] << 16) | ((uint32_t)e << 3) | (uint32_t)(e & 1); }
+// the state word of entry e (Qe << kQeShift | 8 e | MPS)
+__device__ __forceinline__ uint32_t mq_word(int e) {
+    return ((uint32_t)c_qe[e >> 1] << kQeShift) | ((uint32_t)e << 3) | (uint32_t)(e & 1);
+}
 
 // modeller: one decision; returns the context's next state, *code = the
 // coder's input word (C's addend << 16 | renormalisation shifts).  A = the
 // interval register << 16.
 __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, const uint8_t *tab, const uint32_t d,
                                              uint32_t &code) {
+#if JP2HIP_MQ_EXP == 3
+    const uint2 nx = make_uint2(t ^ 0x10008u, t ^ 0x20010u);
+#else
     const uint2 nx = *(const uint2 *)(tab + (t & 0x3F8u));  // NMPS / NLPS words, read first
+#endif
+#if JP2HIP_MQ_MASKS
+    const uint32_t qe = t & 0xFFFF8000u;                              // Qe << 15
+    const int32_t lpsm = __builtin_amdgcn_sbfe((int)(d ^ t), 0, 1);   // -1: the LPS is coded
+    const uint32_t A1 = A - qe;
+    const int32_t ltm = (int32_t)(A1 - qe) >> 31;                     // -1: A - Qe < Qe
+    const uint32_t keepm = ~(uint32_t)(ltm ^ lpsm);                   // -1: A - Qe stays, C gains Qe
+    const uint32_t An = (A1 & keepm) | (qe & ~keepm);
+    // -1: renormalise (the LPS, or A - Qe < 0x8000: bit 30 of A1 clear)
+    const uint32_t renm = (uint32_t)lpsm | ~(uint32_t)__builtin_amdgcn_sbfe((int)A1, 30, 1);
+    const uint32_t n = (uint32_t)__builtin_clz(An) - 1u;              // renormalisation shifts
+    A = An << n;
+    code = (qe & keepm) | n;
+    const uint32_t tl = (nx.y & (uint32_t)lpsm) | (nx.x & ~(uint32_t)lpsm);
+    return (tl & renm) | (t & ~renm);
+#else
     const uint32_t qe = t & 0xFFFF0000u;  // Qe << 16
     const bool isM = d == (t & 1u);
     const uint32_t A1 = A - qe;
@@ -790,6 +826,7 @@ __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, cons
     A = An << n;
     code = (keep ? qe : 0u) | n;
     return ren ? (isM ? nx.x : nx.y) : t;
+#endif
 }
 
 // coder: C += add, then n shifts with their byte-outs.  The (at most one,
@@ -800,8 +837,8 @@ __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, cons
 // in one renormalisation needs n >= CT + 7 >= 8), so its test is left out.
 template <bool TWO>
 __device__ __forceinline__ void mq_code(Mq &m, const uint32_t code, uint8_t *ring, uint32_t lb) {
-    const uint32_t add = code >> 16;
-    const int n = (int)(code & 0xFFFFu);
+    const uint32_t add = code >> kQeShift;
+    const int n = (int)(code & 0x1Fu);
     const uint32_t C0 = m.C + add;
     const int CT = m.CT;
     const bool bo = n >= CT;  // a byte-out inside this renormalisation
@@ -902,7 +939,7 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
     cx[0] = mq_word(2 * 4);
     cx[CX_RL * 64] = mq_word(2 * 3);
     cx[CX_UNI * 64] = mq_word(2 * 46);
-    uint32_t A = 0x8000u << 16;
+    uint32_t A = 0x8000u << kQeShift;
     int nseg = 0, s = 0, k = 0, pass = 2, left = 0, Pt = 0;
     uint32_t cap = 0;
     const uint8_t *sbase = nullptr;
@@ -960,9 +997,11 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         const int buf = it & 1;
         sh.segs[buf][lane] = s;
         if (!__any(active)) {
-            sh.finA[lane] = A >> 16;
+            sh.finA[lane] = A >> kQeShift;
             if (lane == 0) sh.more[buf] = 0;
+#if JP2HIP_MQ_EXP < 2
             __syncthreads();
+#endif
             break;
         }
         if (lane == 0) sh.more[buf] = 1;
@@ -999,9 +1038,19 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
             nx1 = nx2;
         }
         const uint64_t c1 = a.dbg ? __builtin_readcyclecounter() : 0;
+#if JP2HIP_MQ_EXP >= 2
+        __builtin_amdgcn_wave_barrier();
+#else
         __syncthreads();  // chunk `it` ready; the coder is done with chunk it - 1
+#endif
         if (a.dbg) cyc_wait += __builtin_readcyclecounter() - c1;
     }
+#if JP2HIP_MQ_EXP >= 2
+    if (b >= 0) {  // no coder ran: the block codes as empty downstream
+        a.npasses[b] = 0;
+        a.lengths[b] = 0;
+    }
+#endif
     if (a.dbg && b >= 0) {  // debug census: decisions, modeller cycles, of which at the barrier
         a.dbg[(size_t)b * 6 + 0] = ndec;
         a.dbg[(size_t)b * 6 + 1] = (int64_t)(__builtin_readcyclecounter() - cyc0);
@@ -1127,7 +1176,9 @@ __global__ void __launch_bounds__(128) k_t1_mq(T1MqArgs a) {
     }
     __syncthreads();
     if (tid < 64) mq_modeller(a, sh);
+#if JP2HIP_MQ_EXP < 2
     else mq_coder(a, sh);
+#endif
     if (tid == 64) atomicMax(&a.span[1], (unsigned long long)wall_clock64());
 }
 

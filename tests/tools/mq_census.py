@@ -21,10 +21,20 @@ import jp2hip  # noqa: E402
 img = im.synth_rgb8(4000, 6000, seed=1234)
 tif = im.tiff_bytes(img)
 enc = jp2hip.Encoder(0, profile=True)
-enc.encode_tiff(tif, jp2hip.LOSSY)
+try:
+    enc.encode_tiff(tif, jp2hip.LOSSY)
+except jp2hip.Jp2hipError:
+    pass
 d = tempfile.mkdtemp()
 os.environ["JP2HIP_DUMP_DIR"] = d
-out, st = enc.encode_tiff(tif, jp2hip.LOSSY)
+try:
+    out, st = enc.encode_tiff(tif, jp2hip.LOSSY)
+except jp2hip.Jp2hipError as ex:  # census experiment builds (JP2HIP_MQ_EXP) do not produce valid files
+    print("encode:", ex)
+
+    class _St:
+        t1_mq_ms = float("nan")
+    st = _St()
 a = np.fromfile(os.path.join(d, "mqdbg.bin"), dtype=np.int64).reshape(-1, 6)
 dec, mcyc, mwait, ccyc, cwait, pos = (a[:, i] for i in range(6))
 m = dec > 0
@@ -38,8 +48,9 @@ for w in (0, 1, 2, 5, 20, 100):
     mc, mw = mcyc[m][sel].max(), mwait[m][sel].max()
     cc, cw = ccyc[m][sel].max(), cwait[m][sel].max()
     print(f"wave {w:4d}: decisions max {dm:6d}  modeller {mc / dm:6.1f} cyc/dec ({mw / mc * 100:4.1f}% at barrier)"
-          f"  coder {cc / dm:6.1f} cyc/dec ({cw / cc * 100:4.1f}% at barrier)")
-print("stages", {k: round(v, 3) for k, v in st.as_dict().items() if k.endswith("_ms")})
+          f"  coder {cc / dm:6.1f} cyc/dec ({(cw / cc * 100) if cc else 0:4.1f}% at barrier)")
+if hasattr(st, "as_dict"):
+    print("stages", {k: round(v, 3) for k, v in st.as_dict().items() if k.endswith("_ms")})
 sel = os.path.join(d, "seldbg.bin")
 if os.path.exists(sel):
     s = np.fromfile(sel, dtype=np.int64)
