@@ -107,7 +107,15 @@ uint8_t *out_alloc(size_t n) {
     }
     const size_t cap = n + n / 8 + 4096;  // room for a slightly larger file next time
     void *b = nullptr;
+    static const bool log = getenv("JP2HIP_LOG_POOL") != nullptr;  // diagnostics: pool misses
+    const auto t0 = std::chrono::steady_clock::now();
     if (hipHostMalloc(&b, cap, hipHostMallocDefault) != hipSuccess || !b) return nullptr;
+    if (log) {
+        std::lock_guard<std::mutex> lk(P.mu);
+        fprintf(stderr, "jp2hip pool miss: %zu bytes pinned in %.1f ms (idle %zu buffers, %zu bytes)\n", cap,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                P.idle.size(), P.idle_bytes);
+    }
     std::lock_guard<std::mutex> lk(P.mu);
     P.live[b] = cap;
     return (uint8_t *)b;

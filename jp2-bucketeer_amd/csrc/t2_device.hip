@@ -1296,7 +1296,11 @@ bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, u
     if (nb) hipLaunchKernelGGL(k_t2_copy, dim3((nb + 3) / 4), dim3(256), 0, stream, a, nb, (const uint8_t *)t1out.ptr);
     HIPCHECK(hipGetLastError());
     // host_dst is pinned (api.cpp out_alloc)
-#ifndef JP2HIP_D2H_BLIT
+#if defined(JP2HIP_DIAG_NO_D2H)  // diagnostic builds only: the code-stream never leaves the GPU (output invalid)
+    HIPCHECK(hipEventRecord(ev[9], stream));
+    if (!host_wait(err)) return false;
+    (void)host_dst;
+#elif !defined(JP2HIP_D2H_BLIT)
     if (part_bytes) {
         // on a DMA engine, released by the stream (dma_to_host): no blit
         // kernel competes with the other contexts' kernels for CUs
