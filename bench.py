@@ -799,7 +799,7 @@ def main():
         dist.destroy_process_group()
 
 
-def lossless_c3(enc, steps=2, inflight=6, n_each=4):
+def lossless_c3(enc, steps=2, inflight=8, n_each=4):
     """C3 (configs[2]): 10000x8000 RGB16 lossless 5/3, 1024^2 tiles, the
     conversion the reference's service runs (ImageWorkerVerticle.java:64).
     One image alone (latency at the C call) and `inflight` images at once on
