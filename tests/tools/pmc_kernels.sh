@@ -10,7 +10,7 @@ export GPU_MAX_HW_QUEUES=16 JP2HIP_KEEP_HW_QUEUES=1
 o=gpurun_out/${1:-pmc}
 re=${2:-"k_dwt|k_quant|k_t1_cm|k_t1_mq"}
 mkdir -p $o
-B="python bench.py --inflight 1 --steps 3 --warmup 1 --no-cpu-baseline --no-lossless"
+B="python bench.py --inflight 1 --steps 3 --warmup 1 --no-extras"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --kernel-include-regex "$re" -d $o/p1 -o run --output-format csv -- $B > $o/p1.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA --kernel-include-regex "$re" -d $o/p2 -o run --output-format csv -- $B > $o/p2.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$re" -d $o/p3 -o run --output-format csv -- $B > $o/p3.log 2>&1 || exit 1
