@@ -775,16 +775,12 @@ constexpr int kMqChunk = 16;
 #endif
 constexpr uint32_t kPadWord = 0x01010101u * kPadDecision;
 // The modeller's interval register and the state words' Qe field are scaled
-// by 2^kQeShift.  At 2^15 (JP2HIP_MQ_MASKS, the product) A and Qe stay below
-// 2^31, so "A - Qe < Qe" and "A < 0x8000" are sign bits of 32-bit
-// differences: every select of a decision is a bit-field select on VGPR masks
-// (v_bfi), with no compare -> VCC -> v_cndmask or SALU mask hop on the
-// chain (a dependent VALU op costs 9 cycles on gfx950, a v_cmp -> v_cndmask
-// hop 14.5: tests/tools/probe/latency_probe.hip).
-#ifndef JP2HIP_MQ_MASKS
-#define JP2HIP_MQ_MASKS 0
-#endif
-constexpr int kQeShift = JP2HIP_MQ_MASKS ? 15 : 16;
+// by 2^16.  (Measured and dropped: scaled by 2^15, so that "A - Qe < Qe" and
+// "A < 0x8000" are sign bits of 32-bit differences and every select is a
+// bit-field select on VGPR masks, no compare -> VCC -> v_cndmask hop: 255
+// instead of 251 cycles per decision, MQ +3 %, C2 bench -3 %:
+// profiles/r05/ab_mq_masks.txt.)
+constexpr int kQeShift = 16;
 
 // the state word of entry e (Qe << kQeShift | 8 e | MPS)
 __device__ __forceinline__ uint32_t mq_word(int e) {
@@ -801,21 +797,6 @@ __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, cons
 #else
     const uint2 nx = *(const uint2 *)(tab + (t & 0x3F8u));  // NMPS / NLPS words, read first
 #endif
-#if JP2HIP_MQ_MASKS
-    const uint32_t qe = t & 0xFFFF8000u;                              // Qe << 15
-    const int32_t lpsm = __builtin_amdgcn_sbfe((int)(d ^ t), 0, 1);   // -1: the LPS is coded
-    const uint32_t A1 = A - qe;
-    const int32_t ltm = (int32_t)(A1 - qe) >> 31;                     // -1: A - Qe < Qe
-    const uint32_t keepm = ~(uint32_t)(ltm ^ lpsm);                   // -1: A - Qe stays, C gains Qe
-    const uint32_t An = (A1 & keepm) | (qe & ~keepm);
-    // -1: renormalise (the LPS, or A - Qe < 0x8000: bit 30 of A1 clear)
-    const uint32_t renm = (uint32_t)lpsm | ~(uint32_t)__builtin_amdgcn_sbfe((int)A1, 30, 1);
-    const uint32_t n = (uint32_t)__builtin_clz(An) - 1u;              // renormalisation shifts
-    A = An << n;
-    code = (qe & keepm) | n;
-    const uint32_t tl = (nx.y & (uint32_t)lpsm) | (nx.x & ~(uint32_t)lpsm);
-    return (tl & renm) | (t & ~renm);
-#else
     const uint32_t qe = t & 0xFFFF0000u;  // Qe << 16
     const bool isM = d == (t & 1u);
     const uint32_t A1 = A - qe;
@@ -826,7 +807,6 @@ __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, cons
     A = An << n;
     code = (keep ? qe : 0u) | n;
     return ren ? (isM ? nx.x : nx.y) : t;
-#endif
 }
 
 // coder: C += add, then n shifts with their byte-outs.  The (at most one,
