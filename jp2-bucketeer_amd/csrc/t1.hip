@@ -781,17 +781,21 @@ constexpr uint32_t kPadWord = 0x01010101u * kPadDecision;
 // instead of 251 cycles per decision, MQ +3 %, C2 bench -3 %:
 // profiles/r05/ab_mq_masks.txt.)
 constexpr int kQeShift = 16;
+#ifndef JP2HIP_MQ_SCHED
+#define JP2HIP_MQ_SCHED 1
+#endif
+
 
 // the state word of entry e (Qe << kQeShift | 8 e | MPS)
 __device__ __forceinline__ uint32_t mq_word(int e) {
     return ((uint32_t)c_qe[e >> 1] << kQeShift) | ((uint32_t)e << 3) | (uint32_t)(e & 1);
 }
 
-// modeller: one decision; returns the context's next state, *code = the
-// coder's input word (C's addend << 16 | renormalisation shifts).  A = the
-// interval register << 16.
+// modeller: one decision; returns the context's next state and stores the
+// coder's input word (C's addend << 16 | renormalisation shifts) to *code.
+// A = the interval register << 16.
 __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, const uint8_t *tab, const uint32_t d,
-                                             uint32_t &code) {
+                                             uint32_t *code) {
 #if JP2HIP_MQ_EXP == 3
     const uint2 nx = make_uint2(t ^ 0x10008u, t ^ 0x20010u);
 #else
@@ -805,7 +809,19 @@ __device__ __forceinline__ uint32_t mq_model(uint32_t &A, const uint32_t t, cons
     const bool ren = !isM || A1 < 0x80000000u;
     const uint32_t n = (uint32_t)__builtin_clz(An);  // renormalisation shifts
     A = An << n;
-    code = (keep ? qe : 0u) | n;
+    const uint32_t cw = (keep ? qe : 0u) | n;
+#if JP2HIP_MQ_SCHED
+    // the interval register's chain (and what the caller computed before the
+    // call) is issued in full before the wait for the table read: it runs
+    // under the read's latency instead of after it (the wave issues in
+    // order, and the first use of nx waits for LDS).  Census 250 -> 237
+    // cycles per decision, k_t1_mq alone 2.48 -> 2.36 ms on C2
+    // (profiles/r05/mq/ab_sched.txt; the code word stored ahead of the wait
+    // as well: 239; the next table read issued ahead of the next decision's
+    // stream bookkeeping: 245)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    *code = cw;
     return ren ? (isM ? nx.x : nx.y) : t;
 }
 
@@ -897,6 +913,9 @@ struct MqShared {
     uint32_t finA[64];                     // the interval register at the end (mq_flush)
     int32_t blk[64];                       // the lane's block, -1 none
     int32_t more[2];                       // chunk present
+#ifdef JP2HIP_MQ_LDS_PAD  // residency experiments only: bytes of unused LDS per workgroup
+    uint8_t pad_[JP2HIP_MQ_LDS_PAD];
+#endif
 };
 
 // Modeller (wave 0).  One lane per block walks the block's passes -- segments
@@ -1005,11 +1024,10 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
                 nxt_cx = __builtin_amdgcn_ubfe(w[(j + 1) >> 2], ((j + 1) & 3) * 8 + 1, 5);
                 nt = cx[nxt_cx * 64];
             }
-            uint32_t code;
-            const uint32_t tn = mq_model(A, t, mqt, dd, code);
-            out[j * 64] = code;
+            const bool same = nxt_cx == cur_cx;  // (before the call: ahead of the table wait)
+            const uint32_t tn = mq_model(A, t, mqt, dd, &out[j * 64]);
             cx[cur_cx * 64] = tn;
-            t = (nxt_cx == cur_cx) ? tn : nt;
+            t = same ? tn : nt;
         }
         if (active) {
             left -= min(16, left);
