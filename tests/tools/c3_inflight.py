@@ -4,7 +4,8 @@
 (first line: one image's stats -- decisions, tier-1 bytes, stage times)."""
 import os, sys, json
 ns = [int(x) for x in sys.argv[1:]] or [4]
-os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(ns) + 4))  # as bench.py (the box default is 4)
+if not os.environ.get("JP2HIP_KEEP_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(ns) + 4))  # as bench.py (the box default is 4)
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 import torch  # noqa: E402
