@@ -123,6 +123,20 @@ def test_golden_lossy_cases(encoder, golden, testjpx_pixels, name):
     assert ps >= c["opj_psnr"] - 0.1
 
 
+@pytest.mark.parametrize("levels", [6, 0])
+@pytest.mark.parametrize("rate", [3.0, 0.0])
+def test_fine_quantiser_32bit_index_plane(encoder, levels, rate):
+    """An irreversible step fine enough that some band needs more than 15
+    magnitude bit-planes: the DWT (or, with no decomposition, the ingest)
+    writes 32-bit quantisation indices instead of 16-bit ones (QuantTab::q16,
+    csrc/plan.cpp quant_tab) -- byte-identical to the oracle either way, rate
+    driven or not."""
+    img = _img(260, 390, 3, 8, seed=17)
+    rc = jp2hip.recipe(jp2hip.LOSSY, qstep=1.0 / 65536, levels=levels, rate_bpp=rate)
+    got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSY, rc)
+    assert got == ol.encode(img, ol.copy_recipe(rc))
+
+
 @pytest.mark.parametrize("cblk", [4, 5])
 @pytest.mark.parametrize("lossless", [True, False])
 def test_small_codeblocks_identical_to_oracle(encoder, cblk, lossless):
