@@ -784,6 +784,9 @@ constexpr int kQeShift = 16;
 #ifndef JP2HIP_MQ_SCHED
 #define JP2HIP_MQ_SCHED 1
 #endif
+#ifndef JP2HIP_MQ_PASS_PREFETCH
+#define JP2HIP_MQ_PASS_PREFETCH 1
+#endif
 
 
 // the state word of entry e (Qe << kQeShift | 8 e | MPS)
@@ -952,6 +955,31 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
     // is about one chunk's 16 decisions
     uint4 cnt = make_uint4(0u, 0u, 0u, 0u), cur = pad4, nx1 = pad4;
     int64_t ndec = 0;
+#if JP2HIP_MQ_PASS_PREFETCH
+    // The pass after the current one, loaded as soon as the current one
+    // starts (its plane's counts when it opens a plane, its first two
+    // chunks): a pass switch then takes registers instead of a dependent
+    // counts -> stream load while the whole wave waits -- in a wave of 64
+    // blocks some lane switches passes in most chunks
+    int pf_pass = 0, pf_k = 0, pf_valid = 0;
+    uint4 pf_cnt = cnt, pf_cur = pad4, pf_nx1 = pad4;
+    const uint4 *pf_ptr = nullptr;
+    auto prefetch = [&]() {
+        pf_valid = 0;
+        if (s + 1 >= nseg) return;
+        const int np = pass == 2 ? 0 : pass + 1, nk = pass == 2 ? k + 1 : k;
+        const uint4 nc = np == 0 ? cntp[nk] : cnt;
+        const int o_mrp = ((int)cnt.x + 15) & ~15;
+        const int o_cup = (o_mrp + (int)cnt.y + 15) & ~15;
+        pf_ptr = (const uint4 *)(sbase + (size_t)nk * cap + (np == 0 ? 0 : (np == 1 ? o_mrp : o_cup)));
+        pf_cur = pf_ptr[0];
+        pf_nx1 = pf_ptr[1];  // (inside the slot: a pass is padded, a plane's slot has 128 bytes to spare)
+        pf_pass = np;
+        pf_k = nk;
+        pf_cnt = nc;
+        pf_valid = 1;
+    };
+#endif
     if (b >= 0) {
         const BlockDesc d = a.blocks[b];
         Pt = a.P[b];
@@ -970,12 +998,28 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         ndec = left;
         cur = ptr[0];
         if (left > 16) nx1 = ptr[1];
+#if JP2HIP_MQ_PASS_PREFETCH
+        prefetch();
+#endif
     }
     uint64_t cyc_wait = 0;  // debug census: shader cycles spent at the chunk barrier
     const uint64_t cyc0 = __builtin_readcyclecounter();
     for (int it = 0;; it++) {
         // close finished passes (empty passes close at once)
         while (left <= 0 && s < nseg) {
+#if JP2HIP_MQ_PASS_PREFETCH
+            // (the pass's distortion record is written after the block)
+            if (++s >= nseg) break;
+            pass = pf_pass;
+            k = pf_k;
+            cnt = pf_cnt;
+            ptr = pf_ptr;
+            cur = pf_cur;
+            nx1 = pf_nx1;  // (whatever it holds when the pass has <= 16 decisions: never coded)
+            left = pass == 0 ? (int)cnt.x : (pass == 1 ? (int)cnt.y : (int)cnt.z);
+            ndec += left;
+            prefetch();
+#else
             const int p = Pt - 1 - k;
             D[s] = pass == 0 ? dspp[k] : (pass == 1 ? dref[p] : dsig[p] - dspp[k]);
             if (++s >= nseg) break;
@@ -991,6 +1035,7 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
             ndec += left;
             cur = ptr[0];
             nx1 = left > 16 ? ptr[1] : pad4;
+#endif
         }
         const bool active = s < nseg;
         const int buf = it & 1;
@@ -1043,6 +1088,14 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
 #endif
         if (a.dbg) cyc_wait += __builtin_readcyclecounter() - c1;
     }
+#if JP2HIP_MQ_PASS_PREFETCH
+    // the passes' distortion records (segment s: s = 0 the top plane's
+    // cleanup, else pass (s+2)%3 of plane (s+2)/3 from the top)
+    for (int q = 0; q < nseg; q++) {
+        const int kq = q == 0 ? 0 : (q + 2) / 3, pq = q == 0 ? 2 : (q + 2) % 3, p = Pt - 1 - kq;
+        D[q] = pq == 0 ? dspp[kq] : (pq == 1 ? dref[p] : dsig[p] - dspp[kq]);
+    }
+#endif
 #if JP2HIP_MQ_EXP >= 2
     if (b >= 0) {  // no coder ran: the block codes as empty downstream
         a.npasses[b] = 0;
