@@ -256,12 +256,18 @@ __device__ __forceinline__ QLevel qlevel(const QuantTab &qt, int lv) {
     }
     return l;
 }
-// even rows: LL (final at the last level) + HL; odd rows: LH + HH
+// even rows: LL (final at the last level) + HL; odd rows: LH + HH.
+// (Selects of register values: as selects of the struct's fields the
+// compiler made the struct a scratch slot and each select a scratch load
+// from a selected address, per staged row.)
 __device__ __forceinline__ void qrow_bands(QRow &o, const QLevel &l, bool yodd) {
-    o.inv_lo = yodd ? l.inv[2] : l.inv[0];
-    o.lim_lo = yodd ? l.lim[2] : l.lim[0];
-    o.inv_hi = yodd ? l.inv[3] : l.inv[1];
-    o.lim_hi = yodd ? l.lim[3] : l.lim[1];
+    float i0 = l.inv[0], i1 = l.inv[1], i2 = l.inv[2], i3 = l.inv[3];
+    uint32_t m0 = l.lim[0], m1 = l.lim[1], m2 = l.lim[2], m3 = l.lim[3];
+    asm("" : "+v"(i0), "+v"(i1), "+v"(i2), "+v"(i3), "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3));
+    o.inv_lo = yodd ? i2 : i0;
+    o.lim_lo = yodd ? m2 : m0;
+    o.inv_hi = yodd ? i3 : i1;
+    o.lim_hi = yodd ? m3 : m1;
 }
 // the coefficient-plane row `row` of tile-component tc
 __device__ __forceinline__ uint8_t *qplane_row(void *dst, size_t plane, int tc, size_t row, int plane_w, bool q16) {

@@ -968,6 +968,11 @@ __device__ __forceinline__ void mq_modeller(const T1MqArgs &a, MqShared &sh) {
         pf_valid = 0;
         if (s + 1 >= nseg) return;
         const int np = pass == 2 ? 0 : pass + 1, nk = pass == 2 ? k + 1 : k;
+        // (compiled as a flat load from a selected address -- `cnt` gets a
+        // 16-byte scratch slot -- which leaves the next chunks' stream loads
+        // in flight at the chunk start; a global load of plane nk's counts,
+        // selected or not, made that wait vmcnt(0): census 221 -> 243-255
+        // cycles per decision, profiles/r05/mq/ab_pass_counts.txt)
         const uint4 nc = np == 0 ? cntp[nk] : cnt;
         const int o_mrp = ((int)cnt.x + 15) & ~15;
         const int o_cup = (o_mrp + (int)cnt.y + 15) & ~15;
