@@ -6,6 +6,8 @@ import java.net.URLEncoder;
 import java.nio.charset.StandardCharsets;
 import java.util.concurrent.ArrayBlockingQueue;
 import java.util.concurrent.BlockingQueue;
+import java.util.concurrent.TimeUnit;
+import java.util.concurrent.atomic.AtomicBoolean;
 
 import info.freelibrary.util.Logger;
 import info.freelibrary.util.LoggerFactory;
@@ -41,7 +43,14 @@ public class GpuConverter extends AbstractConverter implements Converter, AutoCl
     /** non-null: why this converter cannot encode; every convert() throws IOException */
     private final String myUnavailable;
 
-    private boolean myClosed;
+    /** set once by close(); read without a lock by every convert() and by waiting borrowers */
+    private final AtomicBoolean myClosed = new AtomicBoolean();
+
+    /** serialises split encodes with each other (and with close()), never with pooled conversions */
+    private final Object mySplitLock = new Object();
+
+    /** how often a borrower waiting for a context re-checks myClosed */
+    private static final long BORROW_POLL_MS = 100;
 
     /**
      * Package-private, like KakaduConverter's (KakaduConverter.java:48). The native side either creates every
@@ -95,9 +104,12 @@ public class GpuConverter extends AbstractConverter implements Converter, AutoCl
         final byte[] out = jpx.getAbsolutePath().getBytes(StandardCharsets.UTF_8);
         final String error;
         final long split = myHandles[0];
+        if (myClosed.get()) {
+            throw new IOException("Failed to convert TIFF to JP2: " + aID + ": converter closed");
+        }
         if (split != 0 && nativeTiffPixels(tiff) >= mySplitMinPixels) {
-            synchronized (this) { // one oversized image at a time holds every GPU
-                if (myClosed) {
+            synchronized (mySplitLock) { // one oversized image at a time holds every GPU
+                if (myClosed.get()) {
                     throw new IOException("Failed to convert TIFF to JP2: " + aID + ": converter closed");
                 }
                 error = nativeEncodeFile(split, tiff, out, aConversion.ordinal());
@@ -116,13 +128,23 @@ public class GpuConverter extends AbstractConverter implements Converter, AutoCl
         return jpx;
     }
 
+    /**
+     * A pooled context, or IOException once close() has begun: a waiter re-checks myClosed every
+     * BORROW_POLL_MS, so it never blocks on a pool that close() is draining.
+     */
     private long borrow(final String aID) throws IOException, InterruptedException {
-        synchronized (this) {
-            if (myClosed) {
+        while (true) {
+            final Long ctx = myContexts.poll(BORROW_POLL_MS, TimeUnit.MILLISECONDS);
+            if (myClosed.get()) {
+                if (ctx != null) {
+                    myContexts.put(ctx); // close() is counting them back
+                }
                 throw new IOException("Failed to convert TIFF to JP2: " + aID + ": converter closed");
             }
+            if (ctx != null) {
+                return ctx;
+            }
         }
-        return myContexts.take();
     }
 
     /**
@@ -131,15 +153,13 @@ public class GpuConverter extends AbstractConverter implements Converter, AutoCl
      */
     @Override
     public void close() throws InterruptedException {
-        synchronized (this) {
-            if (myClosed || myHandles.length == 0) {
-                myClosed = true;
-                return;
-            }
-            myClosed = true;
-            for (int index = 1; index < myHandles.length; index++) {
-                myContexts.take(); // waits for conversions that hold one
-            }
+        if (!myClosed.compareAndSet(false, true) || myHandles.length == 0) {
+            return;
+        }
+        for (int index = 1; index < myHandles.length; index++) {
+            myContexts.take(); // waits for conversions that hold one; waiting borrowers give up
+        }
+        synchronized (mySplitLock) { // a split encode in progress finishes first
             nativeClose(myHandles);
         }
     }

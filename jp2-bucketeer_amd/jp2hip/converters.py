@@ -121,6 +121,7 @@ class GpuConverter(Converter):
         self._pool, self._free = [], []
         self._cv = threading.Condition()
         self._split, self._split_lock, self.split_world = None, threading.Lock(), 1
+        self._closed = False
         self.unavailable = None  # reason every convert() fails with (GPU absent / init failed)
         try:
             self.tmp_dir.mkdir(parents=True, exist_ok=True)
@@ -161,19 +162,24 @@ class GpuConverter(Converter):
         c.tmp_dir = Path(tempfile.gettempdir()) / cls.WORKING_DIR_NAME
         c._pool, c._free, c._cv = [], [], threading.Condition()
         c._split, c._split_lock, c.split_world = None, threading.Lock(), 1
+        c._closed = False
         c.unavailable = reason
         return c
 
-    def _acquire(self):
+    def _acquire(self, image_id):
+        # waiters see close() at once (a borrower must get the
+        # IOError, not block on a pool that close() is draining)
         with self._cv:
-            while not self._free:
+            while not self._free and not self._closed:
                 self._cv.wait()
+            if self._closed:
+                raise IOError(BUCKETEER_001.format(image_id) + ": converter closed")
             return self._free.pop()
 
     def _release(self, enc):
         with self._cv:
             self._free.append(enc)
-            self._cv.notify()
+            self._cv.notify_all()
 
     def convert(self, image_id, tiff, conversion):
         if self.unavailable is not None:
@@ -182,13 +188,20 @@ class GpuConverter(Converter):
         jpx = self.tmp_dir / _jpx_name(image_id)
         if not os.access(jpx.parent, os.W_OK):
             raise IOError(BUCKETEER_002.format(jpx))
+        if self._closed:
+            raise IOError(BUCKETEER_001.format(image_id) + ": converter closed")
         try:
             big = self._split is not None and _lib.tiff_pixels(str(tiff.absolute())) >= self.split_min_pixels
             if big:
+                # split encodes take turns with each other only: the pool's
+                # condition (_cv) is never held across an encode, so pooled
+                # conversions go on while an oversized image holds every GPU
                 with self._split_lock:
+                    if self._closed or self._split is None:
+                        raise IOError(BUCKETEER_001.format(image_id) + ": converter closed")
                     self._split.encode_file(str(tiff.absolute()), str(jpx), int(Conversion(conversion)))
                 return jpx
-            enc = self._acquire()
+            enc = self._acquire(image_id)
             try:
                 enc.encode_file(str(tiff.absolute()), str(jpx), int(Conversion(conversion)))
             finally:
@@ -198,11 +211,21 @@ class GpuConverter(Converter):
         return jpx
 
     def close(self):
-        for e in self._pool:
+        """Later conversions (and borrowers still waiting) fail with IOError;
+        conversions in progress finish first, then every context is released
+        (GpuConverter.java close())."""
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+            while len(self._free) < len(self._pool):
+                self._cv.wait()
+            pool, self._pool, self._free = self._pool, [], []
+        for e in pool:
             e.close()
-        if self._split is not None:
-            self._split.close()
-            self._split = None
+        with self._split_lock:
+            if self._split is not None:
+                self._split.close()
+                self._split = None
 
 
 class ConverterFactory:
@@ -211,21 +234,19 @@ class ConverterFactory:
     _converter: Converter | None = None
     _has_kakadu = False
     _lock = threading.Lock()
+    _closing: list[threading.Thread] = []
 
     @classmethod
     def get_converter(cls, klass: type | None = None) -> Converter:
         with cls._lock:
             if klass is None:
+                # exactly the reference's rule (ConverterFactory.java:37-47):
+                # Kakadu if present, else OpenJPEG. The GPU is chosen only by
+                # name (get_converter(GpuConverter), the bucketeer.converter
+                # key), so KakaduConverterTest.java:99's cast still holds on a
+                # host with Kakadu and a gfx950 device.
                 if cls._converter is None:
-                    gpu = None
-                    if cls.check_system_gpu():
-                        try:
-                            gpu = GpuConverter()
-                        except IOError:
-                            gpu = None
-                    if gpu is not None:
-                        cls._converter = gpu
-                    elif cls.check_system_kakadu():
+                    if cls.check_system_kakadu():
                         cls._converter = KakaduConverter()
                     else:
                         cls._converter = OpenJPEGConverter()
@@ -233,9 +254,9 @@ class ConverterFactory:
             if klass is KakaduConverter:
                 if not cls.check_system_kakadu():
                     raise KakaduNotFoundError("Kakadu not found")
-                cls._converter = KakaduConverter()
+                cls._replace(KakaduConverter())
             elif klass is OpenJPEGConverter:
-                cls._converter = OpenJPEGConverter()
+                cls._replace(OpenJPEGConverter())
             elif klass is GpuConverter:
                 # never raises: GPU if usable, else Kakadu if present, else a
                 # converter whose convert() raises IOError (the caller's
@@ -251,10 +272,22 @@ class ConverterFactory:
                     if conv is None:
                         conv = KakaduConverter() if cls.check_system_kakadu() else \
                             GpuConverter.unavailable_converter(reason)
-                    cls._converter = conv
+                    cls._replace(conv)
             else:
                 raise ValueError(BUCKETEER_032)
             return cls._converter
+
+    @classmethod
+    def _replace(cls, conv: Converter):
+        """Install ``conv`` as the singleton; a GpuConverter it displaces is
+        closed on a thread of its own (close() waits for the conversions in
+        progress, which must not hold the factory lock), so its contexts are
+        released instead of leaked."""
+        old, cls._converter = cls._converter, conv
+        if isinstance(old, GpuConverter) and old is not conv:
+            t = threading.Thread(target=old.close, name="GpuConverter-close", daemon=True)
+            t.start()
+            cls._closing.append(t)
 
     @classmethod
     def has_system_kakadu(cls) -> bool:
@@ -286,3 +319,6 @@ class ConverterFactory:
             if isinstance(cls._converter, GpuConverter):
                 cls._converter.close()
             cls._converter = None
+            closing, cls._closing = cls._closing, []
+        for t in closing:
+            t.join()
