@@ -105,10 +105,10 @@ static void t1_lane_order(Plan &P) {
 }
 
 int32_t lossless_layer_frac(int l, int NL) {
-    // 6-layer fractions, indexed by layers below the top (test.jpx fit:
-    // tests/tools/fit_layers.py); other layer counts interpolate linearly at
+    // 6-layer fractions, indexed by layers below the top (fitted to
+    // test.jpx's per-layer PSNR: tests/tools/fit_layers.py); other layer counts interpolate linearly at
     // the same relative depth, integer arithmetic as in the oracle
-    static const int64_t f6[6] = {65536, 35220, 19240, 15100, 12200, 9340};
+    static const int64_t f6[6] = {65536, 44515, 20178, 15645, 12923, 11253};
     if (l >= NL - 1) return 65536;
     const int64_t num = (int64_t)(NL - 1 - l) * 5, den = NL - 1;
     const int64_t i = num / den, r = num % den;

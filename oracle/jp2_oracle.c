@@ -37,8 +37,8 @@
  *   - lossless ("-rate -") layer budgets are fixed fractions of each
  *     -flush_period stripe's tier-1 bytes (lossless_layer_frac), so every
  *     stripe's layers are decided when its own tier-1 is done, as Kakadu's
- *     incremental flushing decides them; the fractions reproduce the layer
- *     sizes of the reference's fixture test.jpx (Kdu-Layer-Info).
+ *     incremental flushing decides them; the fractions reproduce the
+ *     per-layer PSNR of the reference's fixture test.jpx.
  */
 #include "jp2_oracle.h"
 
@@ -715,6 +715,10 @@ int oracle_t1_encode_planes(const int32_t *sm, int w, int h, int band, int lossl
             if (pass == 2) memset(t.pi, 0, fs);
             dists[np] = dd;
             rates[np] = mq_numbytes(&mq) + 3;
+            {   /* experiments: other truncation-length margins (round 6 layer-quality study) */
+                const char *te = ORACLE_EXP("ORACLE_TRUNC_EXTRA");
+                if (te) rates[np] = mq_numbytes(&mq) + atoi(te);
+            }
             if (np < 100) g_pass_dec[np] = g_decisions;  /* experiments: decisions through each pass */
             np++;
             if (mq_numbytes(&mq) + 8 > cap) {
@@ -856,6 +860,7 @@ typedef struct {
     uint32_t est[32];    /* predicted coded size of plane p, 1/16 bit */
     int64_t pd[32];      /* exact distortion decrease of plane p */
     int32_t *pdec;       /* experiments (ORACLE_PASS_WASTE): decisions per coded pass */
+    int comp;            /* component (experiments) */
 } cblk;
 
 typedef struct {
@@ -1133,6 +1138,7 @@ static int code_tilecomp(encoder *E, tileinfo *T, int c, void *buf, int tw, int 
                             if (y1 > ry1) y1 = ry1;
                             cblk *b = (cblk *)calloc(1, sizeof(cblk));
                             b->band = band;
+                            b->comp = c;
                             b->w = (int)(x1 - x0);
                             b->h = (int)(y1 - y0);
                             b->Mb = q.Mb;
@@ -1255,12 +1261,14 @@ static uint64_t select_threshold(const seg *S, int ns, int64_t budget, uint64_t 
  * stripe whose slopes clear the threshold that fits lossless_budget(T, l, NL)
  * bytes of that stripe's T tier-1 bytes; the last layer keeps every pass.
  * The fractions (1/65536 units, indexed by layers below the top) are fitted
- * to the reference fixture test.jpx (KakaduConverter.java:38-42 recipe;
- * its Kdu-Layer-Info reads L = 5.1e4, 6.9e4, 8.7e4, 1.1e5, 1.8e5, 3.0e5
- * bytes: tests/test_oracle.py checks each within 10 %).  Another layer count
- * interpolates the 6-layer curve linearly at the same relative depth, in
- * integers, so libjp2hip (plan.cpp lossless_layer_frac) computes the same. */
-static const int64_t kLosslessFrac6[6] = {65536, 35220, 19240, 15100, 12200, 9340};
+ * (tests/tools/fit_layers.py) so that the first l layers decode
+ * (opj_decompress -l l) to test.jpx's own RGB PSNR at layer l: 35.01 / 36.62 /
+ * 39.06 / 42.36 / 55.50 dB (KakaduConverter.java:38-42 recipe).  A fit, so
+ * tests/test_oracle.py's 0.3 dB check on test.jpx is a fit check; parity of
+ * layer quality is unpinned for other images and layer counts.  Another layer
+ * count interpolates the 6-layer curve linearly at the same relative depth,
+ * in integers, so libjp2hip (plan.cpp lossless_layer_frac) computes the same. */
+static const int64_t kLosslessFrac6[6] = {65536, 44515, 20178, 15645, 12923, 11253};
 
 static int64_t lossless_layer_frac(int l, int NL) {
     if (l >= NL - 1) return 65536;
@@ -1779,6 +1787,12 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
             for (int l = 0; l < NL; l++) {
                 uint64_t Kc = 0;
                 uint64_t K = (l == NL - 1) ? 0 : select_threshold(S, nss, lossless_budget(stotal, l, NL), &Kc);
+                {   /* experiments: fixed normalised slope thresholds instead of budgets */
+                    const char *ls = ORACLE_EXP("ORACLE_LOSSLESS_SLOPES");
+                    double q[5];
+                    if (ls && l < 5 && sscanf(ls, "%lf,%lf,%lf,%lf,%lf", &q[0], &q[1], &q[2], &q[3], &q[4]) == 5)
+                        K = Kc = slope_key(ldexp(pow(2.0, q[l]), 2 * E.bits));
+                }
                 if (Kc > E.K[l]) E.K[l] = Kc;  /* Kdu-Layer-Info: the strictest stripe's */
                 for (int i = b0; i < b1; i++) {
                     cblk *b = E.all[i];
@@ -1810,6 +1824,20 @@ int oracle_encode(const void *pix, int w, int h, int nc, int bits, const oracle_
         }
     }
     free(S);
+    if (ORACLE_EXP("ORACLE_LAYER_DIST")) {  /* experiments: predicted distortion left after each layer */
+        FILE *f = fopen(ORACLE_EXP("ORACLE_LAYER_DIST"), "a");
+        for (int l = 0; f && l < NL; l++) {
+            double left[4] = {0, 0, 0, 0};
+            for (int i = 0; i < E.nall; i++) {
+                cblk *b = E.all[i];
+                double d = 0.0;
+                for (int q = b->nl[l]; q < b->npasses; q++) d += (double)b->dd[q];
+                left[b->comp] += d * b->weight;
+            }
+            fprintf(f, "%d %.6g %.6g %.6g %.6g\n", l, left[0], left[1], left[2], left[3]);
+        }
+        if (f) fclose(f);
+    }
     if (ORACLE_EXP("ORACLE_PASS_WASTE")) {  /* experiments: coded decisions PCRD discards, by pass */
         FILE *f = fopen(ORACLE_EXP("ORACLE_PASS_WASTE"), "a");
         int64_t all = 0, kept = 0, lost[3] = {0, 0, 0}, lost_last[3] = {0, 0, 0}, lost_plane = 0;

@@ -222,9 +222,11 @@ def tiff_bytes(img: np.ndarray, rows_per_strip=64, planar=False, big_endian=Fals
     return hdr + ifd + bytes(extra) + b"".join(strips)
 
 
-def decode_opj(data: bytes, ext=".jpx", area=None) -> np.ndarray:
+def decode_opj(data: bytes, ext=".jpx", area=None, layers=None, reduce=None) -> np.ndarray:
     """Decode with opj_decompress (exact for 16-bit RGB, unlike Pillow);
-    area = (x0, y0, x1, y1) decodes only that window (-d)."""
+    area = (x0, y0, x1, y1) decodes only that window (-d); layers = the
+    first n quality layers only (-l); reduce = drop the r highest
+    resolutions (-r), the views a IIIF image server serves."""
     tool = opj("opj_decompress")
     if tool is None:
         raise RuntimeError("opj_decompress not available")
@@ -236,6 +238,10 @@ def decode_opj(data: bytes, ext=".jpx", area=None) -> np.ndarray:
         cmd = [tool, "-i", src, "-o", dst]
         if area is not None:
             cmd += ["-d", ",".join(str(int(v)) for v in area)]
+        if layers is not None:
+            cmd += ["-l", str(int(layers))]
+        if reduce is not None:
+            cmd += ["-r", str(int(reduce))]
         r = subprocess.run(cmd, capture_output=True)
         if r.returncode != 0:
             raise RuntimeError(r.stderr.decode() + r.stdout.decode())
@@ -576,3 +582,27 @@ def crafted_match_tokens(seed=7):
                 toks.append((L, d))
                 n += L
     return toks
+
+
+def packet_bytes_by_layer(cs: bytes, layers: int, tiles=None) -> list:
+    """Bytes of the packets of each quality layer (SOP through the packet
+    body) in a raw code-stream written with SOP markers and a
+    layer-innermost progression (RPCL / LRCP-free recipes: Nsop mod layers
+    is the layer), summed over ``tiles`` (all when None). This is what a
+    decoder reading the first l layers receives, unlike Kakadu's
+    Kdu-Layer-Info L column, which projects its first flush."""
+    out = [0] * layers
+    p = cs.find(b"\xff\x90")
+    while p >= 0 and cs[p:p + 2] == b"\xff\x90":
+        isot = struct.unpack(">H", cs[p + 4:p + 6])[0]
+        end = p + struct.unpack(">I", cs[p + 6:p + 10])[0]
+        if tiles is None or isot in tiles:
+            body = cs[cs.find(b"\xff\x93", p) + 2:end]
+            sops, j = [], body.find(b"\xff\x91")
+            while j >= 0:
+                sops.append(j)
+                j = body.find(b"\xff\x91", j + 6)
+            for a, b in zip(sops, sops[1:] + [len(body)]):
+                out[struct.unpack(">H", body[a + 4:a + 6])[0] % layers] += b - a
+        p = end
+    return out

@@ -74,7 +74,7 @@ def test_codestream_identical_to_oracle(encoder, case):
         assert np.array_equal(im.decode_opj(got), img)
 
 
-def test_testjpx_pixels_lossless(encoder, testjpx_pixels, golden):
+def test_testjpx_pixels_lossless(encoder, testjpx_pixels, testjpx_bytes, golden):
     """C1: the reference fixture's pixels through the GPU converter path."""
     rc = jp2hip.recipe(jp2hip.LOSSLESS, format=jp2hip.FORMAT_J2K)
     got, st = encoder.encode_tiff(im.tiff_bytes(testjpx_pixels), jp2hip.LOSSLESS, rc)
@@ -88,11 +88,11 @@ def test_testjpx_pixels_lossless(encoder, testjpx_pixels, golden):
     assert [[t[0], t[2], t[3]] for t in im.tile_parts(got)] == g["tp_order"]
     assert np.array_equal(im.decode_pillow(got), testjpx_pixels)
     assert len(got) > g["min_size_assert"]
-    # Kakadu's quality layers: each layer's bytes
-    # within 10 % of test.jpx's Kdu-Layer-Info
-    from test_oracle import kdu_layer_bytes
-    for got_l, ref_l in zip(kdu_layer_bytes(got), [b for _, b in g["kdu_layer_info"]]):
-        assert abs(got_l - ref_l) / ref_l < 0.10
+    # the views a IIIF server reads: every reduced
+    # resolution equals test.jpx's decode bit for bit, every quality layer
+    # within 0.3 dB of test.jpx's PSNR (test_oracle.check_testjpx_views)
+    from test_oracle import check_testjpx_views
+    check_testjpx_views(got, testjpx_bytes, testjpx_pixels)
 
 
 def _golden_lossy_names():
