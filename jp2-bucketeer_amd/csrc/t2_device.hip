@@ -30,6 +30,7 @@
 
 #include "device_common.h"
 #include "gpu_encoder.h"
+#include "host_wait.h"
 
 namespace jp2hip {
 
@@ -1007,6 +1008,31 @@ __global__ void __launch_bounds__(64) k_release_dma(int64_t *dep) {
         }                                                                              \
     } while (0)
 
+// HSA signal waits take their timeout in system-timestamp ticks
+static uint64_t hsa_ticks(uint64_t ns) {
+    static const uint64_t freq = [] {
+        uint64_t f = 0;
+        if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) != HSA_STATUS_SUCCESS || !f) f = 1000000000ull;
+        return f;
+    }();
+    return (uint64_t)((double)ns * (double)freq / 1e9) + 1;
+}
+
+static uint64_t mono_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// one slice of a wait for `sig` to drop below 1 (the copy's completion)
+static jp2hip::SliceResult poll_signal(hsa_signal_t sig, uint64_t slice_ns) {
+    const hsa_signal_value_t v =
+        hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, hsa_ticks(slice_ns), HSA_WAIT_STATE_BLOCKED);
+    return v < 0 ? jp2hip::SliceResult::Error : (v < 1 ? jp2hip::SliceResult::Done : jp2hip::SliceResult::Pending);
+}
+
+static constexpr uint64_t kWaitSliceNs = 50ull * 1000 * 1000;          // 50 ms
+static constexpr uint64_t kDrainedGraceNs = 20ull * 1000 * 1000 * 1000;  // 20 s
+
 static hsa_status_t first_cpu_agent(hsa_agent_t a, void *out) {
     hsa_device_type_t t;
     if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
@@ -1052,7 +1078,12 @@ static int pick_dma_engine(hsa_agent_t gpu, hsa_agent_t cpu, hsa_signal_t sig) {
                     if (hsa_amd_memory_async_copy_on_engine(h, cpu, d, gpu, n, 0, nullptr, sig,
                                                             (hsa_amd_sdma_engine_id_t)(1u << e), true) != HSA_STATUS_SUCCESS)
                         break;
-                    if (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) < 0)
+                    // nothing else is queued: a probe copy that takes more
+                    // than a second is an engine to leave out
+                    std::string perr;
+                    if (!jp2hip::wait_bounded([&](uint64_t ns) { return poll_signal(sig, ns); },
+                                              [](std::string &) { return jp2hip::StreamState::Drained; }, mono_ns,
+                                              kWaitSliceNs, 1000ull * 1000 * 1000, "DMA engine probe", perr))
                         break;
                     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                     best = std::max(best, n / s);
@@ -1122,11 +1153,29 @@ bool GpuEncoder::dma_to_host(uint8_t *host_dst, const void *src, size_t bytes, s
         return false;
     }
     waits++;
-    if (hsa_signal_wait_scacquire(dma_done, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) < 0) {
-        err = "code-stream copy failed (DMA engine reported an error)";
-        return false;
+    // in slices, never unbounded: the copy waits for k_release_dma, which
+    // never runs if an earlier launch on the stream failed (host_wait.h)
+    hipStream_t st = stream;
+    const bool ok = jp2hip::wait_bounded(
+        [&](uint64_t ns) { return poll_signal(dma_done, ns); },
+        [st](std::string &why) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return jp2hip::StreamState::Drained;
+            if (q == hipErrorNotReady) return jp2hip::StreamState::Running;
+            why = hipGetErrorString(q);
+            return jp2hip::StreamState::Failed;
+        },
+        mono_ns, kWaitSliceNs, kDrainedGraceNs, "code-stream copy", err);
+    if (!ok) {
+        // the copy may still be queued behind its gate, holding both
+        // signals: leave them to it (a failure path; a few bytes) and give
+        // the next encode fresh ones, so a late release cannot complete a
+        // wait that belongs to another copy
+        dma_dep.handle = 0;
+        dma_done.handle = 0;
+        dma_ok = false;
     }
-    return true;
+    return ok;
 }
 template <typename T>
 static bool ensure_t2(DevBuf &b, size_t count, std::string &err) {
