@@ -566,8 +566,9 @@ def run_c4(args):
     prescribes for the 10k-row batch), lossless (ImageWorker hard-codes it),
     through one GPU's native batch queue per rank: TIFF read -> encode -> JPX
     write -> stub upload (reads every byte) -> delete.  The timed span runs from
-    the first submit to the last upload, file I/O included; rows are sharded
-    round-robin over ranks (no collective)."""
+    the first submit to the last upload, file I/O included; rows are pulled
+    by the ranks from one shared claim counter (work stealing through the
+    process group's store; no collective on the data path)."""
     import csv as _csv
     import shutil
 
@@ -601,7 +602,14 @@ def run_c4(args):
             wr.writerow(["Item ARK", "File Name"])
             for i in range(rows * world):
                 wr.writerow([f"ark:/99999/synth{i:05d}", os.path.basename(paths[i % ndistinct])])
-        items = jb.shard(jb.read_batch_csv(csv_path, path_prefix=work), rank, world)
+        items = jb.read_batch_csv(csv_path, path_prefix=work)
+        # rows go to the ranks by work stealing: each rank's queue pulls the
+        # next unclaimed row from the process group's store (an atomic add;
+        # no data-path collective), so a faster GPU takes more rows
+        claims = None
+        if world > 1:
+            from torch.distributed import distributed_c10d as c10d
+            claims = jb.StoreClaims(c10d._get_default_store(), len(items), key="jp2hip/c4/next")
         out_dir = os.path.join(work, "out")
         os.makedirs(out_dir, exist_ok=True)
         with jb.BatchQueue(device=local) as q:
@@ -613,9 +621,7 @@ def run_c4(args):
             if world > 1:
                 dist.barrier()
             t0 = time.perf_counter()
-            for it in items:
-                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)))
-            res = q.drain()
+            res = jb.run_batch_dynamic(items, out_dir, [q], claims=claims, depth=32)
             dt = time.perf_counter() - t0
         ok = sum(1 for r in res if r["status"] == 0)
         mp = 5000 * 7000 / 1e6 * ok
@@ -635,7 +641,7 @@ def run_c4(args):
                         "disk, evicted from the page cache before the timed region",
                 "config": {"workload": "C4: Bucketeer batch CSV -> per-GPU native queue (read, lossless 5/3 encode, "
                                        "JPX write, stub upload, delete-after-upload), Kakadu recipe",
-                           "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"shards x{world}",
+                           "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"work stealing x{world}",
                            "ranks_in_process_group": world}}
     finally:
         shutil.rmtree(work, ignore_errors=True)

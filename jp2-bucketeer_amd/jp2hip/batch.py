@@ -14,14 +14,22 @@ src/main/java/edu/ucla/library/bucketeer/):
 
 The queue itself is native (libjp2hip ``jp2hip_batch_*``, csrc/batch.cpp):
 reader threads, one encoder thread per GPU context, uploader threads.  Images
-are independent, so N GPUs run N queues in N processes, each taking the rows
-``i % world == rank`` (``shard``); no collective touches the data.
+are independent, so no collective touches the data.  Rows reach the GPUs by
+work stealing: every GPU's queue pulls the next unclaimed
+row whenever it holds fewer than ``depth`` images, from one shared claim
+counter -- ``LocalClaims`` for N queues in one process, ``StoreClaims``
+(the torch.distributed store's atomic ``add``) for one queue per process --
+so a GPU that drew small images takes more of them and none sits idle while
+rows remain (``run_batch_dynamic``).  ``shard`` (static round-robin) stays
+for callers that want a fixed partition.
 """
 from __future__ import annotations
 
 import csv
 import ctypes
 import os
+import threading
+import time
 import urllib.parse
 from ctypes import CFUNCTYPE, POINTER, Structure, byref, c_char, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 from dataclasses import dataclass
@@ -111,6 +119,85 @@ def read_batch_csv(path: os.PathLike | str, path_prefix: str = "") -> list[Batch
 def shard(items: list, rank: int, world: int) -> list:
     """Static round-robin share of one GPU process (images are independent)."""
     return items[rank::world]
+
+
+class LocalClaims:
+    """Claims on rows 0..n-1 shared by the queues of one process."""
+
+    def __init__(self, n: int):
+        self._n, self._next, self._mu = n, 0, threading.Lock()
+
+    def next(self) -> int | None:
+        with self._mu:
+            if self._next >= self._n:
+                return None
+            i = self._next
+            self._next += 1
+            return i
+
+
+class StoreClaims:
+    """Claims on rows 0..n-1 shared by every rank of a job, through a
+    torch.distributed store (TCPStore / FileStore / HashStore): ``add`` is
+    atomic on the store's server, so each row goes to exactly one rank. Only
+    the row index crosses processes -- control plane, not data path."""
+
+    def __init__(self, store, n: int, key: str = "jp2hip/batch/next"):
+        self._store, self._n, self._key = store, n, key
+
+    def next(self) -> int | None:
+        i = int(self._store.add(self._key, 1)) - 1
+        return i if i < self._n else None
+
+
+def run_batch_dynamic(items: list[BatchItem], out_dir: os.PathLike | str, queues: list, claims=None,
+                      depth: int = 16, conversion: int = _lib.LOSSLESS, poll_ms: int = 20,
+                      trace: list | None = None) -> list[dict]:
+    """Work stealing over ``queues`` (BatchQueue-like: submit / pending /
+    wait): one feeder thread per queue tops its queue up to ``depth``
+    images with the next unclaimed row and collects its results, so rows go
+    to whichever GPU has room. ``claims`` defaults to LocalClaims over
+    ``items``; pass StoreClaims to share rows with other processes.
+    ``trace`` (a list) receives (t, queue, "submit" | "done", job) events.
+    Returns every result, in completion order."""
+    out_dir = Path(out_dir)
+    out_dir.mkdir(parents=True, exist_ok=True)
+    claims = claims or LocalClaims(len(items))
+    results, mu, errors = [], threading.Lock(), []
+    t0 = time.perf_counter()
+
+    def feed(qi, q):
+        try:
+            exhausted = False
+            while True:
+                while not exhausted and q.pending() < depth:
+                    i = claims.next()
+                    if i is None:
+                        exhausted = True
+                        break
+                    it = items[i]
+                    q.submit(it.job, it.image_id, it.tiff, out_dir / jpx_name(it.image_id), conversion)
+                    if trace is not None:
+                        with mu:
+                            trace.append((time.perf_counter() - t0, qi, "submit", it.job))
+                if exhausted and q.pending() == 0:
+                    return
+                got = q.wait(timeout_ms=poll_ms)
+                with mu:
+                    results.extend(got)
+                    if trace is not None:
+                        trace.extend((time.perf_counter() - t0, qi, "done", r["job"]) for r in got)
+        except Exception as e:  # surfaced below, after every feeder stopped
+            errors.append(e)
+
+    threads = [threading.Thread(target=feed, args=(k, q), name=f"jp2hip-feed-{k}") for k, q in enumerate(queues)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return results
 
 
 def jpx_name(image_id: str) -> str:

@@ -160,3 +160,38 @@ def test_batch_c4_full_size_image_identical_to_oracle(tmp_path, golden):
     assert len(data) == g["oracle_bytes"]
     assert hashlib.sha256(data).hexdigest() == g["oracle_sha256"]
     assert not (tmp_path / "c4.jpx").exists()
+
+
+@pytest.mark.gpu
+def test_batch_work_stealing_two_queues_on_the_gpu(tmp_path):
+    """run_batch_dynamic over two native queues (one process, the pull model
+    an N-GPU host uses; here both on device 0): mixed sizes, every row
+    converted once, every file the oracle's, both queues used."""
+    import oracle_lib as ol
+    src = tmp_path / "src"
+    src.mkdir()
+    imgs, rows = {}, []
+    for i in range(10):
+        big = i % 4 == 0
+        img = im.synth_rgb8(1100 if big else 200 + 13 * i, 900 if big else 260 - 7 * i, seed=300 + i)
+        (src / f"m{i}.tif").write_bytes(im.tiff_bytes(img))
+        imgs[f"ark:/21198/m{i}"] = img
+        rows.append((f"ark:/21198/m{i}", f"m{i}", f"m{i}.tif"))
+    _write_csv(tmp_path / "job.csv", rows)
+    items = jb.read_batch_csv(tmp_path / "job.csv", path_prefix=str(src))
+    uploaded, mu = {}, __import__("threading").Lock()
+
+    def upload(image_id, path):
+        with open(path, "rb") as f, mu:
+            uploaded[image_id] = f.read()
+        return True
+
+    trace = []
+    with jb.BatchQueue(contexts=2, reader_threads=1, uploader_threads=1, upload=upload) as q0, \
+            jb.BatchQueue(contexts=2, reader_threads=1, uploader_threads=1, upload=upload) as q1:
+        res = jb.run_batch_dynamic(items, tmp_path / "out", [q0, q1], depth=2, trace=trace)
+    assert sorted(r["job"] for r in res) == [it.job for it in items]
+    assert all(r["status"] == jb.OK for r in res), [r["message"] for r in res]
+    assert {q for _, q, ev, _ in trace if ev == "submit"} == {0, 1}
+    for iid, img in imgs.items():
+        assert uploaded[iid] == ol.encode(img, ol.recipe(True)), iid
