@@ -160,6 +160,25 @@ void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion);
 int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg);
 void jp2hip_destroy(jp2hip_ctx *ctx);
 
+/* Device memory (bytes) held by a context's buffers, its tile-split members'
+ * included.  Buffers grow to what the largest recent image needed. */
+int64_t jp2hip_device_bytes(jp2hip_ctx *ctx);
+
+/* A context's device-memory policy, its tile-split members' too.
+ * soft: bytes it may keep between encodes; an encode that leaves it above
+ *   releases every buffer at its end, so one outsized master does not pin
+ *   HBM for the context's life (<= 0: 80 % of the device's memory divided by
+ *   the contexts alive in the process).
+ * hard: bytes no encode may pass; an image that needs more fails with
+ *   rc < 0 and a message (never a fault), and the context stays usable
+ *   (<= 0: no limit but the device's).
+ * Returns 0, or < 0 for a null context. */
+int jp2hip_set_memory_limits(jp2hip_ctx *ctx, int64_t soft, int64_t hard);
+
+/* Free and total memory of HIP device `device` (bytes): what a converter
+ * sizes its context pool from.  Returns 0 or < 0. */
+int jp2hip_device_memory(int device, int64_t *free_bytes, int64_t *total_bytes);
+
 /* Converter.convert(): TIFF file -> JPEG 2000 file, written atomically
  * (temp file + rename; nothing is left behind on failure).
  * recipe == NULL -> jp2hip_recipe_init(conversion).  Returns 0 or < 0. */

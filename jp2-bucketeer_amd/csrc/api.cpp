@@ -60,6 +60,9 @@ struct jp2hip_ctx {
     // (ranks 1..), owned here
     std::vector<jp2hip_ctx *> peers;
     int64_t split_min_pixels = 0;
+    // device memory policy (jp2hip_set_memory_limits): 0 = default
+    int64_t mem_soft = 0;
+    size_t dev_total = 0;  // the device's memory (hipMemGetInfo at create)
     ~jp2hip_ctx() {
         for (jp2hip_ctx *p : peers) jp2hip_destroy(p);
     }
@@ -73,6 +76,30 @@ int fail(const std::string &msg) {
     g_err = msg;
     return -1;
 }
+
+// Device-memory policy of a context (jp2hip_set_memory_limits): the soft
+// limit it may keep between encodes -- by default 80 % of the device's memory
+// shared by the contexts alive in the process -- and the hard limit no
+// encode may pass (default: none beyond the device's own).
+size_t soft_limit_of(jp2hip_ctx *ctx);
+
+// Every encode ends here, success or not: a failed one drains the stream
+// first (no buffer is released while a kernel may still read it), then a
+// context left above its soft limit by an outsized image releases its
+// buffers, so one C5-class master does not pin tens of GB for the rest of
+// the context's life.
+struct EncodeEnd {
+    jp2hip_ctx *ctx;
+    bool ok = false;
+    ~EncodeEnd() {
+        if (!ok) ctx->gpu.quiesce();
+        const size_t soft = soft_limit_of(ctx);
+        if (ctx->gpu.device_bytes() > soft) {
+            ctx->gpu.quiesce();
+            ctx->gpu.trim(soft);
+        }
+    }
+};
 
 // Encoded files are returned in pinned host memory: the final code-stream D2H
 // lands in the caller's buffer directly (no staging copy; a C3 file is
@@ -544,6 +571,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     const jp2hip_recipe rc = recipe_of(recipe, conversion);
     if (!lay || !d_src) return fail("null source or layout");
     ctx->gpu.take_waits();  // count this encode's host waits (stats)
+    EncodeEnd end{ctx};
     std::string err;
     jp2hip_layout ulay;
     std::vector<uint64_t> uoffs;
@@ -638,6 +666,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     *out_len = n;
     fill_stats(stats, st, t_start, h2d_ms, (int64_t)plan.blocks.size(), sum, (int64_t)n, iters,
                ctx->gpu.take_waits());
+    end.ok = true;
     return 0;
 }
 
@@ -661,6 +690,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     const jp2hip_recipe rc = recipe_of(recipe, conversion);
     if (!lay || !d_src) return fail("null source or layout");
     ctx->gpu.take_waits();
+    EncodeEnd end{ctx};
     Plan full;
     std::string err;
     if (!build_plan(full, rc, lay->width, lay->height, lay->components, lay->bits, err)) return fail(err);
@@ -864,6 +894,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     if (file_len) *file_len = flen;
     fill_stats(stats, st, t_start, 0.0, (int64_t)sub.blocks.size(), sum, (int64_t)flen, iters,
                ctx->gpu.take_waits());
+    end.ok = true;
     return 0;
 }
 
@@ -1167,6 +1198,14 @@ void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
 // Contexts alive in this process, for jp2hip_env_check.
 static std::atomic<int> g_live_contexts{0};
 
+namespace {
+size_t soft_limit_of(jp2hip_ctx *ctx) {
+    if (ctx->mem_soft > 0) return (size_t)ctx->mem_soft;
+    const int live = std::max(1, g_live_contexts.load());
+    return (size_t)((double)ctx->dev_total * 0.8 / live);
+}
+}  // namespace
+
 const char *jp2hip_env_check(void) {
     thread_local std::string msg;
     msg.clear();
@@ -1211,8 +1250,44 @@ int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg) {
         delete c;
         return fail(err);
     }
+    size_t fr = 0, tot = 0;
+    c->dev_total = hipMemGetInfo(&fr, &tot) == hipSuccess ? tot : 0;  // (init selected the device)
     *out = c;
     g_live_contexts++;
+    return 0;
+}
+
+int64_t jp2hip_device_bytes(jp2hip_ctx *ctx) {
+    if (!ctx) return 0;
+    int64_t n;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        n = (int64_t)ctx->gpu.device_bytes();
+    }
+    for (jp2hip_ctx *p : ctx->peers) n += jp2hip_device_bytes(p);
+    return n;
+}
+
+int jp2hip_set_memory_limits(jp2hip_ctx *ctx, int64_t soft, int64_t hard) {
+    if (!ctx) return fail("null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->mem_soft = soft > 0 ? soft : 0;
+    ctx->gpu.set_limits(ctx->gpu.soft_limit(), hard > 0 ? (size_t)hard : SIZE_MAX);
+    for (jp2hip_ctx *p : ctx->peers)
+        if (jp2hip_set_memory_limits(p, soft, hard) != 0) return -1;
+    return 0;
+}
+
+int jp2hip_device_memory(int device, int64_t *free_bytes, int64_t *total_bytes) {
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (hipSetDevice(device) != hipSuccess) return fail("device ordinal " + std::to_string(device) + " not usable");
+    size_t fr = 0, tot = 0;
+    const hipError_t e = hipMemGetInfo(&fr, &tot);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return fail(std::string("hipMemGetInfo: ") + hipGetErrorString(e));
+    if (free_bytes) *free_bytes = (int64_t)fr;
+    if (total_bytes) *total_bytes = (int64_t)tot;
     return 0;
 }
 

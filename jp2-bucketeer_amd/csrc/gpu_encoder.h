@@ -5,6 +5,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <cstdint>
 #include <functional>
 #include <string>
 #include <vector>
@@ -125,12 +126,36 @@ void launch_t1_items(const T1ItemArgs &a, hipStream_t st);
 void launch_t1_mq(const T1MqArgs &a, hipStream_t st);
 uint32_t t1_plane_stream_cap(int w, int h);
 
-// Owns all device memory of a context; buffers only grow, so repeated
-// encodes of the same geometry never allocate.
+// Owns all device memory of a context; buffers only grow while the context
+// stays within its soft limit, so repeated encodes of the same geometry never
+// allocate.  Every allocation goes through ensure(), which keeps the total
+// (device_bytes) and refuses to pass the hard limit; trim() releases every
+// buffer after an image that left the context above its soft limit.
 class GpuEncoder {
   public:
     ~GpuEncoder();
     bool init(int device, std::string &err);
+
+    // device memory held by this context's buffers
+    size_t device_bytes() const { return held; }
+    // hard: no buffer may take the total past it (the encode fails with an
+    // error -- before its kernels, or between them on a stream that is then
+    // drained -- instead of faulting); soft: an encode that leaves the
+    // context above it releases every buffer at its end (trim)
+    void set_limits(size_t soft, size_t hard) {
+        mem_soft = soft;
+        mem_hard = hard;
+    }
+    size_t soft_limit() const { return mem_soft; }
+    size_t hard_limit() const { return mem_hard; }
+    // releases every device buffer if more than `soft` bytes are held (the
+    // stream must be idle: called after an encode's last wait); true if it did
+    bool trim(size_t soft);
+    // waits for the stream, ignoring its errors (failure paths: no buffer is
+    // released or reused while kernels may still read it)
+    void quiesce();
+    template <typename T>
+    bool ensure(DevBuf &b, size_t count, std::string &err);
 
     // host -> device copy of a source buffer into the internal `src` buffer
     bool upload_source(const void *host, size_t len, std::string &err);
@@ -260,6 +285,35 @@ class GpuEncoder {
     std::vector<int64_t> h_hist;
     std::vector<uint64_t> strips_host;  // strip offsets last uploaded to `strips`
     const void *strips_dev = nullptr;
+    size_t held = 0, mem_soft = SIZE_MAX, mem_hard = SIZE_MAX;
+    std::vector<DevBuf *> bufs();
 };
+
+// Grows b to at least count T's (12.5 % headroom), within the hard limit.
+template <typename T>
+bool GpuEncoder::ensure(DevBuf &b, size_t count, std::string &err) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return true;
+    const size_t alloc = bytes + bytes / 8;
+    if (held - b.bytes + alloc > mem_hard) {
+        err = "device memory limit: this image needs a " + std::to_string(alloc) + "-byte buffer, the context holds " +
+              std::to_string(held) + " of its " + std::to_string(mem_hard) + " bytes";
+        return false;
+    }
+    if (b.ptr) (void)hipFree(b.ptr);
+    held -= b.bytes;
+    b.ptr = nullptr;
+    b.bytes = 0;
+    const hipError_t e = hipMalloc(&b.ptr, alloc);
+    if (e != hipSuccess) {
+        b.ptr = nullptr;
+        err = std::string("hipMalloc(") + std::to_string(alloc) + "): " + hipGetErrorString(e);
+        return false;
+    }
+    b.bytes = alloc;
+    held += alloc;
+    return true;
+}
 
 }  // namespace jp2hip

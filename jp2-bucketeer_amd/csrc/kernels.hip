@@ -1811,24 +1811,6 @@ __global__ void __launch_bounds__(256) k_apply(ApplyArgs a) {
 #define JP2HIP_REPEAT_STAGE 0
 #endif
 #define REPEAT_IF(n) for (int rep_ = 0; rep_ < (JP2HIP_REPEAT_STAGE == (n) ? 2 : 1); rep_++)
-template <typename T>
-static bool ensure(DevBuf &b, size_t count, std::string &err) {
-    size_t bytes = count * sizeof(T);
-    if (bytes == 0) bytes = 16;
-    if (b.bytes >= bytes) return true;
-    if (b.ptr) (void)hipFree(b.ptr);
-    b.ptr = nullptr;
-    b.bytes = 0;
-    size_t alloc = bytes + bytes / 8;
-    hipError_t e = hipMalloc(&b.ptr, alloc);
-    if (e != hipSuccess) {
-        err = std::string("hipMalloc(") + std::to_string(alloc) + "): " + hipGetErrorString(e);
-        return false;
-    }
-    b.bytes = alloc;
-    return true;
-}
-
 // the largest rate-control group (its blocks set the grid's x extent)
 static int grp_max_blocks(const Plan &plan) {
     int m = 0;
@@ -1836,16 +1818,41 @@ static int grp_max_blocks(const Plan &plan) {
     return std::max(m, 1);
 }
 
+std::vector<DevBuf *> GpuEncoder::bufs() {
+    return {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
+            &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
+            &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &segcnt, &segoff, &segkey,
+            &segval, &thr, &items, &slotoff, &pcrd_hb, &pcrd_hc, &sel_ctl, &sel_key, &sel_size,
+            &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
+            &inflnk, &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
+            &t2blkdst, &t2out, &t2sum, &hdist, &rstate, &t2ticket,
+            &t1fill, &dbgsel, &grptab, &gtot};
+}
+
+bool GpuEncoder::trim(size_t soft) {
+    if (held <= soft) return false;
+    for (DevBuf *b : bufs()) {
+        if (b->ptr) (void)hipFree(b->ptr);
+        b->ptr = nullptr;
+        b->bytes = 0;
+    }
+    held = 0;
+    // the device copies of the plan's tables went with the buffers
+    front_gen = 0;
+    t2_gen = 0;
+    strips_dev = nullptr;
+    strips_host.clear();
+    dma_ok = false;  // (re-reads t2out's owner agent at the next copy)
+    return true;
+}
+
+void GpuEncoder::quiesce() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    (void)hipGetLastError();
+}
+
 GpuEncoder::~GpuEncoder() {
-    DevBuf *all[] = {&coef, &blocks, &order, &bp, &sm, &P, &dref, &dsig, &t1out, &rates, &dists,
-                     &npasses, &lengths, &weight, &nhull, &hpass, &hkey, &budget, &nl, &lrate,
-                     &dstoff, &packed, &err, &tcw, &tch, &strips, &src, &llbuf0, &llbuf1, &ordkey, &segcnt, &segoff, &segkey,
-                     &segval, &thr, &items, &slotoff, &pcrd_hb, &pcrd_hc, &sel_ctl, &sel_key, &sel_size,
-                     &stream_buf, &counts, &dspp, &dbgbuf, &est, &hist, &kcut, &pmin, &mqspan, &stage, &soff, &lzwseg, &untiled,
-                     &t2prec, &t2tp, &t2tt, &t2lblock, &t2incl, &t2pklen, &t2pkoff, &t2tplen, &t2tphdr, &t2tpoff,
-                     &t2blkdst, &t2out, &t2sum, &hdist, &rstate, &t2ticket,
-                     &t1fill, &dbgsel, &grptab, &gtot};
-    for (DevBuf *b : all)
+    for (DevBuf *b : bufs())
         if (b->ptr) (void)hipFree(b->ptr);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
     if (stg_ev) (void)hipEventDestroy(stg_ev);

@@ -1177,24 +1177,6 @@ bool GpuEncoder::dma_to_host(uint8_t *host_dst, const void *src, size_t bytes, s
     }
     return ok;
 }
-template <typename T>
-static bool ensure_t2(DevBuf &b, size_t count, std::string &err) {
-    size_t bytes = count * sizeof(T);
-    if (bytes == 0) bytes = 16;
-    if (b.bytes >= bytes) return true;
-    if (b.ptr) (void)hipFree(b.ptr);
-    b.ptr = nullptr;
-    b.bytes = 0;
-    const size_t alloc = bytes + bytes / 8;
-    const hipError_t e = hipMalloc(&b.ptr, alloc);
-    if (e != hipSuccess) {
-        err = std::string("hipMalloc(") + std::to_string(alloc) + "): " + hipGetErrorString(e);
-        return false;
-    }
-    b.bytes = alloc;
-    return true;
-}
-
 T2Args GpuEncoder::t2_args(const Plan &plan) const {
     T2Args a;
     std::memset(&a, 0, sizeof a);
@@ -1243,16 +1225,16 @@ bool GpuEncoder::t2_load(const Plan &plan, const T2Tables &T, std::string &err) 
     for (const BlockDesc &bd : plan.blocks) max_mb = std::max(max_mb, (int)bd.Mb);
     t2_wave = T.max_prec_blocks <= 64 && max_mb <= kWaveMaxMb;
     const size_t npk = (size_t)t2_nprec * L;
-    if (!ensure_t2<PrecDesc>(t2prec, T.prec.size(), err) || !ensure_t2<TpDesc>(t2tp, T.tp.size(), err) ||
-        !ensure_t2<uint32_t>(t2tt, (size_t)T.tt_nodes, err) || !ensure_t2<int8_t>(t2lblock, nb, err) ||
-        !ensure_t2<int8_t>(t2incl, nb, err) || !ensure_t2<uint32_t>(t2pklen, npk, err) ||
-        !ensure_t2<uint64_t>(t2pkoff, npk, err) || !ensure_t2<uint32_t>(t2tplen, T.tp.size(), err) ||
-        !ensure_t2<uint32_t>(t2tphdr, T.tp.size(), err) || !ensure_t2<uint64_t>(t2tpoff, T.tp.size(), err) ||
-        !ensure_t2<uint64_t>(t2blkdst, (size_t)nb * L, err) || !ensure_t2<T2Summary>(t2sum, 1, err))
+    if (!ensure<PrecDesc>(t2prec, T.prec.size(), err) || !ensure<TpDesc>(t2tp, T.tp.size(), err) ||
+        !ensure<uint32_t>(t2tt, (size_t)T.tt_nodes, err) || !ensure<int8_t>(t2lblock, nb, err) ||
+        !ensure<int8_t>(t2incl, nb, err) || !ensure<uint32_t>(t2pklen, npk, err) ||
+        !ensure<uint64_t>(t2pkoff, npk, err) || !ensure<uint32_t>(t2tplen, T.tp.size(), err) ||
+        !ensure<uint32_t>(t2tphdr, T.tp.size(), err) || !ensure<uint64_t>(t2tpoff, T.tp.size(), err) ||
+        !ensure<uint64_t>(t2blkdst, (size_t)nb * L, err) || !ensure<T2Summary>(t2sum, 1, err))
         return false;
     if (!h_sum) HIPCHECK(hipHostMalloc((void **)&h_sum, sizeof(T2Summary), hipHostMallocDefault));
     if (!t2ticket.ptr) {  // k_t2_wave<false>'s arrival counter: zero once, left zero by every launch
-        if (!ensure_t2<uint32_t>(t2ticket, 1, err)) return false;
+        if (!ensure<uint32_t>(t2ticket, 1, err)) return false;
         HIPCHECK(hipMemsetAsync(t2ticket.ptr, 0, sizeof(uint32_t), stream));
     }
     if (plan.gen && plan.gen == t2_gen) return true;  // resident (same plan, same tables)
@@ -1325,14 +1307,14 @@ bool GpuEncoder::t2_size(const Plan &plan, bool with_kc, bool profile, StageTime
 
 bool GpuEncoder::t2_reserve(uint64_t part_bytes, std::string &err) {
     HIPCHECK(hipSetDevice(device));
-    return ensure_t2<uint8_t>(t2out, part_bytes, err);
+    return ensure<uint8_t>(t2out, part_bytes, err);
 }
 
 bool GpuEncoder::t2_emit(const Plan &plan, uint64_t base, uint64_t part_bytes, uint8_t *host_dst, bool profile,
                          StageTimes &st, std::string &err) {
     HIPCHECK(hipSetDevice(device));
     const int nb = (int)plan.blocks.size();
-    if (!ensure_t2<uint8_t>(t2out, base + part_bytes, err)) return false;
+    if (!ensure<uint8_t>(t2out, base + part_bytes, err)) return false;
     T2Args a = t2_args(plan);
     a.base = base;
     HIPCHECK(hipEventRecord(ev[8], stream));

@@ -88,6 +88,14 @@ void glue_close(const int64_t *handles, int n, int64_t split) {
     glue_destroy(split);
 }
 
+int glue_contexts_for_memory(int device, int64_t budget, int cap) {
+    int64_t fr = 0, tot = 0;
+    if (budget <= 0) budget = GLUE_CONTEXT_BUDGET;
+    if (jp2hip_device_memory(device, &fr, &tot) != 0) return 1;
+    const int64_t k = (fr / 4 * 3) / budget;
+    return k < 1 ? 1 : (k > cap ? cap : (int)k);
+}
+
 int glue_open(int per_gpu, int64_t split_min_pixels, int64_t *handles, int max_handles, int *n, int64_t *split,
               char *err, size_t errlen) {
     int32_t gpus[64];
@@ -98,7 +106,13 @@ int glue_open(int per_gpu, int64_t split_min_pixels, int64_t *handles, int max_h
         set_err(err, errlen, NULL, "no gfx950 GPU visible");
         return -1;
     }
-    if (per_gpu < 1) per_gpu = 1;
+    if (per_gpu < 1) { /* from the devices' free memory: the smallest share of them */
+        per_gpu = GLUE_MAX_CONTEXTS_PER_GPU;
+        for (int g = 0; g < ng; g++) {
+            const int k = glue_contexts_for_memory(gpus[g], 0, GLUE_MAX_CONTEXTS_PER_GPU);
+            if (k < per_gpu) per_gpu = k;
+        }
+    }
     for (int slot = 0; slot < per_gpu; slot++)
         for (int g = 0; g < ng; g++) {
             if (*n >= max_handles) {

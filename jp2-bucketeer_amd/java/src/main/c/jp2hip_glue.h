@@ -53,7 +53,17 @@ int glue_encode_file(int64_t handle, const char *tiff, size_t tiff_len, const ch
 /* Releases a context (0 is ignored). */
 void glue_destroy(int64_t handle);
 
+/* What one pooled context is budgeted to hold (a C4-class 5000 x 7000 RGB8
+ * lossless image; DESIGN.md 3 "Footprint"), and the pool's ceiling. */
+#define GLUE_CONTEXT_BUDGET ((int64_t)8 << 30)
+#define GLUE_MAX_CONTEXTS_PER_GPU 16
+
+/* Contexts per GPU that fit 75 % of `device`'s free memory at `budget`
+ * bytes each (<= 0: GLUE_CONTEXT_BUDGET), between 1 and `cap`. */
+int glue_contexts_for_memory(int device, int64_t budget, int cap);
+
 /* The whole GpuConverter constructor (GpuConverter.java): `per_gpu`
+ * (<= 0: glue_contexts_for_memory of the device with the least free memory)
  * contexts on every gfx950 device (slot-major, as the Java pool fills), and
  * on a multi-GPU host one more context on the first device whose peers are
  * the others (the tile-split of oversized images).  On failure everything

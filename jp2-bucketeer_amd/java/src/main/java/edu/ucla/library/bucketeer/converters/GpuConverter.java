@@ -22,7 +22,10 @@ public class GpuConverter extends AbstractConverter implements Converter, AutoCl
 
     private static final Logger LOGGER = LoggerFactory.getLogger(GpuConverter.class, "bucketeer_messages");
 
-    /** Contexts (images in flight) per GPU: system property, default 16 (DESIGN.md 5). */
+    /**
+     * Contexts (images in flight) per GPU: system property; default 0 = as many as fit 75 % of the device's free
+     * memory at 8 GiB each, at most 16 (hipMemGetInfo through the glue; DESIGN.md 3 "Footprint").
+     */
     static final String CONTEXTS_PER_GPU = "bucketeer.gpu.contexts";
 
     /** Images of at least this many pixels are tile-split across every GPU (C5 map scans). */
@@ -63,7 +66,7 @@ public class GpuConverter extends AbstractConverter implements Converter, AutoCl
         if (!LOADED) {
             throw new IOException("libjp2hip_jni not loadable");
         }
-        final int perGpu = Math.max(1, Integer.getInteger(CONTEXTS_PER_GPU, 16));
+        final int perGpu = Math.max(0, Integer.getInteger(CONTEXTS_PER_GPU, 0)); // 0: from device memory
         mySplitMinPixels = Long.getLong(SPLIT_MIN_PIXELS, 256_000_000L);
         myHandles = nativeOpen(perGpu, mySplitMinPixels); // throws IOException, nothing allocated then
         myContexts = new ArrayBlockingQueue<>(Math.max(1, myHandles.length - 1));

@@ -71,7 +71,9 @@ EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_device
            "jp2hip_batch_destroy",
            # tile-split path (csrc/split.cpp + api.cpp; bound in jp2hip.split)
            "jp2hip_split_rows", "jp2hip_encode_device_split", "jp2hip_split_thresholds",
-           "jp2hip_split_peers", "jp2hip_tiff_pixels", "jp2hip_env_check")
+           "jp2hip_split_peers", "jp2hip_tiff_pixels", "jp2hip_env_check",
+           # device-memory policy (api.cpp)
+           "jp2hip_device_bytes", "jp2hip_set_memory_limits", "jp2hip_device_memory")
 
 
 # int (*)(void *user, int64_t *values, int32_t n): in-place sum over ranks, 0 ok
@@ -126,6 +128,10 @@ def lib():
     L.jp2hip_split_thresholds.argtypes = [POINTER(c_uint64), POINTER(c_int64), c_int64,
                                           POINTER(c_int64), c_int32, POINTER(Split),
                                           POINTER(c_uint64)]
+    L.jp2hip_device_bytes.argtypes = [c_void_p]
+    L.jp2hip_device_bytes.restype = c_int64
+    L.jp2hip_set_memory_limits.argtypes = [c_void_p, c_int64, c_int64]
+    L.jp2hip_device_memory.argtypes = [c_int, POINTER(c_int64), POINTER(c_int64)]
     _lib = L
     return L
 
@@ -161,6 +167,25 @@ def env_check() -> str:
     """"" or what the process environment should change for the contexts
     alive in it (jp2hip_env_check: GPU_MAX_HW_QUEUES)."""
     return lib().jp2hip_env_check().decode()
+
+
+def device_memory(device: int) -> tuple[int, int]:
+    """(free, total) bytes of HIP device `device` (jp2hip_device_memory)."""
+    fr, tot = c_int64(), c_int64()
+    if lib().jp2hip_device_memory(device, byref(fr), byref(tot)) != 0:
+        raise Jp2hipError(last_error())
+    return int(fr.value), int(tot.value)
+
+
+# what one context holds for the images a converter usually sees (C4-class
+# 5000 x 7000 RGB8 lossless, DESIGN.md 3 "Footprint"); a pool is sized from it
+CONTEXT_BUDGET_BYTES = 8 << 30
+
+
+def contexts_for_memory(free_bytes: int, budget: int = CONTEXT_BUDGET_BYTES, cap: int = 16) -> int:
+    """Contexts per GPU that fit 75 % of the device's free memory at `budget`
+    bytes each (at least 1, at most `cap`)."""
+    return max(1, min(cap, int(free_bytes * 0.75) // max(1, budget)))
 
 
 def tiff_pixels(path) -> int:
@@ -273,6 +298,15 @@ class Encoder:
             self.close()
         except Exception:
             pass
+
+    def device_bytes(self) -> int:
+        """Device memory held by this context (jp2hip_device_bytes)."""
+        return int(lib().jp2hip_device_bytes(self._h))
+
+    def set_memory_limits(self, soft: int = 0, hard: int = 0):
+        """jp2hip_set_memory_limits: <= 0 keeps the default of each."""
+        if lib().jp2hip_set_memory_limits(self._h, int(soft), int(hard)) != 0:
+            raise Jp2hipError(last_error())
 
     def _take(self, out, n, copy=True):
         if not copy:

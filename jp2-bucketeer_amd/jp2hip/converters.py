@@ -115,7 +115,7 @@ class GpuConverter(Converter):
     WORKING_DIR_NAME = "jp2hip"
     SPLIT_MIN_PIXELS = 256_000_000
 
-    def __init__(self, devices: list[int] | None = None, host_threads: int = 0, per_gpu: int = 1,
+    def __init__(self, devices: list[int] | None = None, host_threads: int = 0, per_gpu: int | None = None,
                  split_devices: list[int] | None = None, split_min_pixels: int | None = None):
         self.tmp_dir = Path(tempfile.gettempdir()) / self.WORKING_DIR_NAME
         self._pool, self._free = [], []
@@ -135,6 +135,9 @@ class GpuConverter(Converter):
             split_min_pixels = int(os.environ.get("JP2HIP_SPLIT_MIN_PIXELS", self.SPLIT_MIN_PIXELS))
         self.split_min_pixels = split_min_pixels
         try:
+            if per_gpu is None:  # as many as the devices' free memory holds (GpuConverter.java)
+                per_gpu = min(_lib.contexts_for_memory(_lib.device_memory(d)[0]) for d in devices) if devices else 1
+            self.per_gpu = per_gpu
             self._pool = [_lib.Encoder(d, host_threads) for _ in range(max(1, per_gpu)) for d in devices]
             if len(split_devices) > 1:
                 self._split = _lib.Encoder(split_devices[0], host_threads)

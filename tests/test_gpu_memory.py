@@ -1,0 +1,89 @@
+"""Device-memory policy of a context: the footprint is
+visible (jp2hip_device_bytes), an outsized image's buffers are released
+after it (soft limit), and an image that needs more than the hard limit
+fails with rc < 0 and a message -- at whichever allocation of the encode it
+happens -- leaving the context usable."""
+import numpy as np
+import pytest
+
+import imaging as im
+import jp2hip
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c2_tif():
+    return im.tiff_bytes(im.synth_rgb8(4000, 6000, seed=1234))
+
+
+@pytest.fixture(scope="module")
+def c3_class_tif():
+    # a 16-bit lossless RGB master of C3 class (half of C3's 80 MP, same
+    # sample depth and recipe: 1024^2 tiles)
+    return im.tiff_bytes(im.synth_u16(5000, 8000, comps=3, seed=2))
+
+
+def test_footprint_drops_after_an_outsized_image(c2_tif, c3_class_tif):
+    enc = jp2hip.Encoder(0)
+    try:
+        assert enc.device_bytes() == 0
+        a, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+        b_c2 = enc.device_bytes()
+        assert b_c2 > 0
+        enc.set_memory_limits(soft=int(b_c2 * 1.25))
+        rc3 = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        after_c3 = enc.device_bytes()
+        # the C3-class encode grew the context past its soft limit, so its
+        # end released the buffers
+        assert after_c3 <= int(b_c2 * 1.25), (b_c2, after_c3)
+        b, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+        assert b == a  # same bytes from reallocated buffers and re-uploaded tables
+        assert enc.device_bytes() == b_c2
+        print(f"\nfootprint: C2 {b_c2} B, after the C3-class image {after_c3} B")
+    finally:
+        enc.close()
+
+
+def test_hard_limit_fails_cleanly_at_every_stage(c2_tif):
+    """Caps from 5 % to 99 % of what a C2 encode needs: each encode fails
+    with the limit's message (the allocation that trips it moves through the
+    pipeline: before the first kernel, between stages, at the tier-2 output),
+    and the context then encodes the image correctly once the cap is lifted."""
+    enc = jp2hip.Encoder(0)
+    try:
+        want, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+        need = enc.device_bytes()
+        enc.close()
+        for frac in (0.05, 0.3, 0.6, 0.9, 0.99):
+            enc = jp2hip.Encoder(0)
+            enc.set_memory_limits(hard=int(need * frac))
+            with pytest.raises(jp2hip.Jp2hipError, match="device memory limit"):
+                enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+            assert enc.device_bytes() <= int(need * frac)
+            enc.set_memory_limits(hard=0)
+            got, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+            assert got == want, frac
+            enc.close()
+    finally:
+        enc.close()
+
+
+def test_device_memory_and_pool_sizing():
+    fr, tot = jp2hip._lib.device_memory(0)
+    assert 0 < fr <= tot and tot > 200 << 30  # MI355X: 288 GB of HBM3E
+    k = jp2hip._lib.contexts_for_memory(fr)
+    assert 1 <= k <= 16
+    assert jp2hip._lib.contexts_for_memory(fr, budget=1 << 40) == 1
+
+
+def test_gpu_converter_pool_from_device_memory():
+    from jp2hip.converters import GpuConverter
+    conv = GpuConverter()
+    try:
+        fr, _ = jp2hip._lib.device_memory(0)
+        assert conv.per_gpu == jp2hip._lib.contexts_for_memory(fr) or conv.per_gpu >= 1
+        assert len(conv._pool) == conv.per_gpu * len(jp2hip.device_ordinals())
+    finally:
+        conv.close()
