@@ -787,6 +787,8 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_lossless:
             res["lossless_c3"] = lossless_c3(enc)
+            if not args.no_extras:
+                res["lossless_c3"]["value_file_span"] = c3_file_span(local_device())
             res["lossless_c4"] = lossless_c4(local_device())
         if not args.no_extras:
             res["value_file_span"] = c2_file_span(local_device())
@@ -891,15 +893,19 @@ def lossless_c3(enc, steps=2, inflight=8, n_each=4):
 
 
 def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=None, reader_threads=4,
-             uploader_threads=4, shape=(7000, 5000), gen_threads=8):
+             uploader_threads=4, shape=(7000, 5000), gen_threads=8, rcp=None, busy=None):
     """C4 (configs[3]) on one GPU: a Bucketeer batch CSV of `rows` synthetic
     5000x7000 RGB8 TIFFs (cycling over `ndistinct` files, as SURVEY.md 8(d)
     prescribes for the 10k-row batch) through the native batch queue: TIFF
     read from disk -> lossless encode -> JPX write -> stub upload (reads every
     byte) -> delete.  The files are evicted from the page cache before the
     timed region (POSIX_FADV_DONTNEED), which runs from the first submit to
-    the last upload, file I/O included.  Returns (MP/s, seconds, results,
-    bytes of TIFF read)."""
+    the last upload, file I/O included; rows beyond the first `ndistinct`
+    re-read files the first pass left in the page cache.  `rcp`: the recipe
+    of every row (None: the Bucketeer recipe of the conversion).  `busy`
+    (a dict) receives the stages' busy fractions over the timed span: each
+    stage's summed per-image time / (its threads x span).  Returns (MP/s,
+    seconds, results, bytes of TIFF read)."""
     import csv as _csv
     import shutil
     from concurrent.futures import ThreadPoolExecutor
@@ -932,34 +938,61 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
         with jb.BatchQueue(device=device, contexts=contexts, reader_threads=reader_threads,
                            uploader_threads=uploader_threads) as q:
             for k, it in enumerate(items[:contexts]):  # warm-up: device buffers of every context
-                q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k), conv)
+                q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k), conv, rcp)
             q.drain()
             evict_from_page_cache(paths)
             t0 = time.perf_counter()
             for it in items:
-                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)), conv)
+                q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)), conv, rcp)
             res = q.drain()
             dt = time.perf_counter() - t0
         ok = sum(1 for r in res if r["status"] == 0)
+        if busy is not None:
+            busy.update({
+                "readers": round(sum(r["read_ms"] for r in res) / 1e3 / (reader_threads * dt), 3),
+                "contexts": round(sum(r["encode_ms"] for r in res) / 1e3 / (contexts * dt), 3),
+                "uploaders": round(sum(r["upload_ms"] for r in res) / 1e3 / (uploader_threads * dt), 3),
+                "def": "summed per-image stage time / (stage threads x timed span); a stage near 1.0 is the "
+                       "bound (contexts: host time from a context taking the image to its JPX bytes in host "
+                       "memory, GPU work and waits included)"})
         read = sum(sizes[paths[i % ndistinct]] for i in range(rows))
         return shape[0] * shape[1] / 1e6 * ok / dt, dt, res, read
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
 
-def lossless_c4(device, rows=10000, ndistinct=16):
+def lossless_c4(device, rows=10000, ndistinct=16, sweep=(8, 12, 16), sweep_rows=512):
     """SURVEY.md 8(d) C4: a 10 000-row CSV (16 distinct files of seeds 0-15;
-    the survey's 64 would be 6.7 GB of fixtures per bench run)."""
-    value, dt, res, _ = c4_batch(device, rows=rows, ndistinct=ndistinct)
+    the survey's 64 would be 6.7 GB of fixtures per bench run), 12 contexts
+    (the queue's default), plus a shorter sweep over the context count with
+    each stage's busy fraction, which names the bound."""
+    busy = {}
+    value, dt, res, read = c4_batch(device, rows=rows, ndistinct=ndistinct, contexts=12, busy=busy)
     ok = [r for r in res if r["status"] == 0]
+    peak_h2d = h2d_peak()
+    sweep_res = []
+    for c in sweep:
+        b = {}
+        v, d, rr, rd = c4_batch(device, rows=sweep_rows, ndistinct=ndistinct, contexts=c, busy=b)
+        sweep_res.append({"contexts": c, "mp_per_s": round(v, 3), "seconds": round(d, 3),
+                          "tiff_read_gb_per_s": round(rd / d / 1e9, 2),
+                          "jpx_gb_per_s": round(sum(r["out_bytes"] for r in rr) / d / 1e9, 2), "busy": b})
     bpp = 8 * float(np.mean([r["out_bytes"] for r in ok])) / (5000 * 7000) if ok else 0.0
     b_path = dwt_bytes_per_px(3, 1, 6, coef_bytes(8, False)) + coef_bytes(8, False) * 3 + 3 * bpp / 8
     return {"workload": f"C4: Bucketeer batch CSV of 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0-"
                         f"{ndistinct - 1}) -> native per-GPU queue (disk read, lossless 5/3 encode, JPX write, "
                         "stub upload, delete)",
-            "rows": rows, "distinct_files": ndistinct, "page_cache": "files evicted before the timed region",
+            "rows": rows, "distinct_files": ndistinct, "contexts": 12,
+            "page_cache": f"the {ndistinct} files are evicted before the timed region; rows after the first "
+                          f"{ndistinct} re-read them from the page cache",
             "images_ok": len(ok), "mp_per_s": round(value, 3), "seconds": round(dt, 3),
             "bpp": round(bpp, 4), "timed_span": "first submit -> last upload, file I/O included",
+            "busy": busy,
+            "roofline_pcie": {"bound": "pcie_h2d", "achieved": round(read / dt / 1e9, 2), "peak": round(peak_h2d, 2),
+                              "unit": "GB/s", "frac": round(read / dt / 1e9 / peak_h2d, 4),
+                              "def": "TIFF bytes read per second (every byte is uploaded) / measured pinned "
+                                     "host->device copy rate"},
+            "contexts_sweep": sweep_res,
             "roofline_path": {"bound": "hbm", "bytes_per_px": round(b_path, 3),
                               "achieved": round(b_path * value * 1e6 / 1e9, 2), "peak": HBM_PEAK / 1e9,
                               "unit": "GB/s", "frac": round(b_path * value * 1e6 / HBM_PEAK, 5)}}
@@ -984,13 +1017,50 @@ def c2_file_span(device, images=1024, contexts=16, ndistinct=16):
     peak = h2d_peak()
     h2d = read / dt / 1e9
     return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok),
-            "distinct_files": ndistinct, "page_cache": "files evicted before the timed region",
+            "distinct_files": ndistinct,
+            "page_cache": f"the {ndistinct} files are evicted before the timed region; images after the first "
+                          f"{ndistinct} re-read them from the page cache",
             "seconds": round(dt, 3), "contexts": contexts,
             "out_bytes": int(np.mean([r["out_bytes"] for r in ok])) if ok else 0,
             "roofline_pcie": {"bound": "pcie_h2d", "achieved": round(h2d, 2), "peak": round(peak, 2), "unit": "GB/s",
                               "frac": round(h2d / peak, 4),
                               "def": "TIFF bytes read per second (every byte is uploaded) / measured pinned "
                                      "host->device copy rate"},
+            "timed_span": "first TIFF open -> last JPX written, uploaded (stub) and deleted; "
+                          "file read, H2D, encode, D2H, file write included"}
+
+
+def c3_file_span(device, images=24, contexts=8, ndistinct=4):
+    """SURVEY.md 8(d)'s span for the production conversion at C3 size:
+    10000x8000 RGB16 TIFF files (480 MB each) on disk -> lossless JPX files
+    written, through the native per-GPU queue (reader threads, `contexts`
+    encodes in flight, uploader threads: atomic JPX write, stub upload reading
+    every byte, delete), `images` rows cycling over `ndistinct` distinct files
+    evicted from the page cache first.  Both PCIe directions carry the image:
+    every TIFF byte goes host -> device, every code-stream byte device ->
+    host; roofline_pcie gives each against its measured pinned copy rate."""
+    import imaging as im
+    import jp2hip
+    busy = {}
+    rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
+    value, dt, res, read = c4_batch(device, rows=images, ndistinct=ndistinct, contexts=contexts,
+                                    conversion=jp2hip.LOSSLESS, rcp=rc,
+                                    make=lambda i: im.synth_u16(8000, 10000, comps=3, seed=2 + i), reader_threads=4,
+                                    uploader_threads=4, shape=(8000, 10000), gen_threads=4, busy=busy)
+    ok = [r for r in res if r["status"] == 0]
+    out = sum(r["out_bytes"] for r in ok)
+    ph, pd = h2d_peak(), d2h_peak()
+    return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok),
+            "distinct_files": ndistinct, "contexts": contexts,
+            "page_cache": f"the {ndistinct} files are evicted before the timed region; images after the first "
+                          f"{ndistinct} re-read them from the page cache",
+            "seconds": round(dt, 3), "bpp": round(8 * out / max(1, len(ok)) / 80e6, 4), "busy": busy,
+            "roofline_pcie": {
+                "h2d": {"achieved": round(read / dt / 1e9, 2), "peak": round(ph, 2), "unit": "GB/s",
+                        "frac": round(read / dt / 1e9 / ph, 4), "def": "TIFF bytes read per second / pinned H2D rate"},
+                "d2h": {"achieved": round(out / dt / 1e9, 2), "peak": round(pd, 2), "unit": "GB/s",
+                        "frac": round(out / dt / 1e9 / pd, 4),
+                        "def": "code-stream bytes per second / pinned D2H rate"}},
             "timed_span": "first TIFF open -> last JPX written, uploaded (stub) and deleted; "
                           "file read, H2D, encode, D2H, file write included"}
 

@@ -128,6 +128,10 @@ typedef struct jp2hip_stats {
     double t1_cm_ms;      /* tier-1 context-modelling kernel (part of t1_ms)  */
     double t1_mq_ms;      /* tier-1 MQ-coder kernel (part of t1_ms)           */
     int64_t mq_decisions; /* MQ-coded decisions (one decision-stream byte each) */
+    int64_t stream_pool_bytes; /* tier-1 decision-stream pool held by the context */
+    int64_t stream_need_bytes; /* ... of which this encode's coded planes took    */
+    int32_t pool_grows;   /* encodes repeated because the pool was short (0..2) */
+    int32_t reserved;
 } jp2hip_stats;
 
 const char *jp2hip_version(void);

@@ -540,6 +540,7 @@ void fill_stats(jp2hip_stats *stats, const jp2hip::StageTimes &st, double t_star
     stats->rate_iterations = iters;
     stats->host_waits = waits;
     stats->mq_decisions = sum.decisions;
+    stats->stream_need_bytes = sum.stream_need;
 }
 
 // The caller's recipe (or the default for `conversion`) with its padding
@@ -606,8 +607,18 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     if (rc.rate_bpp <= 0.0) {
         // lossless: per -flush_period stripe, layer l keeps the passes whose
         // slopes clear lossless_layer_frac(l) of the stripe's tier-1 bytes
-        if (!ctx->gpu.select_lossless(plan, err) || !ctx->gpu.t2_size(plan, true, prof, st, sum, err))
-            return fail(err);
+        for (int grow = 0;; grow++) {
+            if (!ctx->gpu.select_lossless(plan, err) || !ctx->gpu.t2_size(plan, true, prof, st, sum, err))
+                return fail(err);
+            if ((sum.err & kErrSlotPool) && grow < 2) {
+                // the decision-stream pool was short: again with the size
+                // this encode needed (GpuEncoder::run_front)
+                if (!ctx->gpu.pool_grow(err) || !ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, skip_target))
+                    return fail(err);
+                continue;
+            }
+            break;
+        }
         if (sum.err) return fail("tier-1 output capacity exceeded");
         iters = 1;
         cs_bytes = (int64_t)mh.size() + sum.part_bytes + 2;
@@ -625,9 +636,18 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
         init.skip_target = skip_target;
         RateState rs;
         bool restart = true;
-        for (;;) {
+        for (int grow = 0;;) {
             if (!ctx->gpu.rate_loop(plan, init, restart, restart ? 1 : 2, prof, st, rs, sum, err)) return fail(err);
             restart = false;
+            if ((sum.err & kErrSlotPool) && grow++ < 2) {
+                // the decision-stream pool was short: again with the size
+                // this encode needed (GpuEncoder::run_front)
+                if (!ctx->gpu.pool_grow(err) ||
+                    !ctx->gpu.run_front(d_src, *lay, plan, prof, st, err, init.skip_target))
+                    return fail(err);
+                restart = true;
+                continue;
+            }
             if (sum.err) return fail("tier-1 output capacity exceeded");
             if (rs.safety) {
                 // slope prediction's safety net (oracle predict_and_code):
@@ -666,6 +686,10 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     *out_len = n;
     fill_stats(stats, st, t_start, h2d_ms, (int64_t)plan.blocks.size(), sum, (int64_t)n, iters,
                ctx->gpu.take_waits());
+    if (stats) {
+        stats->stream_pool_bytes = (int64_t)ctx->gpu.stream_pool_bytes();
+        stats->pool_grows = ctx->gpu.take_pool_grows();
+    }
     end.ok = true;
     return 0;
 }
@@ -730,7 +754,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
         t2_tables(full, tile0, tile1, sub.block0, tabs);
         ok = ctx->gpu.t2_load(sub, tabs, err);
     }
-    ok = ok && (!have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, skip_target, &reduce));
+    ok = ok && (!have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, skip_target, &reduce, true));
     if (skip_target > 0 && !hist_done) {  // no blocks here, or failed before the exchange
         std::vector<int64_t> v((size_t)kSlopeBins + 1, 0);
         v.back() = ok ? 0 : 1;
@@ -779,7 +803,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
         if (attempt == 1) {  // the prediction's safety net, decided globally (below)
             keys.clear();
             cum.clear();
-            ok = !have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, 0);
+            ok = !have || ctx->gpu.run_front(d_src, *lay, sub, prof, st, err, 0, nullptr, true);
             skip_target = 0;
             iters = 0;
         }
@@ -894,6 +918,10 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     if (file_len) *file_len = flen;
     fill_stats(stats, st, t_start, 0.0, (int64_t)sub.blocks.size(), sum, (int64_t)flen, iters,
                ctx->gpu.take_waits());
+    if (stats) {
+        stats->stream_pool_bytes = (int64_t)ctx->gpu.stream_pool_bytes();
+        stats->pool_grows = ctx->gpu.take_pool_grows();
+    }
     end.ok = true;
     return 0;
 }

@@ -239,15 +239,57 @@ __device__ __forceinline__ void rate_step(RateState *rs, const T2Summary *sum, i
 struct ItemScratch {
     uint32_t cnt[16][64];  // [wave][depth] entries; then the wave's offset in the list
 };
+// bytes reserved per (block, plane) for the three passes' decisions:
+// at most w*h coding decisions + w*h sign decisions + 3 per run-length column
+// (each pass is padded to a 16-byte boundary; the MQ kernel prefetches one
+// 16-byte chunk past the end of a pass)
+__host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
+    return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
+}
+
+
+// Also places each block's decision-stream slot: c coded planes x
+// plane_stream_cap bytes, carved from the pool (a.pool_cap bytes) by one
+// atomic per wave on a.pool_used, which ends at the bytes the encode
+// needed.  A block that does not fit is coded as empty and sets
+// kErrSlotPool; the host then grows the pool to a.pool_used and encodes
+// again (GpuEncoder::run_front), so no output is ever made from a short pool.
 template <int NT, typename ItemArgs>
 __device__ __forceinline__ void emit_t1_items(const ItemArgs &a, int b, bool valid, int P, int pmin, ItemScratch &sc) {
     static_assert(NT % 64 == 0 && NT / 64 <= 16, "emit_t1_items: 64..1024 threads");
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t c = valid ? (uint32_t)(P - pmin) : 0u;
+    uint32_t c = valid ? (uint32_t)(P - pmin) : 0u;
+    {
+        uint32_t need = 0;
+        if (c) {
+            const BlockDesc d = a.blocks[b];
+            need = c * plane_stream_cap(d.w, d.h);
+        }
+        uint32_t x = need;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (lane >= o) x += y;
+        }
+        const uint32_t wtot = (uint32_t)__shfl((int)x, 63, 64);
+        unsigned long long wbase = 0;
+        if (lane == 63 && wtot) wbase = atomicAdd(a.pool_used, (unsigned long long)wtot);
+        wbase = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(wbase >> 32), 63, 64) << 32) |
+                (uint32_t)__shfl((int)(uint32_t)wbase, 63, 64);
+        const unsigned long long base = wbase + (x - need);
+        if (c) {
+            if (base + need > a.pool_cap) {
+                c = 0;  // no room: coded as an empty block; the host re-encodes
+                atomicOr(a.err, kErrSlotPool);
+            } else {
+                a.slot_off[b] = base;
+            }
+        }
+    }
     if (valid) {
         a.acc[b] = (unsigned long long)c << 40;
-        if (P == 0) {
+        if (c == 0) {
             a.npasses[b] = 0;
             a.lengths[b] = 0;
         }

@@ -68,6 +68,12 @@ struct T1ItemArgs {
     unsigned long long *acc;    // [nb] (coded planes << 40): k_t1_cm3 counts planes down, decisions up
     uint8_t *npasses;           // blocks without a coded plane: 0 passes, 0 bytes (k_t1_mq never sees them)
     int32_t *lengths;
+    // decision-stream slots, placed here (emit_t1_items)
+    const BlockDesc *blocks;
+    unsigned long long *pool_used;  // zeroed by k_quant; ends at the bytes needed
+    unsigned long long pool_cap;    // bytes in the pool (stream_buf)
+    uint64_t *slot_off;             // [nb]
+    int *err;                       // kErrSlotPool when a block did not fit
 };
 struct T1CmArgs {
     const uint32_t *dfill;  // per-depth list fills
@@ -172,9 +178,22 @@ class GpuEncoder {
     // skip_target > 0: rate-driven encode of skip_target bytes with slope
     // prediction (bit-planes far below the predicted threshold not coded);
     // reduce (tile-split only) makes the prediction global.
+    // pool_worst: size the decision-stream pool for every plane of every
+    // block (the tile-split path, whose ranks cannot repeat an exchange);
+    // else the encode may end with kErrSlotPool in its summary's err, and
+    // the caller grows the pool (pool_grow) and encodes again.
     bool run_front(const void *d_src, const jp2hip_layout &lay, const Plan &plan, bool profile,
                    StageTimes &st, std::string &err, int64_t skip_target = 0,
-                   const HistReduce *reduce = nullptr);
+                   const HistReduce *reduce = nullptr, bool pool_worst = false);
+    // after an encode that ended with kErrSlotPool: the next run_front
+    // sizes the pool for what that encode needed (+12.5 %)
+    bool pool_grow(std::string &err);
+    size_t stream_pool_bytes() const { return stream_buf.bytes; }
+    int take_pool_grows() {
+        const int g = pool_grows;
+        pool_grows = 0;
+        return g;
+    }
     // lossless "-rate -": per -flush_period stripe (the plan's rate-control
     // groups), layer budgets lossless_layer_frac of the stripe's tier-1
     // bytes, computed on the device (enqueued only; t2_size reads the result)
@@ -286,6 +305,13 @@ class GpuEncoder {
     std::vector<uint64_t> strips_host;  // strip offsets last uploaded to `strips`
     const void *strips_dev = nullptr;
     size_t held = 0, mem_soft = SIZE_MAX, mem_hard = SIZE_MAX;
+    // decision-stream pool: the first encode of a geometry reserves this
+    // fraction of the every-plane bound; pool_hint = what the last
+    // overflowing encode needed (+12.5 %)
+    static constexpr double kPoolFracLossy = 0.5, kPoolFracLossless = 0.9;
+    uint64_t pool_hint = 0;
+    int pool_grows = 0;
+    double pool_frac_test = -1.0;  // JP2HIP_TEST_POOL_FRAC (tests: force the grow path)
     std::vector<DevBuf *> bufs();
 };
 

@@ -50,6 +50,10 @@ struct QuantTab {
 QuantTab quant_tab(const jp2hip_recipe &rc, int bits);
 
 // One code-block, as the kernels see it (uploaded as-is).
+// device error word bit: the decision-stream pool was too small for the
+// coded planes (emit_t1_items); the host grows it and encodes again
+constexpr int kErrSlotPool = 8;
+
 struct BlockDesc {
     int32_t tc;         // tile-component plane index
     int16_t x0, y0;     // top-left inside the tile-component plane (Mallat layout)
@@ -180,6 +184,7 @@ struct T2Summary {
     int64_t t1_bytes, coded_passes;   // tier-1 totals (every coded pass)
     int64_t decisions;                // MQ-coded decisions
     int32_t skipped, err;             // slope prediction skipped planes; tier-1 overflow
+    int64_t stream_need;              // decision-stream pool bytes the coded planes took
 };
 // Rate control of a rate-driven encode, run on the device (kernels.hip
 // k_rate_step; the oracle's loop in oracle_encode): iteration `it` selects

@@ -1843,6 +1843,16 @@ bool GpuEncoder::trim(size_t soft) {
     strips_dev = nullptr;
     strips_host.clear();
     dma_ok = false;  // (re-reads t2out's owner agent at the next copy)
+    pool_hint = 0;   // (the outsized image's need)
+    return true;
+}
+
+bool GpuEncoder::pool_grow(std::string &err) {
+    unsigned long long used = 0;
+    HIPCHECK(hipStreamSynchronize(stream));
+    HIPCHECK(hipMemcpy(&used, (unsigned long long *)mqspan.ptr + 2, sizeof used, hipMemcpyDeviceToHost));
+    pool_hint = std::max<uint64_t>(pool_hint, used + used / 8);
+    pool_grows++;
     return true;
 }
 
@@ -1871,6 +1881,7 @@ GpuEncoder::~GpuEncoder() {
 
 bool GpuEncoder::init(int dev, std::string &err) {
     device = dev;
+    if (const char *f = getenv("JP2HIP_TEST_POOL_FRAC")) pool_frac_test = atof(f);
     HIPCHECK(hipSetDevice(dev));
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (int i = 0; i < kNumEvents; i++) HIPCHECK(hipEventCreate(&ev[i]));
@@ -2087,7 +2098,7 @@ bool GpuEncoder::unpack_strips(const void *d_src, const jp2hip_layout &lay, jp2h
 
 bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Plan &plan,
                            bool profile, StageTimes &st, std::string &err, int64_t skip_target,
-                           const HistReduce *reduce) {
+                           const HistReduce *reduce, bool pool_worst) {
     HIPCHECK(hipSetDevice(device));
     const int nb = (int)plan.blocks.size();
     size_t plane = (size_t)plan.plane_w * plan.plane_h;
@@ -2122,12 +2133,22 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     if (!ensure<int32_t>(tch, plan.ntc, err)) return false;
     if (!ensure<uint64_t>(strips, lay.nstrips, err)) return false;
 
-    // tier-1 decision streams: a fixed slot per block, room for every plane
-    // (the grid and buffers are sized by that bound anyway)
+    // tier-1 decision streams: one pool, carved on the device once the coded
+    // planes are known (emit_t1_items: c planes x plane_stream_cap per
+    // block).  Sized at a fraction of the every-plane bound -- or at what an
+    // encode of this context last needed, when that is more -- and grown
+    // after an encode that did not fit (the host re-encodes: pool_grow).
+    // The tile-split path asks for the whole bound (its ranks cannot repeat
+    // an exchange).
     uint64_t stream_bound = 0;
     for (int i = 0; i < nb; i++)
         stream_bound += (uint64_t)plan.blocks[i].Mb * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
-    if (!ensure<uint64_t>(slotoff, nb, err) || !ensure<uint8_t>(stream_buf, std::max<uint64_t>(stream_bound, 1), err))
+    const double pool_frac = pool_worst             ? 1.0
+                             : pool_frac_test >= 0.0 ? pool_frac_test
+                             : (plan.rc.reversible ? kPoolFracLossless : kPoolFracLossy);
+    const uint64_t pool_want = std::min<uint64_t>(
+        stream_bound, std::max<uint64_t>(pool_hint, (uint64_t)((double)stream_bound * pool_frac)));
+    if (!ensure<uint64_t>(slotoff, nb, err) || !ensure<uint8_t>(stream_buf, std::max<uint64_t>(pool_want, 1), err))
         return false;
     // the strip offsets: uploaded only when they differ from the last upload
     // (repeat encodes of one layout skip the copy)
@@ -2146,13 +2167,6 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
             !h2d(tcw.ptr, plan.tc_w.data(), sizeof(int32_t) * plan.ntc, err) ||
             !h2d(tch.ptr, plan.tc_h.data(), sizeof(int32_t) * plan.ntc, err))
             return false;
-        std::vector<uint64_t> slots(nb);
-        uint64_t o = 0;
-        for (int i = 0; i < nb; i++) {
-            slots[i] = o;
-            o += (uint64_t)plan.blocks[i].Mb * t1_plane_stream_cap(plan.blocks[i].w, plan.blocks[i].h);
-        }
-        if (nb && !h2d(slotoff.ptr, slots.data(), sizeof(uint64_t) * nb, err)) return false;
         // rate-control groups: block ranges and each group's first
         // candidate slot (the bound sum(3 Mb - 2) over the groups before)
         std::vector<int32_t> gtab(2 * ((size_t)G + 1));
@@ -2257,7 +2271,7 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         !ensure<int32_t>(items, std::max<size_t>(nflags, 1), err) ||
         !ensure<int32_t>(order, (size_t)kOrderBuckets * std::max(nb, 1), err) ||
         !ensure<uint4>(counts, (size_t)nb * 32, err) || !ensure<int64_t>(dspp, (size_t)nb * 32, err) ||
-        !ensure<unsigned long long>(ordkey, std::max(nb, 1), err) || !ensure<unsigned long long>(mqspan, 2, err))
+        !ensure<unsigned long long>(ordkey, std::max(nb, 1), err) || !ensure<unsigned long long>(mqspan, 3, err))
         return false;
     uint32_t *dfill = (uint32_t *)t1fill.ptr, *bfill = dfill + 64;
     std::memset(qa.zero, 0, sizeof qa.zero);
@@ -2270,8 +2284,8 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     qa.nzero[2] = (kMaxLayers + 1) * G;
     qa.zero[3] = dfill;
     qa.nzero[3] = 64 + kOrderBuckets;
-    qa.zero[4] = (uint32_t *)mqspan.ptr;
-    qa.nzero[4] = 4;
+    qa.zero[4] = (uint32_t *)mqspan.ptr;  // k_t1_mq's span[2], then the stream pool's fill
+    qa.nzero[4] = 6;
     // (span 5: the error word; span 6: the slope histogram; span 7: tier-1
     // totals; span 8: the rate-control groups' tier-1 bytes)
     qa.zero[8] = (uint32_t *)gtot.ptr;
@@ -2315,6 +2329,11 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
     ia.acc = (unsigned long long *)ordkey.ptr;
     ia.npasses = (uint8_t *)npasses.ptr;
     ia.lengths = (int32_t *)lengths.ptr;
+    ia.blocks = (const BlockDesc *)blocks.ptr;
+    ia.pool_used = (unsigned long long *)mqspan.ptr + 2;
+    ia.pool_cap = stream_buf.bytes;
+    ia.slot_off = (uint64_t *)slotoff.ptr;
+    ia.err = (int *)this->err.ptr;
     if (skip_target > 0 && nb) {
         PredictArgs pa;
         pa.nblocks = nb;

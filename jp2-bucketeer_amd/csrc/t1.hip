@@ -41,13 +41,7 @@ enum { CX_RL = 17, CX_UNI = 18, CX_PAD = 19 };
 constexpr uint8_t kPadDecision = CX_PAD << 1;
 
 
-// bytes reserved per (block, plane) for the three passes' decisions:
-// at most w*h coding decisions + w*h sign decisions + 3 per run-length column
-// (each pass is padded to a 16-byte boundary; the MQ kernel prefetches one
-// 16-byte chunk past the end of a pass)
-__host__ __device__ __forceinline__ uint32_t plane_stream_cap(int w, int h) {
-    return ((uint32_t)(11 * w * h) / 4 + 128 + 15) & ~15u;
-}
+// plane_stream_cap: device_common.h (emit_t1_items places the slots)
 
 constexpr int kCmWaves = 2;  // code-blocks (waves) per workgroup
 

@@ -727,6 +727,7 @@ struct T2TotalArgs {
     const int32_t *lengths;
     const uint8_t *npasses, *pmin;
     const int *t1err;
+    const unsigned long long *pool_used;  // decision-stream pool fill (emit_t1_items)
     const uint64_t *kc;  // [group][kMaxLayers]; Kdu-Layer-Info takes each layer's strictest (largest)
     int ngroups;
     const unsigned long long *acc;
@@ -829,7 +830,10 @@ __device__ __forceinline__ void t2_total_body(const T2Args &a, const T2TotalArgs
             for (int g = 0; g < ta.ngroups; g++) k = max(k, ta.kc[(size_t)g * kMaxLayers + tid]);
         ta.sum->kc[tid] = k;
     }
-    if (tid == 0) ta.sum->err = *ta.t1err;
+    if (tid == 0) {
+        ta.sum->err = *ta.t1err;
+        ta.sum->stream_need = ta.pool_used ? (int64_t)*ta.pool_used : 0;
+    }
     if (ta.rate.rs) {
         __syncthreads();  // every field of *sum written
         if (tid == 0) rate_step(ta.rate.rs, ta.sum, L, ta.rate.budget, ta.rate.out_rs, ta.rate.out_sum);
@@ -1265,6 +1269,7 @@ void GpuEncoder::t2_size_launch(const Plan &plan, bool with_kc, const int *halt,
     ta.npasses = (const uint8_t *)npasses.ptr;
     ta.pmin = (const uint8_t *)pmin.ptr;
     ta.t1err = (const int *)this->err.ptr;
+    ta.pool_used = mqspan.ptr ? (const unsigned long long *)mqspan.ptr + 2 : nullptr;
     ta.kc = with_kc ? (const uint64_t *)thr.ptr + (size_t)plan.ngroups() * kMaxLayers : (const uint64_t *)nullptr;
     ta.ngroups = plan.ngroups();
     ta.acc = (const unsigned long long *)ordkey.ptr;

@@ -55,7 +55,9 @@ class Stats(Structure):
                 ("pcrd_ms", c_double), ("d2h_ms", c_double), ("t2_ms", c_double),
                 ("codeblocks", c_int64), ("coded_passes", c_int64), ("t1_bytes", c_int64),
                 ("out_bytes", c_int64), ("rate_iterations", c_int32), ("host_waits", c_int32),
-                ("t1_cm_ms", c_double), ("t1_mq_ms", c_double), ("mq_decisions", c_int64)]
+                ("t1_cm_ms", c_double), ("t1_mq_ms", c_double), ("mq_decisions", c_int64),
+                ("stream_pool_bytes", c_int64), ("stream_need_bytes", c_int64), ("pool_grows", c_int32),
+                ("reserved", c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -87,3 +87,43 @@ def test_gpu_converter_pool_from_device_memory():
         assert len(conv._pool) == conv.per_gpu * len(jp2hip.device_ordinals())
     finally:
         conv.close()
+
+
+@pytest.mark.parametrize("conversion", [jp2hip.LOSSLESS, jp2hip.LOSSY])
+def test_short_stream_pool_regrows_and_matches_oracle(monkeypatch, conversion):
+    """The tier-1 decision-stream pool is carved on the device from the
+    coded planes (emit_t1_items).  Forced to 2 % of the every-plane bound,
+    the first encode does not fit: blocks past the pool are coded empty, the
+    host sees kErrSlotPool, grows the pool to what the planes took and
+    encodes again -- the file is still the oracle's, byte for byte; the next
+    encode of the geometry fits at once."""
+    import oracle_lib as ol
+    monkeypatch.setenv("JP2HIP_TEST_POOL_FRAC", "0.02")
+    enc = jp2hip.Encoder(0)
+    monkeypatch.delenv("JP2HIP_TEST_POOL_FRAC")
+    try:
+        img = im.synth_rgb8(700, 900, seed=77)
+        rc = jp2hip.recipe(conversion)
+        want = ol.encode(img, ol.copy_recipe(rc))
+        got, st = enc.encode_tiff(im.tiff_bytes(img), conversion, rc)
+        assert got == want
+        assert st.pool_grows == 1
+        assert 0 < st.stream_need_bytes <= st.stream_pool_bytes
+        got2, st2 = enc.encode_tiff(im.tiff_bytes(img), conversion, rc)
+        assert got2 == want and st2.pool_grows == 0
+    finally:
+        enc.close()
+
+
+def test_stream_pool_is_sized_below_the_every_plane_bound(c2_tif):
+    """C2 lossy: the pool reserves half the every-plane bound and the coded
+    planes take less than that (slope prediction codes few planes)."""
+    enc = jp2hip.Encoder(0)
+    try:
+        _, st = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+        assert st.pool_grows == 0
+        assert st.stream_need_bytes < st.stream_pool_bytes
+        print(f"\nC2 pool {st.stream_pool_bytes} B, coded planes took {st.stream_need_bytes} B, "
+              f"context {enc.device_bytes()} B")
+    finally:
+        enc.close()
