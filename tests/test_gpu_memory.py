@@ -116,7 +116,7 @@ def test_short_stream_pool_regrows_and_matches_oracle(monkeypatch, conversion):
 
 
 def test_stream_pool_is_sized_below_the_every_plane_bound(c2_tif):
-    """C2 lossy: the pool reserves half the every-plane bound and the coded
+    """C2 lossy: the pool reserves 30 % of the every-plane bound and the coded
     planes take less than that (slope prediction codes few planes)."""
     enc = jp2hip.Encoder(0)
     try:
