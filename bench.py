@@ -801,6 +801,8 @@ def main():
                     res["lossless_c3"]["mp_per_s_inflight_c_api"] / res["cpu_baseline_lossless"]["value"], 2)
             res["cpu_not_a_reference"] = cpu_oracle_not_a_reference(img)
     if rank == 0:
+        import jp2hip
+        res["dma_engines"] = jp2hip._lib.dma_engines()  # engine choice differs per box: record it
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist

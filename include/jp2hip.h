@@ -179,6 +179,12 @@ int64_t jp2hip_device_bytes(jp2hip_ctx *ctx);
  * Returns 0, or < 0 for a null context. */
 int jp2hip_set_memory_limits(jp2hip_ctx *ctx, int64_t soft, int64_t hard);
 
+/* Which SDMA engines the code-stream copies use, per GPU probed so far, and
+ * every engine's measured device -> host rate ("" before the first encode):
+ * engines differ several-fold on MI355X and the choice is timed once per
+ * GPU, so a benchmark records it to be comparable with another run. */
+const char *jp2hip_dma_engines(void);
+
 /* Free and total memory of HIP device `device` (bytes): what a converter
  * sizes its context pool from.  Returns 0 or < 0. */
 int jp2hip_device_memory(int device, int64_t *free_bytes, int64_t *total_bytes);

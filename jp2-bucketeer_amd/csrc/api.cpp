@@ -1306,6 +1306,12 @@ int jp2hip_set_memory_limits(jp2hip_ctx *ctx, int64_t soft, int64_t hard) {
     return 0;
 }
 
+const char *jp2hip_dma_engines(void) {
+    thread_local std::string s;
+    s = jp2hip::dma_engine_report();
+    return s.c_str();
+}
+
 int jp2hip_device_memory(int device, int64_t *free_bytes, int64_t *total_bytes) {
     int prev = -1;
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;

@@ -49,6 +49,9 @@ uint64_t lzw_slices(const uint64_t *strip_bytes, int nstrips, std::vector<uint64
 size_t lzw_scratch_bytes(int nstrips, uint64_t segs);
 bool launch_lzw(const UnpackArgs &u, uint64_t segs, void *scratch, hipStream_t st);
 
+// the SDMA engines chosen per GPU and their probed rates (t2_device.hip)
+std::string dma_engine_report();
+
 // tier-1 kernels (t1.hip)
 #ifndef JP2HIP_ORDER_SUB
 #define JP2HIP_ORDER_SUB 16  // MQ lane-order buckets per octave of decision count

@@ -21,9 +21,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1051,10 +1054,16 @@ static hsa_status_t first_cpu_agent(hsa_agent_t a, void *out) {
 // the runtime's own pick -- at 30, engines 4-15 at 7-13), so the engines are
 // timed once per process and GPU on a 32 MiB copy, and the contexts spread
 // over the ones within 10 % of the fastest.
+struct DmaGpu {
+    std::mutex mu;            // this GPU's probe (other GPUs probe in parallel)
+    bool probed = false;
+    std::vector<int> fast;    // engine ids within 10 % of the fastest
+    std::vector<std::pair<int, double>> rates;  // (engine, GB/s) as probed
+    std::atomic<unsigned> next{0};               // round-robin cursor
+};
 struct DmaEngines {
-    std::mutex mu;
-    std::map<uint64_t, std::vector<int>> fast;  // GPU agent handle -> engine ids
-    std::map<uint64_t, int> next;               // round-robin cursor
+    std::mutex mu;  // the map only
+    std::map<uint64_t, std::unique_ptr<DmaGpu>> gpu;  // GPU agent handle -> its engines
 };
 static DmaEngines &dma_engines() {
     static DmaEngines *e = new DmaEngines();  // never destroyed: contexts may outlive static teardown
@@ -1063,49 +1072,77 @@ static DmaEngines &dma_engines() {
 
 static int pick_dma_engine(hsa_agent_t gpu, hsa_agent_t cpu, hsa_signal_t sig) {
     DmaEngines &E = dma_engines();
-    std::lock_guard<std::mutex> lk(E.mu);
-    auto it = E.fast.find(gpu.handle);
-    if (it == E.fast.end()) {
-        std::vector<int> fast;
-        uint32_t mask = 0;
-        const size_t n = 32u << 20;
-        void *d = nullptr, *h = nullptr;
-        if (hsa_amd_memory_copy_engine_status(cpu, gpu, &mask) == HSA_STATUS_SUCCESS && mask &&
-            hipMalloc(&d, n) == hipSuccess && hipHostMalloc(&h, n, hipHostMallocDefault) == hipSuccess) {
-            std::vector<std::pair<double, int>> rate;
-            for (int e = 0; e < 16; e++) {
-                if (!(mask & (1u << e))) continue;
-                double best = 0.0;
-                for (int r = 0; r < 2; r++) {  // the first copy also maps the pages
-                    hsa_signal_store_relaxed(sig, 1);
-                    const auto t0 = std::chrono::steady_clock::now();
-                    if (hsa_amd_memory_async_copy_on_engine(h, cpu, d, gpu, n, 0, nullptr, sig,
-                                                            (hsa_amd_sdma_engine_id_t)(1u << e), true) != HSA_STATUS_SUCCESS)
-                        break;
-                    // nothing else is queued: a probe copy that takes more
-                    // than a second is an engine to leave out
-                    std::string perr;
-                    if (!jp2hip::wait_bounded([&](uint64_t ns) { return poll_signal(sig, ns); },
-                                              [](std::string &) { return jp2hip::StreamState::Drained; }, mono_ns,
-                                              kWaitSliceNs, 1000ull * 1000 * 1000, "DMA engine probe", perr))
-                        break;
-                    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                    best = std::max(best, n / s);
-                }
-                if (best > 0.0) rate.emplace_back(best, e);
-            }
-            double top = 0.0;
-            for (auto &r : rate) top = std::max(top, r.first);
-            for (auto &r : rate)
-                if (r.first >= 0.9 * top) fast.push_back(r.second);
-        }
-        if (d) (void)hipFree(d);
-        if (h) (void)hipHostFree(h);
-        it = E.fast.emplace(gpu.handle, fast).first;  // empty: the runtime picks the engine
+    DmaGpu *G;
+    {
+        std::lock_guard<std::mutex> lk(E.mu);
+        std::unique_ptr<DmaGpu> &slot = E.gpu[gpu.handle];
+        if (!slot) slot.reset(new DmaGpu());
+        G = slot.get();
     }
-    if (it->second.empty()) return -1;
-    int &k = E.next[gpu.handle];
-    return it->second[(size_t)(k++) % it->second.size()];
+    {
+        std::lock_guard<std::mutex> lk(G->mu);  // the first context of this GPU probes; the others wait
+        if (!G->probed) {
+            uint32_t mask = 0;
+            const size_t n = 32u << 20;
+            void *d = nullptr, *h = nullptr;
+            if (hsa_amd_memory_copy_engine_status(cpu, gpu, &mask) == HSA_STATUS_SUCCESS && mask &&
+                hipMalloc(&d, n) == hipSuccess && hipHostMalloc(&h, n, hipHostMallocDefault) == hipSuccess) {
+                for (int e = 0; e < 16; e++) {
+                    if (!(mask & (1u << e))) continue;
+                    double best = 0.0;
+                    for (int r = 0; r < 2; r++) {  // the first copy also maps the pages
+                        hsa_signal_store_relaxed(sig, 1);
+                        const auto t0 = std::chrono::steady_clock::now();
+                        if (hsa_amd_memory_async_copy_on_engine(h, cpu, d, gpu, n, 0, nullptr, sig,
+                                                                (hsa_amd_sdma_engine_id_t)(1u << e), true) != HSA_STATUS_SUCCESS)
+                            break;
+                        // nothing else is queued: a probe copy that takes more
+                        // than a second is an engine to leave out
+                        std::string perr;
+                        if (!jp2hip::wait_bounded([&](uint64_t ns) { return poll_signal(sig, ns); },
+                                                  [](std::string &) { return jp2hip::StreamState::Drained; }, mono_ns,
+                                                  kWaitSliceNs, 1000ull * 1000 * 1000, "DMA engine probe", perr))
+                            break;
+                        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                        best = std::max(best, n / sec);
+                    }
+                    if (best > 0.0) G->rates.emplace_back(e, best / 1e9);
+                }
+                double top = 0.0;
+                for (auto &r : G->rates) top = std::max(top, r.second);
+                for (auto &r : G->rates)
+                    if (r.second >= 0.9 * top) G->fast.push_back(r.first);
+            }
+            if (d) (void)hipFree(d);
+            if (h) (void)hipHostFree(h);
+            G->probed = true;  // empty `fast`: the runtime picks the engine
+        }
+    }
+    if (G->fast.empty()) return -1;
+    return G->fast[(size_t)(G->next++) % G->fast.size()];
+}
+
+// "GPU agent <handle>: engines e,e,.. used of (e rate, ...)" per probed GPU
+std::string dma_engine_report() {
+    DmaEngines &E = dma_engines();
+    std::lock_guard<std::mutex> lk(E.mu);
+    std::string out;
+    char buf[64];
+    for (auto &kv : E.gpu) {
+        DmaGpu &G = *kv.second;
+        std::lock_guard<std::mutex> lg(G.mu);
+        if (!G.probed) continue;
+        if (!out.empty()) out += "; ";
+        out += "agent " + std::to_string(kv.first) + ": using";
+        for (int e : G.fast) out += " " + std::to_string(e);
+        if (G.fast.empty()) out += " the runtime's choice";
+        out += " of";
+        for (auto &r : G.rates) {
+            std::snprintf(buf, sizeof buf, " %d:%.1fGB/s", r.first, r.second);
+            out += buf;
+        }
+    }
+    return out;
 }
 
 bool GpuEncoder::dma_init(std::string &err) {

@@ -75,7 +75,7 @@ EXPORTS = ("jp2hip_version", "jp2hip_last_error", "jp2hip_probe", "jp2hip_device
            "jp2hip_split_rows", "jp2hip_encode_device_split", "jp2hip_split_thresholds",
            "jp2hip_split_peers", "jp2hip_tiff_pixels", "jp2hip_env_check",
            # device-memory policy (api.cpp)
-           "jp2hip_device_bytes", "jp2hip_set_memory_limits", "jp2hip_device_memory")
+           "jp2hip_device_bytes", "jp2hip_set_memory_limits", "jp2hip_device_memory", "jp2hip_dma_engines")
 
 
 # int (*)(void *user, int64_t *values, int32_t n): in-place sum over ranks, 0 ok
@@ -134,6 +134,7 @@ def lib():
     L.jp2hip_device_bytes.restype = c_int64
     L.jp2hip_set_memory_limits.argtypes = [c_void_p, c_int64, c_int64]
     L.jp2hip_device_memory.argtypes = [c_int, POINTER(c_int64), POINTER(c_int64)]
+    L.jp2hip_dma_engines.restype = c_char_p
     _lib = L
     return L
 
@@ -169,6 +170,11 @@ def env_check() -> str:
     """"" or what the process environment should change for the contexts
     alive in it (jp2hip_env_check: GPU_MAX_HW_QUEUES)."""
     return lib().jp2hip_env_check().decode()
+
+
+def dma_engines() -> str:
+    """The SDMA engines the code-stream copies use and their probed rates."""
+    return lib().jp2hip_dma_engines().decode()
 
 
 def device_memory(device: int) -> tuple[int, int]:
