@@ -485,3 +485,44 @@ def test_concurrent_callers(tmp_path):
     for i, a in enumerate(imgs):
         assert np.array_equal(im.decode_pillow(results[i]), a)
     conv.close()
+
+
+def test_concurrent_contexts_stay_byte_identical():
+    """Round 5's one unexplained mismatch was a batch-queue
+    file whose code-stream length differed while three contexts encoded at
+    once.  Guard against any state shared between contexts: four contexts
+    encode eight different images (both conversions, ragged sizes, two flush
+    stripes) in parallel threads, three rounds in shuffled orders, and every
+    file must equal the oracle's."""
+    import random
+    cases = []
+    for i in range(8):
+        img = im.synth_rgb8(300 + 97 * i, 420 - 23 * i + (700 if i % 3 == 0 else 0), seed=500 + i)
+        conv = jp2hip.LOSSLESS if i % 2 == 0 else jp2hip.LOSSY
+        rc = jp2hip.recipe(conv)
+        cases.append((im.tiff_bytes(img, rows_per_strip=16 + i), conv, rc, ol.encode(img, ol.copy_recipe(rc))))
+    encs = [jp2hip.Encoder(0) for _ in range(4)]
+    errors = []
+    try:
+        for rnd in range(3):
+            order = list(range(len(cases)))
+            random.Random(rnd).shuffle(order)
+
+            def work(k):
+                try:
+                    for j in order[k::4]:
+                        tif, conv, rc, want = cases[j]
+                        got, _ = encs[k].encode_tiff(tif, conv, rc)
+                        if got != want:
+                            errors.append((rnd, j, len(got), len(want)))
+                except Exception as e:  # noqa: BLE001 -- reported below
+                    errors.append(repr(e))
+            th = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        assert errors == []
+    finally:
+        for e in encs:
+            e.close()
