@@ -969,13 +969,18 @@ def lossless_c4(device, rows=10000, ndistinct=16, sweep=(8, 12, 16), sweep_rows=
     (the queue's default), plus a shorter sweep over the context count with
     each stage's busy fraction, which names the bound."""
     busy = {}
-    value, dt, res, read = c4_batch(device, rows=rows, ndistinct=ndistinct, contexts=12, busy=busy)
+    # 6 readers / 8 uploaders: with 4 uploaders (the queue's default) the
+    # upload stage -- JPX write, stub read-back, delete -- is the bound
+    # (busy 0.95-1.0; profiles/r06/c4_sweep.jsonl), with 8 the contexts are
+    value, dt, res, read = c4_batch(device, rows=rows, ndistinct=ndistinct, contexts=12, busy=busy,
+                                    reader_threads=6, uploader_threads=8)
     ok = [r for r in res if r["status"] == 0]
     peak_h2d = h2d_peak()
     sweep_res = []
     for c in sweep:
         b = {}
-        v, d, rr, rd = c4_batch(device, rows=sweep_rows, ndistinct=ndistinct, contexts=c, busy=b)
+        v, d, rr, rd = c4_batch(device, rows=sweep_rows, ndistinct=ndistinct, contexts=c, busy=b,
+                                reader_threads=6, uploader_threads=8)
         sweep_res.append({"contexts": c, "mp_per_s": round(v, 3), "seconds": round(d, 3),
                           "tiff_read_gb_per_s": round(rd / d / 1e9, 2),
                           "jpx_gb_per_s": round(sum(r["out_bytes"] for r in rr) / d / 1e9, 2), "busy": b})
@@ -984,7 +989,7 @@ def lossless_c4(device, rows=10000, ndistinct=16, sweep=(8, 12, 16), sweep_rows=
     return {"workload": f"C4: Bucketeer batch CSV of 5000x7000 RGB8 TIFFs ({ndistinct} distinct, seeds 0-"
                         f"{ndistinct - 1}) -> native per-GPU queue (disk read, lossless 5/3 encode, JPX write, "
                         "stub upload, delete)",
-            "rows": rows, "distinct_files": ndistinct, "contexts": 12,
+            "rows": rows, "distinct_files": ndistinct, "contexts": 12, "reader_threads": 6, "uploader_threads": 8,
             "page_cache": f"the {ndistinct} files are evicted before the timed region; rows after the first "
                           f"{ndistinct} re-read them from the page cache",
             "images_ok": len(ok), "mp_per_s": round(value, 3), "seconds": round(dt, 3),
@@ -1032,7 +1037,7 @@ def c2_file_span(device, images=1024, contexts=16, ndistinct=16):
                           "file read, H2D, encode, D2H, file write included"}
 
 
-def c3_file_span(device, images=24, contexts=8, ndistinct=4):
+def c3_file_span(device, images=64, contexts=8, ndistinct=4):
     """SURVEY.md 8(d)'s span for the production conversion at C3 size:
     10000x8000 RGB16 TIFF files (480 MB each) on disk -> lossless JPX files
     written, through the native per-GPU queue (reader threads, `contexts`
@@ -1047,8 +1052,8 @@ def c3_file_span(device, images=24, contexts=8, ndistinct=4):
     rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
     value, dt, res, read = c4_batch(device, rows=images, ndistinct=ndistinct, contexts=contexts,
                                     conversion=jp2hip.LOSSLESS, rcp=rc,
-                                    make=lambda i: im.synth_u16(8000, 10000, comps=3, seed=2 + i), reader_threads=4,
-                                    uploader_threads=4, shape=(8000, 10000), gen_threads=4, busy=busy)
+                                    make=lambda i: im.synth_u16(8000, 10000, comps=3, seed=2 + i), reader_threads=6,
+                                    uploader_threads=8, shape=(8000, 10000), gen_threads=4, busy=busy)
     ok = [r for r in res if r["status"] == 0]
     out = sum(r["out_bytes"] for r in ok)
     ph, pd = h2d_peak(), d2h_peak()
