@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "device_common.h"
 #include "gpu_encoder.h"
@@ -652,6 +653,11 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
 #define JP2HIP_STREAM_BAND 64
 #endif
 constexpr int kStreamBand = JP2HIP_STREAM_BAND;
+#ifndef JP2HIP_L1S_PF
+#define JP2HIP_L1S_PF 1  // row pairs fetched ahead (1, 2 or 3; 2 and 3 measured slower: profiles/r06/ab_l1s_prefetch.txt)
+#endif
+constexpr int kL1sPf = JP2HIP_L1S_PF;
+static_assert(kL1sPf >= 1 && kL1sPf <= 3, "JP2HIP_L1S_PF: 1..3");
 #ifndef JP2HIP_L1S_INTERIOR
 #define JP2HIP_L1S_INTERIOR 0  // A/B: the select-free interior lifting path
 #endif
@@ -706,12 +712,12 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         for (int c = 0; c < NC; c++)
 #pragma unroll
             for (int i = 0; i < NWIN; i++) w[j][c][i] = 0;
-    // raw (level-shifted) samples of the next row pair, fetched one
-    // iteration ahead so the loads are in flight during the lifting
-    int32_t pf[2][CPT][NC];
+    // raw (level-shifted) samples of the next kL1sPf row pairs, fetched
+    // ahead so the loads are in flight during the lifting of the rows before
+    // them: row r (counted from s-1) lives in slot r % (2 kL1sPf)
+    int32_t pf[2 * kL1sPf][CPT][NC];
     // raw sample bits only (a u8, or the u16 as stored): the level shift and
-    // byte order wait for place(), so nothing uses a load until the next
-    // iteration
+    // byte order wait for place(), so nothing uses a load until it is placed
     auto fetch = [&](int q) {  // the next row (s, s+1, ...) into pf[q]
         const int ncp = a.planar == 2 ? NC : 1;
         uint64_t ro[NC];
@@ -758,24 +764,31 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
             }
         }
     };
+    // rows s .. s + 2 kL1sPf - 2 ahead of the first iteration
     fetch(1);  // row s (iteration m = s takes rows s-1, s)
+#pragma unroll
+    for (int q = 2; q < 2 * kL1sPf; q++)
+        if (s + q - 1 < e) fetch(q);
     const int nlv = (H + 1) / 2;
     const bool q16 = a.qt.q16 != 0;
     const QLevel ql = qlevel(a.qt, 1);
     int bb = r0;  // first row of the batch being filled
     // iteration m (even): rows m-1, m arrive; the last iteration emits row r1-1
     const int m_last = ((r1 - 1 + NS - 1) + 1) & ~1;
-    for (int m = s; m <= m_last; m += 2) {
+    // (the loop body is instantiated once per slot pair, so the prefetch
+    // slots stay compile-time register indices)
+    auto body = [&](int m, auto sa_c) {
+        constexpr int SA = decltype(sa_c)::value, SB = SA + 1;
 #pragma unroll
         for (int j = 0; j < CPT; j++)
 #pragma unroll
             for (int c = 0; c < NC; c++)
 #pragma unroll
                 for (int i = 0; i + 2 < NWIN; i++) w[j][c][i] = w[j][c][i + 2];
-        if (m - 1 >= s && m - 1 < e) place(0, NWIN - 2);
-        if (m < e) place(1, NWIN - 1);
-        if (m + 1 < e) fetch(0);
-        if (m + 2 < e) fetch(1);
+        if (m - 1 >= s && m - 1 < e) place(SA, NWIN - 2);
+        if (m < e) place(SB, NWIN - 1);
+        if (m + 2 * kL1sPf - 1 < e) fetch(SA);
+        if (m + 2 * kL1sPf < e) fetch(SB);
         // interior iterations (every step's rows and neighbours inside the
         // streamed rows and the signal, none at row 0): fixed neighbour slots,
         // no per-value selects -- the same expressions in the same order
@@ -865,6 +878,11 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
             __syncthreads();
             bb += RB;
         }
+    };
+    for (int m = s; m <= m_last; m += 2) {
+        if (kL1sPf == 1 || (((m - s) >> 1) % kL1sPf) == 0) body(m, std::integral_constant<int, 0>{});
+        else if (kL1sPf >= 2 && (((m - s) >> 1) % kL1sPf) == 1) body(m, std::integral_constant<int, (kL1sPf >= 2 ? 2 : 0)>{});
+        else if (kL1sPf >= 3 && (((m - s) >> 1) % kL1sPf) == 2) body(m, std::integral_constant<int, (kL1sPf >= 3 ? 4 : 0)>{});
     }
 }
 
