@@ -231,6 +231,14 @@ constexpr int kPadL = 4;   // LDS words in front of row 0 (the first segment's l
 // mod 64 so consecutive rows start on different banks
 __host__ __device__ constexpr int lds_row_stride(int W) { return ((W + 63) & ~63) + 4; }
 constexpr int kPadR = 24;  // LDS words after the last row (the last segment's right halo)
+// Skewed staging layout (k_dwt_l1s): 4 words of padding after every 16
+// samples.  hlift_seg's lanes read 16-sample segments, 16 bytes at a time;
+// in the dense layout the 16 lanes of a ds_read_b128 group sit 16 words
+// apart, so only 4 distinct bank windows serve them (4-way conflicts); at 20
+// words apart every lane of the group has its own 4 banks.
+__host__ __device__ constexpr int skew_x(int x) { return x + ((x >> 4) << 2); }
+__host__ __device__ constexpr int lds_row_stride_skew(int W) { return ((W + 15) >> 4) * 20 + 4; }
+constexpr int kPadLs = 8;  // ... words in front of row 0: segment 0 reads 8 words before its samples
 
 // Where one staged row's outputs go: its low half raw to the next level's LL
 // row `ll` (a non-final level's even rows), or -- like its high half --
@@ -363,7 +371,7 @@ __device__ __forceinline__ void hlift_write(int32_t *lds, int W, int ld, bool q1
 // the 4-step footprint: the 16 kept samples are exact, as in lift_regs),
 // scaled and written de-interleaved as 8 low + 8 high words (two 16-byte
 // stores each when the row is aligned).  Rows as in hlift_write.
-template <bool REV, int NROWS, bool ALIGNED, int NT = kDwtThreads, typename RowFn>
+template <bool REV, int NROWS, bool ALIGNED, int NT = kDwtThreads, bool SKEW = false, typename RowFn>
 __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, bool q16, RowFn rows,
                                           int nrows = NROWS) {
     const int nseg = (W + 15) >> 4;
@@ -371,12 +379,21 @@ __device__ __forceinline__ void hlift_seg(const int32_t *lds, int W, int ld, boo
     for (int it = threadIdx.x; it < nrows * nseg; it += NT) {
         const int r = it / nseg, k = it - r * nseg;
         const int x0 = (k << 4) - 4;  // window: samples x0 .. x0+23 (even start)
-        const int4 *src = (const int4 *)(lds + kPadL + r * ld + x0);
         int32_t v[24];
+        if (SKEW) {  // segment k's samples at word 20 k: the halos are the neighbours' edges
+            const int32_t *rb = lds + kPadLs + r * ld + 20 * k;
 #pragma unroll
-        for (int q = 0; q < 6; q++) {
-            const int4 t = src[q];
-            v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+            for (int q = 0; q < 6; q++) {
+                const int4 t = *(const int4 *)(rb + (q == 0 ? -8 : (q == 5 ? 20 : 4 * (q - 1))));
+                v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+            }
+        } else {
+            const int4 *src = (const int4 *)(lds + kPadL + r * ld + x0);
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                const int4 t = src[q];
+                v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+            }
         }
         if (ALIGNED) {  // caller: W > 1 and a multiple of 16
             // W a multiple of 16 (every full tile): the signal ends fall on
@@ -653,6 +670,10 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1(DwtBandArgs a) {
 #define JP2HIP_STREAM_BAND 64
 #endif
 constexpr int kStreamBand = JP2HIP_STREAM_BAND;
+#ifndef JP2HIP_L1S_SKEW
+#define JP2HIP_L1S_SKEW 1  // the skewed staging layout (hlift_seg's reads conflict-free)
+#endif
+constexpr bool kL1sSkew = JP2HIP_L1S_SKEW != 0;
 #ifndef JP2HIP_L1S_PF
 #define JP2HIP_L1S_PF 1  // row pairs fetched ahead (1, 2 or 3; 2 and 3 measured slower: profiles/r06/ab_l1s_prefetch.txt)
 #endif
@@ -682,7 +703,8 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
     const int r1 = min(H, r0 + kStreamBand);
     const int s = max(0, r0 - NS), e = min(H, r1 + NS);  // rows streamed [s, e); s even
     const int tid = threadIdx.x;
-    const int ld = lds_row_stride(W);
+    const int ld = kL1sSkew ? lds_row_stride_skew(W) : lds_row_stride(W);
+    constexpr int kP = kL1sSkew ? kPadLs : kPadL;
     const int32_t off = 1 << (a.bits - 1);
     const int bps = a.bits >> 3;
     const size_t row_bytes = (size_t)a.img_w * (a.planar == 2 ? 1 : NC) * bps;
@@ -856,7 +878,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
                 for (int c = 0; c < NC; c++) {
                     int32_t v = w[j][c][1 + q];
                     if (!REV && H > 1) v = __float_as_int(__int_as_float(v) * (q ? K97 : INVK97));
-                    lds[kPadL + (c * RB + (y - bb)) * ld + x] = v;
+                    lds[kP + (c * RB + (y - bb)) * ld + (kL1sSkew ? skew_x(x) : x)] = v;
                 }
             }
         }
@@ -864,7 +886,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         if (ylast >= r0 && (ylast - bb == RB - 1 || ylast >= r1 - 1)) {
             __syncthreads();
             const int nkeep = min(RB, r1 - bb);
-            hlift_seg<REV, NC * RB, ALIGNED>(lds, W, ld, q16, [&](int r, QRow &o) -> bool {
+            hlift_seg<REV, NC * RB, ALIGNED, kDwtThreads, kL1sSkew>(lds, W, ld, q16, [&](int r, QRow &o) -> bool {
                 const int c = r / RB, k = r - c * RB;
                 if (k >= nkeep) return false;
                 const int tc = tc0 + c, y = bb + k;
@@ -1131,7 +1153,9 @@ bool launch_dwt(const DwtLaunch &p, hipStream_t st) {
             // streaming vertical pass (k_dwt_l1s), bands of kStreamBand rows,
             // horizontal batches of 4 rows
             a.R = JP2HIP_L1S_R;
-            const size_t lds_s = ((size_t)p.nc * a.R * lds_row_stride(maxW) + kPadL + kPadR) * 4;
+            const size_t lds_s =
+                ((size_t)p.nc * a.R * (kL1sSkew ? lds_row_stride_skew(maxW) : lds_row_stride(maxW)) +
+                 (kL1sSkew ? kPadLs : kPadL) + kPadR) * 4;
             dim3 g1((maxH + kStreamBand - 1) / kStreamBand, p.ntc / p.nc);
             if (p.reversible) launch_l1s<true>(p.nc, cpt, g1, lds_s, st, a);
             else launch_l1s<false>(p.nc, cpt, g1, lds_s, st, a);

@@ -311,7 +311,7 @@ class GpuEncoder {
     // decision-stream pool: the first encode of a geometry reserves this
     // fraction of the every-plane bound; pool_hint = what the last
     // overflowing encode needed (+12.5 %)
-    static constexpr double kPoolFracLossy = 0.3, kPoolFracLossless = 0.9;
+    static constexpr double kPoolFracLossy = 0.3, kPoolFracLossless = 0.7;
     uint64_t pool_hint = 0;
     int pool_grows = 0;
     double pool_frac_test = -1.0;  // JP2HIP_TEST_POOL_FRAC (tests: force the grow path)
