@@ -191,7 +191,11 @@ def _rank_main(rank, world, store_path, out_path, n):
     q = FakeQueue(contexts=2, speed=3.0 if rank == 1 else 1.0)  # rank 1's GPU is 3x faster
     try:
         dist.barrier()
-        res = jb.run_batch_dynamic(items, f"/tmp/ws_{os.getpid()}", [q], claims=jb.StoreClaims(store, n), depth=2)
+        # the process group's own store, as bench.py --workload c4 takes it
+        from torch.distributed import distributed_c10d as c10d
+        claims = jb.StoreClaims(c10d._get_default_store(), n)
+        out_dir = os.path.join(os.path.dirname(out_path), f"jpx{rank}")
+        res = jb.run_batch_dynamic(items, out_dir, [q], claims=claims, depth=2)
     finally:
         q.close()
     dist.barrier()
