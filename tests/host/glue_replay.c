@@ -139,6 +139,11 @@ int main(int argc, char **argv) {
         int32_t ord[64];
         const int ng = glue_device_ordinals(ord, 64);
         CHECK(ng >= 1, "probe said yes but no ordinals");
+        /* the default pool size (bucketeer.gpu.contexts = 0): from free memory */
+        const int k = glue_contexts_for_memory(ord[0], 0, GLUE_MAX_CONTEXTS_PER_GPU);
+        printf("contexts for memory %d\n", k);
+        CHECK(k >= 1 && k <= GLUE_MAX_CONTEXTS_PER_GPU, "pool size out of range");
+        CHECK(glue_contexts_for_memory(ord[0], (int64_t)1 << 50, 16) == 1, "a huge budget must still give 1");
         int64_t a = 0, b = 5;
         CHECK(glue_create(ord[0], 0, &a, err, sizeof err) == 0, "create on GPU %d: %s", ord[0], err);
         const int rc = glue_create(4096, 0, &b, err, sizeof err);

@@ -134,6 +134,7 @@ def test_glue_replay_on_gpu_under_asan(tmp_path, conversion):
     assert r.stdout.strip().endswith("REPLAY OK")
     assert "via split context: ok" in r.stdout and "via pooled context: ok" in r.stdout
     assert "create on ordinal 4096: rc -1" in r.stdout and "split_peers with ordinal 4096: rc -1" in r.stdout
+    assert "contexts for memory 16" in r.stdout  # an idle MI355X: 288 GB x 0.75 / 8 GiB > 16
     assert "AddressSanitizer" not in r.stderr
     import jp2hip
     for i, img in enumerate(imgs):
