@@ -170,12 +170,17 @@ int64_t jp2hip_device_bytes(jp2hip_ctx *ctx);
 
 /* A context's device-memory policy, its tile-split members' too.
  * soft: bytes it may keep between encodes; an encode that leaves it above
- *   releases every buffer at its end, so one outsized master does not pin
- *   HBM for the context's life (<= 0: 80 % of the device's memory divided by
- *   the contexts alive in the process).
+ *   releases every buffer at its end (<= 0, the default: relative to the
+ *   context's usual image -- it releases when it holds more than twice the
+ *   median of what its last 8 encodes needed, so one outsized master does
+ *   not pin HBM for the context's life while a steady run of large masters
+ *   keeps its buffers).
  * hard: bytes no encode may pass; an image that needs more fails with
  *   rc < 0 and a message (never a fault), and the context stays usable
  *   (<= 0: no limit but the device's).
+ * When the device itself runs out of memory, the allocating encode takes
+ * back the buffers of idle contexts of the same device and waits (up to
+ * 30 s) for busy ones to become idle before it fails.
  * Returns 0, or < 0 for a null context. */
 int jp2hip_set_memory_limits(jp2hip_ctx *ctx, int64_t soft, int64_t hard);
 

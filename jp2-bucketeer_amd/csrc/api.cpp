@@ -63,6 +63,8 @@ struct jp2hip_ctx {
     // device memory policy (jp2hip_set_memory_limits): 0 = default
     int64_t mem_soft = 0;
     size_t dev_total = 0;  // the device's memory (hipMemGetInfo at create)
+    std::vector<size_t> needs;  // what the last encodes asked for (the context's usual image)
+    int64_t reclaimed = 0;      // times another context took this one's idle buffers
     ~jp2hip_ctx() {
         for (jp2hip_ctx *p : peers) jp2hip_destroy(p);
     }
@@ -77,26 +79,41 @@ int fail(const std::string &msg) {
     return -1;
 }
 
-// Device-memory policy of a context (jp2hip_set_memory_limits): the soft
-// limit it may keep between encodes -- by default 80 % of the device's memory
-// shared by the contexts alive in the process -- and the hard limit no
-// encode may pass (default: none beyond the device's own).
-size_t soft_limit_of(jp2hip_ctx *ctx);
-
 // Every encode ends here, success or not: a failed one drains the stream
-// first (no buffer is released while a kernel may still read it), then a
-// context left above its soft limit by an outsized image releases its
-// buffers, so one C5-class master does not pin tens of GB for the rest of
-// the context's life.
+// first (no buffer is released while a kernel may still read it), then the
+// context's device-memory policy decides whether it keeps its buffers.
+//  - an explicit soft limit (jp2hip_set_memory_limits): release everything
+//    when the context holds more;
+//  - by default, relative to the context's usual image: release everything
+//    when it holds more than twice the median of what its last 8 encodes
+//    needed (plus 256 MiB) -- one C5-class master in a pool of C2 / C4 work
+//    is released right after it, while a steady run of large masters (C3
+//    every time) keeps its buffers instead of reallocating per image.
+// Memory pressure between contexts is handled where it arises: an
+// allocation that fails takes back what idle contexts of the device hold
+// (reclaim_idle).
 struct EncodeEnd {
     jp2hip_ctx *ctx;
     bool ok = false;
     ~EncodeEnd() {
         if (!ok) ctx->gpu.quiesce();
-        const size_t soft = soft_limit_of(ctx);
-        if (ctx->gpu.device_bytes() > soft) {
+        const size_t need = ctx->gpu.need_bytes();
+        if (ok && need) {
+            ctx->needs.push_back(need);
+            if (ctx->needs.size() > 8) ctx->needs.erase(ctx->needs.begin());
+        }
+        size_t limit;
+        if (ctx->mem_soft > 0) {
+            limit = (size_t)ctx->mem_soft;
+        } else {
+            if (ctx->needs.empty()) return;
+            std::vector<size_t> v = ctx->needs;
+            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            limit = 2 * v[v.size() / 2] + ((size_t)256 << 20);
+        }
+        if (ctx->gpu.device_bytes() > limit) {
             ctx->gpu.quiesce();
-            ctx->gpu.trim(soft);
+            ctx->gpu.trim(limit);
         }
     }
 };
@@ -572,6 +589,7 @@ int encode_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const jp2hip
     const jp2hip_recipe rc = recipe_of(recipe, conversion);
     if (!lay || !d_src) return fail("null source or layout");
     ctx->gpu.take_waits();  // count this encode's host waits (stats)
+    ctx->gpu.begin_encode();
     EncodeEnd end{ctx};
     std::string err;
     jp2hip_layout ulay;
@@ -714,6 +732,7 @@ int encode_split_core(jp2hip_ctx *ctx, const void *d_src, size_t src_len, const 
     const jp2hip_recipe rc = recipe_of(recipe, conversion);
     if (!lay || !d_src) return fail("null source or layout");
     ctx->gpu.take_waits();
+    ctx->gpu.begin_encode();
     EncodeEnd end{ctx};
     Plan full;
     std::string err;
@@ -1226,13 +1245,26 @@ void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
 // Contexts alive in this process, for jp2hip_env_check.
 static std::atomic<int> g_live_contexts{0};
 
-namespace {
-size_t soft_limit_of(jp2hip_ctx *ctx) {
-    if (ctx->mem_soft > 0) return (size_t)ctx->mem_soft;
-    const int live = std::max(1, g_live_contexts.load());
-    return (size_t)((double)ctx->dev_total * 0.8 / live);
+// Every context alive in the process, by device: an allocation that fails
+// for lack of device memory takes back the buffers of idle contexts of its
+// device (GpuEncoder::reclaim -> reclaim_idle).  A context is idle when its
+// lock is free (no encode in it); its buffers are rebuilt by its next encode.
+static std::mutex g_reg_mu;
+static std::vector<jp2hip_ctx *> g_reg;
+
+static bool reclaim_idle(jp2hip_ctx *self) {
+    bool freed = false;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (jp2hip_ctx *c : g_reg) {
+        if (c == self || c->cfg.device != self->cfg.device) continue;
+        std::unique_lock<std::mutex> cl(c->mu, std::try_to_lock);
+        if (!cl.owns_lock() || c->gpu.device_bytes() == 0) continue;
+        c->gpu.quiesce();
+        freed = c->gpu.trim(0) || freed;
+        c->reclaimed++;
+    }
+    return freed;
 }
-}  // namespace
 
 const char *jp2hip_env_check(void) {
     thread_local std::string msg;
@@ -1280,6 +1312,11 @@ int jp2hip_create(jp2hip_ctx **out, const jp2hip_config *cfg) {
     }
     size_t fr = 0, tot = 0;
     c->dev_total = hipMemGetInfo(&fr, &tot) == hipSuccess ? tot : 0;  // (init selected the device)
+    c->gpu.reclaim = [c] { return reclaim_idle(c); };
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.push_back(c);
+    }
     *out = c;
     g_live_contexts++;
     return 0;
@@ -1327,6 +1364,10 @@ int jp2hip_device_memory(int device, int64_t *free_bytes, int64_t *total_bytes) 
 
 void jp2hip_destroy(jp2hip_ctx *ctx) {
     if (!ctx) return;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.erase(std::remove(g_reg.begin(), g_reg.end(), ctx), g_reg.end());
+    }
     g_live_contexts--;  // its peers count themselves down as they go
     delete ctx;
 }

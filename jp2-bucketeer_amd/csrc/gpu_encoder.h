@@ -5,9 +5,11 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <chrono>
 #include <cstdint>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "jp2hip_internal.h"
@@ -17,6 +19,7 @@ namespace jp2hip {
 struct DevBuf {
     void *ptr = nullptr;
     size_t bytes = 0;
+    size_t want = 0;  // bytes the current encode asked for (need accounting)
 };
 
 struct StageTimes {
@@ -160,6 +163,20 @@ class GpuEncoder {
     // releases every device buffer if more than `soft` bytes are held (the
     // stream must be idle: called after an encode's last wait); true if it did
     bool trim(size_t soft);
+    // need accounting: begin_encode() clears every buffer's request, and
+    // need_bytes() is what this encode asked for (held may be more: buffers
+    // keep the size of the largest image since the last trim)
+    void begin_encode() {
+        for (DevBuf *b : bufs()) b->want = 0;
+    }
+    size_t need_bytes() {
+        size_t n = 0;
+        for (DevBuf *b : bufs()) n += b->want;
+        return n;
+    }
+    // called when hipMalloc fails: frees what other, idle contexts of the
+    // device hold (api.cpp); true if anything was released
+    std::function<bool()> reclaim;
     // waits for the stream, ignoring its errors (failure paths: no buffer is
     // released or reused while kernels may still read it)
     void quiesce();
@@ -308,6 +325,11 @@ class GpuEncoder {
     std::vector<uint64_t> strips_host;  // strip offsets last uploaded to `strips`
     const void *strips_dev = nullptr;
     size_t held = 0, mem_soft = SIZE_MAX, mem_hard = SIZE_MAX;
+    static constexpr int kReclaimWaitMs = 30000;
+    // hipMalloc, or hipErrorOutOfMemory past JP2HIP_TEST_DEVICE_BYTES held by
+    // every context of the process together (tests: a small device)
+    hipError_t device_alloc(void **p, size_t n);
+    void device_free(DevBuf &b);
     // decision-stream pool: the first encode of a geometry reserves this
     // fraction of the every-plane bound; pool_hint = what the last
     // overflowing encode needed (+12.5 %)
@@ -324,18 +346,29 @@ bool GpuEncoder::ensure(DevBuf &b, size_t count, std::string &err) {
     size_t bytes = count * sizeof(T);
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return true;
+    if (bytes > b.want) b.want = bytes;
     const size_t alloc = bytes + bytes / 8;
     if (held - b.bytes + alloc > mem_hard) {
         err = "device memory limit: this image needs a " + std::to_string(alloc) + "-byte buffer, the context holds " +
               std::to_string(held) + " of its " + std::to_string(mem_hard) + " bytes";
         return false;
     }
-    if (b.ptr) (void)hipFree(b.ptr);
-    held -= b.bytes;
-    b.ptr = nullptr;
-    b.bytes = 0;
-    const hipError_t e = hipMalloc(&b.ptr, alloc);
+    device_free(b);
+    hipError_t e = device_alloc(&b.ptr, alloc);
+    // out of device memory: other contexts of this device that are idle give
+    // their buffers back (they reallocate at their next encode), and an
+    // encode in progress elsewhere is waited for -- up to kReclaimWaitMs --
+    // before this encode fails
+    for (int waited = 0; e == hipErrorOutOfMemory && reclaim && waited <= kReclaimWaitMs;) {
+        (void)hipGetLastError();
+        if (!reclaim()) {
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+            waited += 5;
+        }
+        e = device_alloc(&b.ptr, alloc);
+    }
     if (e != hipSuccess) {
+        (void)hipGetLastError();
         b.ptr = nullptr;
         err = std::string("hipMalloc(") + std::to_string(alloc) + "): " + hipGetErrorString(e);
         return false;

@@ -1829,13 +1829,44 @@ std::vector<DevBuf *> GpuEncoder::bufs() {
             &t1fill, &dbgsel, &grptab, &gtot};
 }
 
+// test-only model of a small device: every context's buffers together may
+// not pass JP2HIP_TEST_DEVICE_BYTES (0 / unset: the device's own memory)
+static std::atomic<long long> g_test_held{0};
+static long long test_device_bytes() {
+    static const long long v = [] {
+        const char *s = getenv("JP2HIP_TEST_DEVICE_BYTES");
+        return s ? atoll(s) : 0ll;
+    }();
+    return v;
+}
+
+hipError_t GpuEncoder::device_alloc(void **p, size_t n) {
+    const long long cap = test_device_bytes();
+    if (cap > 0) {
+        if (g_test_held.fetch_add((long long)n) + (long long)n > cap) {
+            g_test_held.fetch_sub((long long)n);
+            return hipErrorOutOfMemory;
+        }
+        const hipError_t e = hipMalloc(p, n);
+        if (e != hipSuccess) g_test_held.fetch_sub((long long)n);
+        return e;
+    }
+    return hipMalloc(p, n);
+}
+
+void GpuEncoder::device_free(DevBuf &b) {
+    if (b.ptr) {
+        (void)hipFree(b.ptr);
+        if (test_device_bytes() > 0) g_test_held.fetch_sub((long long)b.bytes);
+    }
+    held -= b.bytes;
+    b.ptr = nullptr;
+    b.bytes = 0;
+}
+
 bool GpuEncoder::trim(size_t soft) {
     if (held <= soft) return false;
-    for (DevBuf *b : bufs()) {
-        if (b->ptr) (void)hipFree(b->ptr);
-        b->ptr = nullptr;
-        b->bytes = 0;
-    }
+    for (DevBuf *b : bufs()) device_free(*b);
     held = 0;
     // the device copies of the plan's tables went with the buffers
     front_gen = 0;
@@ -1862,8 +1893,7 @@ void GpuEncoder::quiesce() {
 }
 
 GpuEncoder::~GpuEncoder() {
-    for (DevBuf *b : bufs())
-        if (b->ptr) (void)hipFree(b->ptr);
+    for (DevBuf *b : bufs()) device_free(*b);
     if (sync_ev) (void)hipEventDestroy(sync_ev);
     if (stg_ev) (void)hipEventDestroy(stg_ev);
     for (const PinnedChunk &c : stg) (void)hipHostFree(c.p);

@@ -127,3 +127,76 @@ def test_stream_pool_is_sized_below_the_every_plane_bound(c2_tif):
               f"context {enc.device_bytes()} B")
     finally:
         enc.close()
+
+
+def test_relative_release_policy(c2_tif, c3_class_tif):
+    """Default policy (no explicit soft limit): a context keeps its buffers
+    through a steady run of large masters, and releases them right after an
+    image far larger than its usual work (twice the median of its last 8
+    encodes' needs)."""
+    rc3 = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
+    enc = jp2hip.Encoder(0)
+    try:
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        b1 = enc.device_bytes()
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        assert enc.device_bytes() == b1 > 0  # steady: nothing released, nothing reallocated
+    finally:
+        enc.close()
+    enc = jp2hip.Encoder(0)
+    try:
+        want = None
+        for _ in range(3):
+            got, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+            want = want or got
+        b_c2 = enc.device_bytes()
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        assert enc.device_bytes() == 0  # outsized against its usual C2: released
+        got, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
+        assert got == want and enc.device_bytes() == b_c2
+    finally:
+        enc.close()
+
+
+RECLAIM_SCRIPT = r"""
+import os, sys, json
+sys.path.insert(0, os.path.join(os.environ["ROOT"], "jp2-bucketeer_amd"))
+sys.path.insert(0, os.path.join(os.environ["ROOT"], "tests"))
+import imaging as im, jp2hip, oracle_lib as ol
+img = im.synth_rgb8(1500, 2000, seed=91)
+tif = im.tiff_bytes(img)
+rc = jp2hip.recipe(jp2hip.LOSSLESS)
+want = ol.encode(img, ol.copy_recipe(rc))
+encs = [jp2hip.Encoder(0) for _ in range(3)]
+out = []
+for e in encs:  # one after another: the device holds about two contexts' worth
+    got, _ = e.encode_tiff(tif, jp2hip.LOSSLESS, rc)
+    out.append({"equal": got == want, "bytes": [x.device_bytes() for x in encs]})
+print(json.dumps(out))
+"""
+
+
+def test_out_of_device_memory_reclaims_idle_contexts(tmp_path):
+    """A device that holds about two contexts' buffers (modelled with
+    JP2HIP_TEST_DEVICE_BYTES, a separate process): three contexts encode
+    one after another; the third's allocations fail, take back the idle
+    contexts' buffers, and its file is still the oracle's."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = jp2hip.Encoder(0)
+    try:
+        probe.encode_tiff(im.tiff_bytes(im.synth_rgb8(1500, 2000, seed=91)), jp2hip.LOSSLESS)
+        one = probe.device_bytes()
+    finally:
+        probe.close()
+    env = dict(os.environ, ROOT=root, JP2HIP_TEST_DEVICE_BYTES=str(int(one * 2.3)))
+    r = subprocess.run([sys.executable, "-c", RECLAIM_SCRIPT], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(o["equal"] for o in out)
+    assert out[1]["bytes"][0] > 0 and out[1]["bytes"][1] > 0  # two fit
+    last = out[2]["bytes"]
+    assert last[2] > 0 and (last[0] == 0 or last[1] == 0)  # the third took an idle one's buffers
