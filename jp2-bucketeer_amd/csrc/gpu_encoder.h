@@ -345,8 +345,8 @@ template <typename T>
 bool GpuEncoder::ensure(DevBuf &b, size_t count, std::string &err) {
     size_t bytes = count * sizeof(T);
     if (bytes == 0) bytes = 16;
+    if (bytes > b.want) b.want = bytes;  // (also when the buffer is big enough already)
     if (b.bytes >= bytes) return true;
-    if (bytes > b.want) b.want = bytes;
     const size_t alloc = bytes + bytes / 8;
     if (held - b.bytes + alloc > mem_hard) {
         err = "device memory limit: this image needs a " + std::to_string(alloc) + "-byte buffer, the context holds " +
