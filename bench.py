@@ -523,6 +523,8 @@ def run(args):
             "t1": {"codeblocks": int(avg["codeblocks"]), "coded_passes": int(avg["coded_passes"]),
                    "mq_bytes": int(avg["t1_bytes"]), "mq_decisions": int(avg["mq_decisions"])},
         }
+    for e in encs[1:]:  # their HBM and streams back before the lossless legs
+        e.close()
     return res, img, world, rank, encs[0]
 
 
@@ -809,7 +811,7 @@ def main():
         dist.destroy_process_group()
 
 
-def lossless_c3(enc, steps=2, inflight=8, n_each=4):
+def lossless_c3(enc, steps=2, inflight=12, n_each=4):
     """C3 (configs[2]): 10000x8000 RGB16 lossless 5/3, 1024^2 tiles, the
     conversion the reference's service runs (ImageWorkerVerticle.java:64).
     One image alone (latency at the C call) and `inflight` images at once on
