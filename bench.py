@@ -627,12 +627,17 @@ def run_c4(args):
             dt = time.perf_counter() - t0
         ok = sum(1 for r in res if r["status"] == 0)
         mp = 5000 * 7000 / 1e6 * ok
+        rows_by_rank = [ok]
         if world > 1:
             import torch
             t = torch.tensor([dt, mp], dtype=torch.float64)
             dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
             dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
             dt, mp = float(t[0]), float(t[1])
+            per = torch.zeros(world, dtype=torch.int64)
+            per[rank] = ok
+            dist.all_reduce(per, op=dist.ReduceOp.SUM)  # (bookkeeping after the timed region)
+            rows_by_rank = [int(x) for x in per]
             dist.destroy_process_group()
         if rank != 0:
             return None
@@ -643,7 +648,8 @@ def run_c4(args):
                         "disk, evicted from the page cache before the timed region",
                 "config": {"workload": "C4: Bucketeer batch CSV -> per-GPU native queue (read, lossless 5/3 encode, "
                                        "JPX write, stub upload, delete-after-upload), Kakadu recipe",
-                           "rows_per_gpu": rows, "images_ok": ok, "parallelism": f"work stealing x{world}",
+                           "rows_per_gpu": rows, "images_ok": sum(rows_by_rank), "rows_by_rank": rows_by_rank,
+                           "parallelism": f"work stealing x{world}",
                            "ranks_in_process_group": world}}
     finally:
         shutil.rmtree(work, ignore_errors=True)
