@@ -614,7 +614,7 @@ def run_c4(args):
             claims = jb.StoreClaims(c10d._get_default_store(), len(items), key="jp2hip/c4/next")
         out_dir = os.path.join(work, "out")
         os.makedirs(out_dir, exist_ok=True)
-        with jb.BatchQueue(device=local) as q:
+        with jb.BatchQueue(device=local, reader_threads=6, uploader_threads=8) as q:
             # warm-up: one image per context, so device buffers exist
             for k, it in enumerate(items[:12]):
                 q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k))
