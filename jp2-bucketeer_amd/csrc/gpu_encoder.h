@@ -359,12 +359,11 @@ bool GpuEncoder::ensure(DevBuf &b, size_t count, std::string &err) {
     // their buffers back (they reallocate at their next encode), and an
     // encode in progress elsewhere is waited for -- up to kReclaimWaitMs --
     // before this encode fails
-    for (int waited = 0; e == hipErrorOutOfMemory && reclaim && waited <= kReclaimWaitMs;) {
+    // (every round counts 5 ms against the wait, freed or not, so two
+    // contexts taking memory from each other cannot loop for ever)
+    for (int waited = 0; e == hipErrorOutOfMemory && reclaim && waited <= kReclaimWaitMs; waited += 5) {
         (void)hipGetLastError();
-        if (!reclaim()) {
-            std::this_thread::sleep_for(std::chrono::milliseconds(5));
-            waited += 5;
-        }
+        if (!reclaim()) std::this_thread::sleep_for(std::chrono::milliseconds(5));
         e = device_alloc(&b.ptr, alloc);
     }
     if (e != hipSuccess) {
