@@ -32,6 +32,7 @@
 #include "gpu_encoder.h"
 #include "jp2hip.h"
 #include "jp2hip_internal.h"
+#include "mem_policy.h"
 
 // The last geometry's plan, tier-2 tables and main-header length: a batch of
 // same-size images (the common case) builds them once (C2: ~5 ms of host
@@ -97,20 +98,8 @@ struct EncodeEnd {
     bool ok = false;
     ~EncodeEnd() {
         if (!ok) ctx->gpu.quiesce();
-        const size_t need = ctx->gpu.need_bytes();
-        if (ok && need) {
-            ctx->needs.push_back(need);
-            if (ctx->needs.size() > 8) ctx->needs.erase(ctx->needs.begin());
-        }
-        size_t limit;
-        if (ctx->mem_soft > 0) {
-            limit = (size_t)ctx->mem_soft;
-        } else {
-            if (ctx->needs.empty()) return;
-            std::vector<size_t> v = ctx->needs;
-            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-            limit = 2 * v[v.size() / 2] + ((size_t)256 << 20);
-        }
+        if (ok) jp2hip::record_need(ctx->needs, ctx->gpu.need_bytes());
+        const size_t limit = jp2hip::keep_limit(ctx->needs, ctx->mem_soft);  // (mem_policy.h)
         if (ctx->gpu.device_bytes() > limit) {
             ctx->gpu.quiesce();
             ctx->gpu.trim(limit);

@@ -1,0 +1,33 @@
+// A context's device-memory decisions, as pure functions (api.cpp EncodeEnd
+// uses them; tests/host/test_mem_policy.cpp checks them on the CPU).
+#pragma once
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace jp2hip {
+
+constexpr size_t kNeedHistory = 8;                   // encodes the usual image is taken over
+constexpr size_t kReleaseSlack = (size_t)256 << 20;  // bytes above twice the usual
+
+// Record what one encode needed (the last kNeedHistory are kept).
+inline void record_need(std::vector<size_t> &needs, size_t need) {
+    if (!need) return;
+    needs.push_back(need);
+    if (needs.size() > kNeedHistory) needs.erase(needs.begin());
+}
+
+// The bytes a context may keep after an encode: the explicit soft limit if
+// one is set (> 0), else twice the median of the recent needs plus
+// kReleaseSlack; SIZE_MAX when there is nothing to go by.
+inline size_t keep_limit(const std::vector<size_t> &needs, int64_t soft) {
+    if (soft > 0) return (size_t)soft;
+    if (needs.empty()) return SIZE_MAX;
+    std::vector<size_t> v = needs;
+    std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+    return 2 * v[v.size() / 2] + kReleaseSlack;
+}
+
+}  // namespace jp2hip

@@ -88,10 +88,10 @@ def idle_gaps(trace, nq, n_items, min_gap):
     out = []
     held = [0] * nq
     submitted = 0
-    empty_since = [0.0] * nq
+    empty_since = [None] * nq  # the initial fill is not a gap: a queue counts once it has drained
     for t, q, ev, _ in sorted(trace, key=lambda e: (e[0], e[2] != "done")):
         if ev == "submit":
-            if held[q] == 0 and submitted < n_items and t - empty_since[q] > min_gap and submitted > 0:
+            if held[q] == 0 and empty_since[q] is not None and t - empty_since[q] > min_gap:
                 out.append((q, empty_since[q], t))
             held[q] += 1
             submitted += 1
