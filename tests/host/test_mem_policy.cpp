@@ -28,6 +28,14 @@ int main() {
     for (int i = 0; i < 3; i++) record_need(needs, 2 * GB);
     record_need(needs, 42 * GB);
     CHECK(keep_limit(needs, 0) == 4 * GB + kReleaseSlack);
+    // a second one in a row is kept: a lasting shift costs one release
+    record_need(needs, 42 * GB);
+    CHECK(keep_limit(needs, 0) == 84 * GB + kReleaseSlack);
+    // back to the small images: kept for one more encode, released after two
+    record_need(needs, 2 * GB);
+    CHECK(keep_limit(needs, 0) == 84 * GB + kReleaseSlack);
+    record_need(needs, 2 * GB);
+    CHECK(keep_limit(needs, 0) == 4 * GB + kReleaseSlack);
     // the history keeps the last 8 only: after 8 masters the pool is theirs
     for (int i = 0; i < 8; i++) record_need(needs, 42 * GB);
     CHECK(needs.size() == kNeedHistory);
@@ -35,8 +43,8 @@ int main() {
     // half small, half large: the median is the upper middle, large kept
     needs.clear();
     for (int i = 0; i < 4; i++) {
-        record_need(needs, 2 * GB);
         record_need(needs, 17 * GB);
+        record_need(needs, 2 * GB);
     }
     CHECK(keep_limit(needs, 0) == 34 * GB + kReleaseSlack);
     if (failures) return 1;

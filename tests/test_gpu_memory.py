@@ -132,8 +132,9 @@ def test_stream_pool_is_sized_below_the_every_plane_bound(c2_tif):
 def test_relative_release_policy(c2_tif, c3_class_tif):
     """Default policy (no explicit soft limit): a context keeps its buffers
     through a steady run of large masters, and releases them right after an
-    image far larger than its usual work (twice the median of its last 8
-    encodes' needs)."""
+    image far larger than its usual work (twice the larger of the median of
+    its last 8 encodes' needs and the previous encode's), and keeps them from
+    the second such image on (a lasting shift costs one release)."""
     rc3 = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
     enc = jp2hip.Encoder(0)
     try:
@@ -154,6 +155,13 @@ def test_relative_release_policy(c2_tif, c3_class_tif):
         assert enc.device_bytes() == 0  # outsized against its usual C2: released
         got, _ = enc.encode_tiff(c2_tif, jp2hip.LOSSY)
         assert got == want and enc.device_bytes() == b_c2
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        assert enc.device_bytes() == 0  # the previous encode was a C2: released again
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        b3 = enc.device_bytes()
+        assert b3 > b_c2  # two in a row: kept
+        enc.encode_tiff(c3_class_tif, jp2hip.LOSSLESS, rc3)
+        assert enc.device_bytes() == b3
     finally:
         enc.close()
 
