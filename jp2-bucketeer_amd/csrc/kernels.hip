@@ -2219,8 +2219,11 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         HIPCHECK(hipMemsetAsync(t2sum.ptr, 0, sizeof(T2Summary), stream));  // (k_hull's totals: none)
     }
 
-    HIPCHECK(hipEventRecord(ev[0], stream));
-    HIPCHECK(hipEventRecord(ev[1], stream));
+    // the first stage's arguments are prepared before its events: on an idle
+    // stream the GPU waits from the event to the first launch, so host work
+    // placed there was timed as DWT (≈80 us of a 310 us C2 stage alone,
+    // against 232 us of DWT kernels in the rocprofv3 trace of the same run,
+    // profiles/r06/dwt_stage_events.txt)
     // every stage's device buffer written to files: a debug build only
     // (make JP2HIP_DEBUG=1), for the tools in tests/tools
 #ifdef JP2HIP_DEBUG_DUMPS
@@ -2230,29 +2233,26 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
 #endif
     // the final coefficients are written as quantisation indices
     const QuantTab qt = quant_tab(plan.rc, plan.bits);
+    IngestArgs ing;
+    DwtLaunch dl;
     if (plan.rc.levels == 0) {
         // S1+S2 only: no decomposition
-        IngestArgs ia;
-        ia.src = (const uint8_t *)d_src;
-        ia.strip_off = (const uint64_t *)strips.ptr;
-        ia.rps = lay.rows_per_strip;
-        ia.w = plan.w; ia.h = plan.band_h; ia.nc = plan.nc; ia.bits = plan.bits;
-        ia.row0 = plan.row0;
-        ia.planar = lay.planar; ia.big_endian = lay.big_endian;
-        ia.mct = plan.rc.mct; ia.reversible = plan.rc.reversible;
-        ia.ntx = plan.ntx; ia.tile_w = plan.rc.tile_w; ia.tile_h = plan.rc.tile_h;
-        ia.plane_w = plan.plane_w; ia.plane_h = plan.plane_h;
-        ia.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
-        ia.coef = coef.ptr;
-        ia.inv = qt.inv[0][0]; ia.lim = qt.lim[0][0]; ia.q16 = qt.q16;
-        dim3 gi((plan.w + 63) / 64, (plan.band_h + 3) / 4);
-        hipLaunchKernelGGL(k_ingest, gi, dim3(256), 0, stream, ia);
-        HIPCHECK(hipGetLastError());
+        ing.src = (const uint8_t *)d_src;
+        ing.strip_off = (const uint64_t *)strips.ptr;
+        ing.rps = lay.rows_per_strip;
+        ing.w = plan.w; ing.h = plan.band_h; ing.nc = plan.nc; ing.bits = plan.bits;
+        ing.row0 = plan.row0;
+        ing.planar = lay.planar; ing.big_endian = lay.big_endian;
+        ing.mct = plan.rc.mct; ing.reversible = plan.rc.reversible;
+        ing.ntx = plan.ntx; ing.tile_w = plan.rc.tile_w; ing.tile_h = plan.rc.tile_h;
+        ing.plane_w = plan.plane_w; ing.plane_h = plan.plane_h;
+        ing.spp_strips = (plan.h + lay.rows_per_strip - 1) / lay.rows_per_strip;
+        ing.coef = coef.ptr;
+        ing.inv = qt.inv[0][0]; ing.lim = qt.lim[0][0]; ing.q16 = qt.q16;
     } else {
         // S1+S2+S3 fused: ingest inside DWT level 1 (dwt.hip)
         const size_t llw = (size_t)((plan.plane_w + 1) / 2) * ((plan.plane_h + 1) / 2) * plan.ntc;
         if (!ensure<int32_t>(llbuf0, llw, err) || !ensure<int32_t>(llbuf1, llw, err)) return false;
-        DwtLaunch dl;
         dl.tif = d_src;
         dl.strip_off = (const uint64_t *)strips.ptr;
         dl.rps = lay.rows_per_strip;
@@ -2266,6 +2266,14 @@ bool GpuEncoder::run_front(const void *d_src, const jp2hip_layout &lay, const Pl
         dl.tc_w = (const int32_t *)tcw.ptr; dl.tc_h = (const int32_t *)tch.ptr;
         dl.coef = coef.ptr; dl.scratch0 = llbuf0.ptr; dl.scratch1 = llbuf1.ptr;
         dl.qt = qt;
+    }
+    HIPCHECK(hipEventRecord(ev[0], stream));
+    HIPCHECK(hipEventRecord(ev[1], stream));
+    if (plan.rc.levels == 0) {
+        dim3 gi((plan.w + 63) / 64, (plan.band_h + 3) / 4);
+        hipLaunchKernelGGL(k_ingest, gi, dim3(256), 0, stream, ing);
+        HIPCHECK(hipGetLastError());
+    } else {
         bool dwt_ok = true;
         REPEAT_IF(1) dwt_ok = dwt_ok && launch_dwt(dl, stream);
         if (!dwt_ok) {
