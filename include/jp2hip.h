@@ -172,9 +172,11 @@ int64_t jp2hip_device_bytes(jp2hip_ctx *ctx);
  * soft: bytes it may keep between encodes; an encode that leaves it above
  *   releases every buffer at its end (<= 0, the default: relative to the
  *   context's usual image -- it releases when it holds more than twice the
- *   median of what its last 8 encodes needed, so one outsized master does
- *   not pin HBM for the context's life while a steady run of large masters
- *   keeps its buffers).
+ *   larger of the median of what its last 8 encodes needed and what the
+ *   encode before this one needed, plus 256 MiB, so one outsized master
+ *   does not pin HBM for the context's life, a steady run of large masters
+ *   keeps its buffers, and a lasting change to larger images costs one
+ *   release).
  * hard: bytes no encode may pass; an image that needs more fails with
  *   rc < 0 and a message (never a fault), and the context stays usable
  *   (<= 0: no limit but the device's).
