@@ -107,17 +107,33 @@ struct EncodeEnd {
     }
 };
 
+// Contexts alive in this process (jp2hip_env_check, the pinned pool's cap).
+static std::atomic<int> g_live_contexts{0};
+
 // Encoded files are returned in pinned host memory: the final code-stream D2H
 // lands in the caller's buffer directly (no staging copy; a C3 file is
-// ~340 MB) and jp2hip_free() hands the buffer back to a small pool, so steady
-// state allocates and pins nothing.  jp2hip_free() of a pointer the pool does
-// not know is plain free().
+// ~340 MB) and jp2hip_free() hands the buffer back to a pool, so steady state
+// allocates and pins nothing.  The pool keeps returned buffers up to one of
+// the largest per live context (at least 4 GiB): with a fixed 4 GiB, twelve
+// contexts of C3 files (385 MB buffers) overflowed it whenever most of their
+// files were returned at once, and the next encodes pinned fresh buffers --
+// hipHostMalloc / hipHostFree of that size took tens of ms and held up the
+// other contexts' launches meanwhile (a 19 ms window with no kernel on the
+// GPU, profiles/r06/c3_pinned_pool.txt).  jp2hip_free() of a pointer the
+// pool does not know is plain free().
 struct PinnedPool {
     std::mutex mu;
     std::unordered_map<void *, size_t> live;   // handed out: capacity
     std::multimap<size_t, void *> idle;        // returned: capacity -> buffer
     size_t idle_bytes = 0;
-    static constexpr size_t kIdleCap = (size_t)4 << 30;
+    size_t max_cap = 0;                        // the largest buffer pinned so far
+    static constexpr size_t kIdleFloor = (size_t)4 << 30;
+    size_t idle_cap() const {
+#ifdef JP2HIP_POOL_FIXED_CAP  // A/B: the fixed 4 GiB of rounds 2-5
+        return kIdleFloor;
+#endif
+        return std::max(kIdleFloor, (size_t)std::max(1, g_live_contexts.load()) * max_cap);
+    }
 };
 PinnedPool &pinned_pool() {
     static PinnedPool *p = new PinnedPool();  // never destroyed: buffers may be freed at exit
@@ -151,6 +167,7 @@ uint8_t *out_alloc(size_t n) {
     }
     std::lock_guard<std::mutex> lk(P.mu);
     P.live[b] = cap;
+    P.max_cap = std::max(P.max_cap, cap);
     return (uint8_t *)b;
 }
 
@@ -169,7 +186,8 @@ void out_free(void *p) {
         P.live.erase(it);
         P.idle.emplace(cap, p);
         P.idle_bytes += cap;
-        while (P.idle_bytes > PinnedPool::kIdleCap && !P.idle.empty()) {  // largest first
+        const size_t idle_cap = P.idle_cap();
+        while (P.idle_bytes > idle_cap && !P.idle.empty()) {  // largest first
             auto last = std::prev(P.idle.end());
             P.idle_bytes -= last->first;
             drop.push_back(last->second);
@@ -1230,9 +1248,6 @@ int jp2hip_device_count(void) { return jp2hip_device_ordinals(nullptr, 0); }
 void jp2hip_recipe_init(jp2hip_recipe *recipe, int conversion) {
     if (recipe) default_recipe(recipe, conversion);
 }
-
-// Contexts alive in this process, for jp2hip_env_check.
-static std::atomic<int> g_live_contexts{0};
 
 // Every context alive in the process, by device: an allocation that fails
 // for lack of device memory takes back the buffers of idle contexts of its
