@@ -951,7 +951,14 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
         os.makedirs(out_dir, exist_ok=True)
         with jb.BatchQueue(device=device, contexts=contexts, reader_threads=reader_threads,
                            uploader_threads=uploader_threads) as q:
-            for k, it in enumerate(items[:contexts]):  # warm-up: device buffers of every context
+            # warm-up: every context's device buffers, and the pinned host
+            # buffers of a full pipeline -- files read ahead, in the contexts,
+            # queued for and in the uploaders (pinning a 480 MB C3 buffer took
+            # 16-500 ms; without this the first rows of the timed region
+            # pinned them)
+            nwarm = 2 * contexts + reader_threads + uploader_threads
+            for k in range(nwarm):
+                it = items[k % len(items)]
                 q.submit(-1 - k, it.image_id, it.tiff, os.path.join(out_dir, "warm%d.jpx" % k), conv, rcp)
             q.drain()
             evict_from_page_cache(paths)

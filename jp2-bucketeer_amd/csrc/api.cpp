@@ -113,26 +113,30 @@ static std::atomic<int> g_live_contexts{0};
 // Encoded files are returned in pinned host memory: the final code-stream D2H
 // lands in the caller's buffer directly (no staging copy; a C3 file is
 // ~340 MB) and jp2hip_free() hands the buffer back to a pool, so steady state
-// allocates and pins nothing.  The pool keeps returned buffers up to one of
-// the largest per live context (at least 4 GiB): with a fixed 4 GiB, twelve
-// contexts of C3 files (385 MB buffers) overflowed it whenever most of their
-// files were returned at once, and the next encodes pinned fresh buffers --
+// allocates and pins nothing.  The pool keeps returned buffers up to the
+// most that were ever handed out at once, each counted at the largest size
+// pinned so far (at least 4 GiB): with a fixed 4 GiB, twelve contexts of C3
+// files (385 MB buffers) overflowed it whenever most of their files were
+// returned at once, and the next encodes pinned fresh buffers --
 // hipHostMalloc / hipHostFree of that size took tens of ms and held up the
 // other contexts' launches meanwhile (a 19 ms window with no kernel on the
-// GPU, profiles/r06/c3_pinned_pool.txt).  jp2hip_free() of a pointer the
-// pool does not know is plain free().
+// GPU, profiles/r06/c3_pinned_pool.txt); a batch queue holds more files than
+// contexts (its uploaders' queue), hence the high-water mark rather than the
+// context count.  jp2hip_free() of a pointer the pool does not know is plain
+// free().
 struct PinnedPool {
     std::mutex mu;
     std::unordered_map<void *, size_t> live;   // handed out: capacity
     std::multimap<size_t, void *> idle;        // returned: capacity -> buffer
     size_t idle_bytes = 0;
     size_t max_cap = 0;                        // the largest buffer pinned so far
+    size_t peak_live = 0;                      // the most buffers handed out at once
     static constexpr size_t kIdleFloor = (size_t)4 << 30;
     size_t idle_cap() const {
 #ifdef JP2HIP_POOL_FIXED_CAP  // A/B: the fixed 4 GiB of rounds 2-5
         return kIdleFloor;
 #endif
-        return std::max(kIdleFloor, (size_t)std::max(1, g_live_contexts.load()) * max_cap);
+        return std::max(kIdleFloor, peak_live * max_cap);
     }
 };
 PinnedPool &pinned_pool() {
@@ -149,6 +153,7 @@ uint8_t *out_alloc(size_t n) {
         if (it != P.idle.end() && it->first <= 2 * n + ((size_t)1 << 20)) {
             void *b = it->second;
             P.live[b] = it->first;
+            P.peak_live = std::max(P.peak_live, P.live.size());
             P.idle_bytes -= it->first;
             P.idle.erase(it);
             return (uint8_t *)b;
@@ -167,6 +172,7 @@ uint8_t *out_alloc(size_t n) {
     }
     std::lock_guard<std::mutex> lk(P.mu);
     P.live[b] = cap;
+    P.peak_live = std::max(P.peak_live, P.live.size());
     P.max_cap = std::max(P.max_cap, cap);
     return (uint8_t *)b;
 }
