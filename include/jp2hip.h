@@ -230,8 +230,11 @@ int jp2hip_encode_device(jp2hip_ctx *ctx, const void *d_src, size_t src_len,
                          const jp2hip_recipe *recipe, uint8_t **out, size_t *out_len,
                          jp2hip_stats *stats);
 
-/* Releases an *out buffer of the encode calls (returned to a small pool of
- * pinned buffers, so steady-state encodes pin nothing new). */
+/* Releases an *out buffer of the encode calls.  It returns to the process's
+ * pool of pinned buffers, so steady-state encodes pin nothing new; the pool
+ * keeps as many returned buffers as were ever handed out at once (each
+ * counted at the largest size pinned), at least 4 GiB, and unpins the
+ * largest beyond that. */
 void jp2hip_free(void *p);
 
 /* ------------------------------------------------------------------------
