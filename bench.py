@@ -199,6 +199,14 @@ def cpu_reference_opj(img):
         ok = all(p.wait() == 0 for p in ps)
         dt = time.perf_counter() - t0
         nbytes = os.path.getsize(os.path.join(d, "o0.j2k")) if ok else 0
+        # one process with every core gives the
+        # single-image latency (beside the GPU's config.single_image_latency_ms)
+        lat = None
+        if ok:
+            t0 = time.perf_counter()
+            if subprocess.run(cmd + ["-threads", str(cores), "-o", os.path.join(d, "lat.j2k")],
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL).returncode == 0:
+                lat = time.perf_counter() - t0
     if not ok:
         return None
     mp = cores * img.shape[0] * img.shape[1] / 1e6
@@ -206,7 +214,9 @@ def cpu_reference_opj(img):
             "tool": "opj_compress 2.4.0 (north_star's stand-in for the proprietary kdu_compress)",
             "cpu_model": model, "seconds": round(dt, 2), "bytes_per_image": nbytes,
             "sample": f"{cores} concurrent processes, each one full 6000x4000 RGB8 C2 image, lossy 3 bpp, "
-                      "Appendix A recipe"}
+                      "Appendix A recipe",
+            "single_image_latency_ms": round(lat * 1e3, 1) if lat else None,
+            "latency_sample": f"one process, -threads {cores}, the same image and recipe"}
 
 
 def cpu_reference_opj_lossless(crop_h=4096, crop_w=2048):
