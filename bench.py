@@ -533,9 +533,41 @@ def run(args):
             "t1": {"codeblocks": int(avg["codeblocks"]), "coded_passes": int(avg["coded_passes"]),
                    "mq_bytes": int(avg["t1_bytes"]), "mq_decisions": int(avg["mq_decisions"])},
         }
+    if rank == 0:
+        res["validation"] = validate_c2(encs[0], d_src, lay, rc, img, rank)
     for e in encs[1:]:  # their HBM and streams back before the lossless legs
         e.close()
     return res, img, world, rank, encs[0]
+
+
+def validate_c2(enc, d_src, lay, rc, img, rank):
+    """validation (decode and compare) is mandatory but not
+    timed.  One more encode of the bench image after the timed region: its
+    code-stream against the oracle's SHA-256 committed for this image
+    (tests/golden/golden.json c2_synth_rgb8_6000x4000, seed 1234 -- rank 0's
+    image), and its opj_decompress decode against the pixels (PSNR)."""
+    import hashlib
+
+    import jp2hip
+    import imaging as im
+    got, _ = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSY, rc)
+    cs = im.codestream(got)
+    sha = hashlib.sha256(cs).hexdigest()
+    out = {"codestream_bytes": len(cs), "codestream_sha256": sha, "equals_oracle_sha256": None, "psnr_db": None,
+           "oracle_psnr_db": None, "golden": "tests/golden/golden.json c2_synth_rgb8_6000x4000"}
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            g = [x for x in json.load(f)["lossy"] if x["name"] == "c2_synth_rgb8_6000x4000"][0]
+        if rank == 0:
+            out["equals_oracle_sha256"] = sha == g["oracle_sha256"]
+        out["oracle_psnr_db"] = g.get("oracle_psnr")
+    except (OSError, KeyError, IndexError, ValueError):
+        pass
+    try:
+        out["psnr_db"] = round(im.psnr(im.decode_opj(got), img, 8), 4)
+    except Exception as ex:  # the decoder is a check, not the product: record why it is absent
+        out["psnr_db"] = f"not decoded: {ex}"
+    return out
 
 
 C5 = {"w": 40000, "h": 30000, "levels": 7, "tile": 512, "rps": 64, "seed": 5}
