@@ -945,6 +945,19 @@ def lossless_c3(enc, steps=2, inflight=12, n_each=8):
                                   "note": "not the bound of a lossless encode: see roofline_pcie"}})
     for e in encs[1:]:
         e.close()
+    # SURVEY.md 8(d) validation, untimed: one more encode against the SHA-256
+    # of the oracle's file for this image (tests/golden/make_golden.py c3_full)
+    import hashlib
+    got, _ = enc.encode_device(d_src.data_ptr(), d_src.numel(), lay, jp2hip.LOSSLESS, rc)
+    val = {"bytes": len(got), "sha256": hashlib.sha256(got).hexdigest(), "equals_oracle_sha256": None,
+           "golden": "tests/golden/golden.json c3_full"}
+    del got
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            val["equals_oracle_sha256"] = val["sha256"] == json.load(f)["c3_full"]["oracle_sha256"]
+    except (OSError, KeyError, ValueError):
+        pass
+    res["validation"] = val
     return res
 
 

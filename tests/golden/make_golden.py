@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 import imaging as im  # noqa: E402
 
 # usage: make_golden.py            -- everything (about 15 minutes)
-#        make_golden.py NAME ...   -- only these lossy cases / "c5_full"
+#        make_golden.py NAME ...   -- only these lossy cases / "c5_full" / "c3_full"
 
 PREC = "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]"
 
@@ -68,6 +68,20 @@ def c5_full_sha(w=40000, h=30000):
             "oracle_sha256": hashlib.sha256(cs).hexdigest()}
 
 
+def c3_full_sha():
+    """SHA-256 of the oracle's file for the full C3 image (BASELINE.json
+    configs[2]: 10000x8000 RGB16, lossless 5/3, 1024^2 tiles, JPX; the bench
+    image, seed 2), so bench.py's lossless_c3 leg checks its output against
+    the oracle without running it on the GPU box."""
+    import hashlib
+    import oracle_lib as ol
+    img = im.synth_u16(8000, 10000, comps=3, seed=2)
+    cs = ol.encode(img, ol.recipe(True, tile_w=1024, tile_h=1024))
+    assert np.array_equal(im.decode_opj(cs), img)
+    return {"name": "c3_rgb16_10000x8000_lossless_jpx", "oracle_bytes": len(cs),
+            "oracle_sha256": hashlib.sha256(cs).hexdigest()}
+
+
 def c4_lossless():
     """Lossless at full C4 size (BASELINE.json configs[3]: one 5000x7000 RGB8
     batch image, seed 0, JPX as the batch writes it): the oracle file's
@@ -99,6 +113,9 @@ def main(only=None):
         if "c5_full" in only:
             g["c5_full"] = c5_full_sha()
             print(g["c5_full"])
+        if "c3_full" in only:
+            g["c3_full"] = c3_full_sha()
+            print(g["c3_full"])
         if "lossless" in only:
             g["lossless"] = c4_lossless()
             print(g["lossless"])
@@ -132,6 +149,7 @@ def main(only=None):
     g["lossless"] = c4_lossless()
     print(g["lossless"])
     g["c5_full"] = c5_full_sha()
+    g["c3_full"] = c3_full_sha()
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(g, f, indent=1)
     print(json.dumps(g["testjpx"], indent=1))

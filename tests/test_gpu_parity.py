@@ -185,11 +185,15 @@ def test_c2_full_size_jpx_on_rate(encoder, golden):
     assert st.host_waits <= 2, st.host_waits
 
 
-def test_c3_full_size_lossless_roundtrip(encoder):
-    """C3 at full size: 10000x8000 RGB16 lossless, 1024^2 tiles -> decode exact."""
+def test_c3_full_size_lossless_roundtrip(encoder, golden):
+    """C3 at full size: 10000x8000 RGB16 lossless, 1024^2 tiles -> decode
+    exact, and the file equals the oracle's (SHA-256 committed by
+    tests/golden/make_golden.py c3_full)."""
+    import hashlib
     img = im.synth_u16(8000, 10000, comps=3, seed=2)
     rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
     got, st = encoder.encode_tiff(im.tiff_bytes(img), jp2hip.LOSSLESS, rc)
+    assert hashlib.sha256(got).hexdigest() == golden["c3_full"]["oracle_sha256"]
     assert np.array_equal(im.decode_opj(got), img)
     assert st.host_waits <= 2, st.host_waits
 
