@@ -961,8 +961,26 @@ def lossless_c3(enc, steps=2, inflight=12, n_each=8):
     return res
 
 
+def golden_sha(which):
+    """The oracle's SHA-256 for a bench image from tests/golden/golden.json
+    (committed fixtures; None when absent): "c2" (its code-stream), "c3" and
+    "c4" (the whole file)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            g = json.load(f)
+        if which == "c2":
+            return [x for x in g["lossy"] if x["name"] == "c2_synth_rgb8_6000x4000"][0]["oracle_sha256"]
+        if which == "c3":
+            return g["c3_full"]["oracle_sha256"]
+        if which == "c4":
+            return [x for x in g["lossless"] if x["name"] == "c4_synth_rgb8_5000x7000_seed0_jpx"][0]["oracle_sha256"]
+    except (OSError, KeyError, IndexError, ValueError):
+        return None
+    return None
+
+
 def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=None, reader_threads=4,
-             uploader_threads=4, shape=(7000, 5000), gen_threads=8, rcp=None, busy=None):
+             uploader_threads=4, shape=(7000, 5000), gen_threads=8, rcp=None, busy=None, validate=None):
     """C4 (configs[3]) on one GPU: a Bucketeer batch CSV of `rows` synthetic
     5000x7000 RGB8 TIFFs (cycling over `ndistinct` files, as SURVEY.md 8(d)
     prescribes for the 10k-row batch) through the native batch queue: TIFF
@@ -973,7 +991,10 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
     re-read files the first pass left in the page cache.  `rcp`: the recipe
     of every row (None: the Bucketeer recipe of the conversion).  `busy`
     (a dict) receives the stages' busy fractions over the timed span: each
-    stage's summed per-image time / (its threads x span).  Returns (MP/s,
+    stage's summed per-image time / (its threads x span).  `validate` (a
+    dict with "golden": a golden_sha() name) receives, untimed, the SHA-256
+    of the first distinct file's JPX from one more pass through a queue that
+    keeps its output, and whether it equals the oracle's.  Returns (MP/s,
     seconds, results, bytes of TIFF read)."""
     import csv as _csv
     import shutil
@@ -1022,6 +1043,22 @@ def c4_batch(device, rows=16, ndistinct=2, contexts=8, conversion=None, make=Non
                 q.submit(it.job, it.image_id, it.tiff, os.path.join(out_dir, jb.jpx_name(it.image_id)), conv, rcp)
             res = q.drain()
             dt = time.perf_counter() - t0
+        if validate is not None:  # decode-and-compare, untimed
+            import hashlib
+            vout = os.path.join(out_dir, "validate.jpx")
+            with jb.BatchQueue(device=device, contexts=1, reader_threads=1, uploader_threads=1,
+                               delete_after_upload=False) as vq:
+                vq.submit(-1, "validate", paths[0], vout, conv, rcp)
+                vres = vq.drain()
+            sha = None
+            if vres and vres[0]["status"] == 0 and os.path.exists(vout):
+                with open(vout, "rb") as f:
+                    data = f.read()
+                sha = hashlib.sha256(im.codestream(data) if validate.get("golden") == "c2" else data).hexdigest()
+            want = golden_sha(validate.get("golden"))
+            validate.update({"file": "the first distinct file (row 0) through a one-context queue that keeps its "
+                                     "output", "sha256": sha,
+                             "equals_oracle_sha256": (sha == want) if (sha and want) else None})
         ok = sum(1 for r in res if r["status"] == 0)
         if busy is not None:
             busy.update({
@@ -1046,8 +1083,9 @@ def lossless_c4(device, rows=10000, ndistinct=16, sweep=(8, 12, 16), sweep_rows=
     # 6 readers / 8 uploaders: with 4 uploaders (the queue's default) the
     # upload stage -- JPX write, stub read-back, delete -- is the bound
     # (busy 0.95-1.0; profiles/r06/c4_sweep.jsonl), with 8 the contexts are
+    val = {"golden": "c4"}
     value, dt, res, read = c4_batch(device, rows=rows, ndistinct=ndistinct, contexts=12, busy=busy,
-                                    reader_threads=6, uploader_threads=8)
+                                    reader_threads=6, uploader_threads=8, validate=val)
     ok = [r for r in res if r["status"] == 0]
     peak_h2d = h2d_peak()
     sweep_res = []
@@ -1068,7 +1106,7 @@ def lossless_c4(device, rows=10000, ndistinct=16, sweep=(8, 12, 16), sweep_rows=
                           f"{ndistinct} re-read them from the page cache",
             "images_ok": len(ok), "mp_per_s": round(value, 3), "seconds": round(dt, 3),
             "bpp": round(bpp, 4), "timed_span": "first submit -> last upload, file I/O included",
-            "busy": busy,
+            "busy": busy, "validation": val,
             "roofline_pcie": {"bound": "pcie_h2d", "achieved": round(read / dt / 1e9, 2), "peak": round(peak_h2d, 2),
                               "unit": "GB/s", "frac": round(read / dt / 1e9 / peak_h2d, 4),
                               "def": "TIFF bytes read per second (every byte is uploaded) / measured pinned "
@@ -1090,14 +1128,15 @@ def c2_file_span(device, images=1024, contexts=16, ndistinct=16):
     roofline_pcie is that rate against the measured pinned H2D rate."""
     import imaging as im
     import jp2hip
+    val = {"golden": "c2"}
     value, dt, res, read = c4_batch(device, rows=images, ndistinct=ndistinct, contexts=contexts,
                                     conversion=jp2hip.LOSSY,
                                     make=lambda i: im.synth_rgb8(4000, 6000, seed=1234 + i), reader_threads=8,
-                                    uploader_threads=8, shape=(4000, 6000))
+                                    uploader_threads=8, shape=(4000, 6000), validate=val)
     ok = [r for r in res if r["status"] == 0]
     peak = h2d_peak()
     h2d = read / dt / 1e9
-    return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok),
+    return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok), "validation": val,
             "distinct_files": ndistinct,
             "page_cache": f"the {ndistinct} files are evicted before the timed region; images after the first "
                           f"{ndistinct} re-read them from the page cache",
@@ -1124,14 +1163,16 @@ def c3_file_span(device, images=64, contexts=8, ndistinct=4):
     import jp2hip
     busy = {}
     rc = jp2hip.recipe(jp2hip.LOSSLESS, tile_w=1024, tile_h=1024)
+    val = {"golden": "c3"}
     value, dt, res, read = c4_batch(device, rows=images, ndistinct=ndistinct, contexts=contexts,
                                     conversion=jp2hip.LOSSLESS, rcp=rc,
                                     make=lambda i: im.synth_u16(8000, 10000, comps=3, seed=2 + i), reader_threads=6,
-                                    uploader_threads=8, shape=(8000, 10000), gen_threads=4, busy=busy)
+                                    uploader_threads=8, shape=(8000, 10000), gen_threads=4, busy=busy,
+                                    validate=val)
     ok = [r for r in res if r["status"] == 0]
     out = sum(r["out_bytes"] for r in ok)
     ph, pd = h2d_peak(), d2h_peak()
-    return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok),
+    return {"value": round(value, 3), "unit": "MP/s", "images": images, "images_ok": len(ok), "validation": val,
             "distinct_files": ndistinct, "contexts": contexts,
             "page_cache": f"the {ndistinct} files are evicted before the timed region; images after the first "
                           f"{ndistinct} re-read them from the page cache",
