@@ -254,6 +254,40 @@ def cpu_reference_opj_lossless(crop_h=4096, crop_w=2048):
                       "(RGB16), lossless 5/3, C3 recipe (1024^2 tiles)"}
 
 
+def cpu_reference_opj_c4():
+    """SURVEY.md 8(d) item 3, the C4 CPU baseline: `nproc` concurrent
+    opj_compress processes, each one full 5000x7000 RGB8 C4 image (the seed-0
+    file, as SURVEY.md 8(d) item 2 runs `nproc` copies),
+    lossless 5/3 with the Bucketeer recipe (512^2 tiles, Appendix A) -- one
+    image per core of the 10k-row list (the list itself would take hours).
+    value = processes x 35 MP / wall time."""
+    import imaging as im
+    tool = im.opj("opj_compress")
+    if tool is None:
+        return None
+    cores, model = host_cpu()
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "c4.tif")
+        with open(src, "wb") as f:
+            f.write(im.tiff_bytes(im.synth_rgb8(7000, 5000, seed=0)))
+        srcs = [src] * cores
+        cmd = [tool, "-n", "7", "-t", "512,512", "-b", "64,64", "-p", "RPCL", "-SOP", "-EPH", "-PLT", "-TP", "R",
+               "-c", "[256,256],[256,256],[128,128],[128,128],[128,128],[128,128],[128,128]",
+               "-r", "64,32,16,8,4,1"]
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen(cmd + ["-i", srcs[i], "-o", os.path.join(d, f"o{i}.j2k")], stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL) for i in range(cores)]
+        ok = all(p.wait() == 0 for p in ps)
+        dt = time.perf_counter() - t0
+    if not ok:
+        return None
+    return {"value": round(cores * 35.0 / dt, 3), "unit": "MP/s", "cores": cores, "kind": "reference",
+            "tool": "opj_compress 2.4.0 (north_star's stand-in for the proprietary kdu_compress)",
+            "cpu_model": model, "seconds": round(dt, 2),
+            "sample": f"{cores} concurrent processes, each one full 5000x7000 RGB8 C4 image (the seed-0 file), "
+                      "lossless 5/3, Bucketeer recipe"}
+
+
 def d2h_peak(nbytes=256 << 20, reps=5):
     """Device -> pinned host copy rate (GB/s) on this box: the bound of a
     lossless encode, whose code-stream (~34 bpp for C3) must cross PCIe."""
@@ -846,6 +880,10 @@ def main():
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_reference_opj(img)
             res["cpu_baseline_lossless"] = cpu_reference_opj_lossless()
+            res["cpu_baseline_c4"] = cpu_reference_opj_c4()
+            if res.get("lossless_c4") and res["cpu_baseline_c4"]:
+                res["lossless_c4"]["vs_cpu_baseline_c4"] = round(
+                    res["lossless_c4"]["mp_per_s"] / res["cpu_baseline_c4"]["value"], 2)
             if res.get("lossless_c3") and res["cpu_baseline_lossless"]:
                 res["lossless_c3"]["vs_cpu_baseline_lossless"] = round(
                     res["lossless_c3"]["mp_per_s_inflight_c_api"] / res["cpu_baseline_lossless"]["value"], 2)
