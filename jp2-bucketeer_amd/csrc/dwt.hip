@@ -688,8 +688,30 @@ static_assert(kL1sPf >= 1 && kL1sPf <= 3, "JP2HIP_L1S_PF: 1..3");
 // (101 VGPRs, 4 waves per SIMD for the C2 variant; a budget for 5 --
 // amdgpu_waves_per_eu(5), 5 VGPRs spilled -- measured no faster: 146.7 vs
 // 146.4 us, profiles/r05/ab_select_fold.txt)
+#ifndef JP2HIP_L1S_CENSUS
+#define JP2HIP_L1S_CENSUS 0  // debug builds: shader cycles per phase of the row pipeline (output to stderr)
+#endif
+#if JP2HIP_L1S_CENSUS
+__device__ unsigned long long g_l1s_census[8];  // phases 0..6, then waves
+#define L1S_TICK(k)                                        \
+    do {                                                   \
+        __builtin_amdgcn_sched_barrier(0);                 \
+        const uint64_t t_ = __builtin_readcyclecounter();  \
+        cz[k] += t_ - tc;                                  \
+        tc = t_;                                           \
+        __builtin_amdgcn_sched_barrier(0);                 \
+    } while (0)
+#else
+#define L1S_TICK(k) \
+    do {            \
+    } while (0)
+#endif
 template <bool REV, int NC, int CPT, int RB, bool ALIGNED>
 __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
+#if JP2HIP_L1S_CENSUS
+    uint64_t cz[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t tc = __builtin_readcyclecounter();
+#endif
     extern __shared__ int32_t lds[];
     constexpr int NS = REV ? 2 : 4;  // lifting steps
     constexpr int NWIN = NS + 2;     // rows m-NS-1 .. m
@@ -807,10 +829,13 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
             for (int c = 0; c < NC; c++)
 #pragma unroll
                 for (int i = 0; i + 2 < NWIN; i++) w[j][c][i] = w[j][c][i + 2];
+        L1S_TICK(6);
         if (m - 1 >= s && m - 1 < e) place(SA, NWIN - 2);
         if (m < e) place(SB, NWIN - 1);
+        L1S_TICK(0);
         if (m + 2 * kL1sPf - 1 < e) fetch(SA);
         if (m + 2 * kL1sPf < e) fetch(SB);
+        L1S_TICK(1);
         // interior iterations (every step's rows and neighbours inside the
         // streamed rows and the signal, none at row 0): fixed neighbour slots,
         // no per-value selects -- the same expressions in the same order
@@ -865,6 +890,7 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
                     }
             }
         }
+        L1S_TICK(2);
         // rows m-NS (even) and m-NS+1 (odd) are final: scale, stage in LDS
 #pragma unroll
         for (int q = 0; q < 2; q++) {
@@ -883,8 +909,10 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
             }
         }
         const int ylast = m - NS + 1;
+        L1S_TICK(3);
         if (ylast >= r0 && (ylast - bb == RB - 1 || ylast >= r1 - 1)) {
             __syncthreads();
+            L1S_TICK(4);
             const int nkeep = min(RB, r1 - bb);
             hlift_seg<REV, NC * RB, ALIGNED, kDwtThreads, kL1sSkew>(lds, W, ld, q16, [&](int r, QRow &o) -> bool {
                 const int c = r / RB, k = r - c * RB;
@@ -897,7 +925,9 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
                 qrow_bands(o, ql, !ylo);
                 return true;
             });
+            L1S_TICK(5);
             __syncthreads();
+            L1S_TICK(4);
             bb += RB;
         }
     };
@@ -906,6 +936,12 @@ __global__ void __launch_bounds__(kDwtThreads) k_dwt_l1s(DwtBandArgs a) {
         else if (kL1sPf >= 2 && (((m - s) >> 1) % kL1sPf) == 1) body(m, std::integral_constant<int, (kL1sPf >= 2 ? 2 : 0)>{});
         else if (kL1sPf >= 3 && (((m - s) >> 1) % kL1sPf) == 2) body(m, std::integral_constant<int, (kL1sPf >= 3 ? 4 : 0)>{});
     }
+#if JP2HIP_L1S_CENSUS
+    if ((tid & 63) == 0) {  // per wave: vector atomics on a global word
+        for (int k = 0; k < 7; k++) atomicAdd(&g_l1s_census[k], (unsigned long long)cz[k]);
+        atomicAdd(&g_l1s_census[7], 1ull);
+    }
+#endif
 }
 
 struct DwtTailArgs {
@@ -1070,6 +1106,18 @@ static void launch_l1s_rb(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs 
     }
     hipLaunchKernelGGL((k_dwt_l1s<REV, NC, CPT, RB, true>), g, dim3(kDwtThreads), lds, st, a);
     if (a.ragged) hipLaunchKernelGGL((k_dwt_l1s<REV, NC, CPT, RB, false>), g, dim3(kDwtThreads), lds, st, a);
+#if JP2HIP_L1S_CENSUS
+    unsigned long long h[8];
+    if (hipStreamSynchronize(st) == hipSuccess &&
+        hipMemcpyFromSymbol(h, HIP_SYMBOL(g_l1s_census), sizeof h) == hipSuccess && h[7]) {
+        fprintf(stderr, "l1s census: waves %llu, cycles per wave: place %.0f fetch %.0f vlift %.0f stage %.0f "
+                        "barriers %.0f hlift %.0f loop %.0f\n", h[7], (double)h[0] / h[7], (double)h[1] / h[7],
+                (double)h[2] / h[7], (double)h[3] / h[7], (double)h[4] / h[7], (double)h[5] / h[7],
+                (double)h[6] / h[7]);
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_l1s_census), z, sizeof z);
+    }
+#endif
 }
 template <bool REV, int NC, int CPT>
 static void launch_l1s_c(dim3 g, size_t lds, hipStream_t st, const DwtBandArgs &a) {
